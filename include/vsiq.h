@@ -1,0 +1,172 @@
+/*
+ * vsiq.h — C ABI of the MI355X (gfx950) fake-quantization kernels.
+ *
+ * The drop-in boundary of this repository: every entry point below replaces
+ * one link of VSIQuantization's eager-PyTorch fake-quant chain (reference
+ * tranngocduvnvp/VSIQuantization, file:line cited per function).  The
+ * reference's own plugin API is Python (CLASS_REGISTRY names, utils/registry.py:
+ * 2-27); its Python classes are re-implemented in vsiquantization_amd/ and call
+ * these functions through ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - All tensor pointers are DEVICE pointers (hipMalloc / torch caching
+ *     allocator).  The library never allocates, frees or synchronises.
+ *   - `stream` is a hipStream_t passed as void*; NULL = the null stream.
+ *   - Return value: 0 on success, a hipError_t (>0) from the launch, or a
+ *     negative VSIQ_E* code for invalid arguments (nothing is launched then).
+ *   - fp32 element arithmetic is IEEE (true division, rint half-to-even,
+ *     NaN-propagating clamp, denormals kept): bit-identical to the reference's
+ *     PyTorch CPU path.  Quantization parameters are computed in float64 on
+ *     the device exactly as the reference does on the host in Python floats.
+ *   - Workspaces: `ws` is a float64 device buffer of at least
+ *     vsiq_workspace_doubles(n) entries and `counter` one uint32 device word
+ *     that is 0 before the first call; every reducing kernel resets it to 0
+ *     when it finishes (stream-ordered reuse is safe, concurrent reuse on two
+ *     streams is not).
+ *   - Masks are uint8 (1 = value was inside [qmin, qmax] after rounding,
+ *     ClampBackward1 semantics), codes are int8 (symmetric) or uint8
+ *     (asymmetric) holding clamp(round(x/s+zp)); NaN inputs give code 0.
+ */
+#ifndef VSIQ_H_
+#define VSIQ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSIQ_ABI_VERSION 1
+
+#define VSIQ_E_ARG (-1)      /* invalid argument (null pointer, bad size, qmin>qmax) */
+#define VSIQ_E_ALIGN (-2)    /* misaligned pointer where alignment is required */
+#define VSIQ_E_WS (-3)       /* workspace too small */
+
+/* stats record written by vsiq_observe_f32 (float64 entries) */
+#define VSIQ_ST_MIN 0        /* min of this call's non-NaN x (as f64), +inf if none */
+#define VSIQ_ST_MAX 1        /* max of this call's non-NaN x, -inf if none */
+#define VSIQ_ST_NAN 2        /* count of NaN elements */
+#define VSIQ_ST_SUMABS 3     /* sum |x| (f64 accumulation) */
+#define VSIQ_ST_SUM 4        /* sum x */
+#define VSIQ_ST_SUMSQ 5      /* sum x^2 */
+#define VSIQ_ST_N 6          /* element count */
+#define VSIQ_ST_MEANABS 7    /* fp32-rounded mean(|x|)        (qm.py:66) */
+#define VSIQ_ST_MEAN 8       /* fp32-rounded mean(x)          (qm.py:67) */
+#define VSIQ_ST_STD 9        /* fp32-rounded unbiased std(x)  (qm.py:68) */
+#define VSIQ_ST_LEN 10
+
+/* qparams record (float64 entries) */
+#define VSIQ_QP_SCALE 0      /* scale, Python-float semantics          (minmax.py:70-75) */
+#define VSIQ_QP_ZP 1         /* zero point as an integer-valued f64; NaN if Python round() would raise */
+#define VSIQ_QP_MIN 2        /* running min_val after this call        (minmax.py:44-45) */
+#define VSIQ_QP_MAX 3        /* running max_val after this call        (minmax.py:46-47) */
+#define VSIQ_QP_LEN 4
+
+int vsiq_abi_version(void);
+const char *vsiq_error_string(int code);
+
+/* float64 workspace entries needed by the reducing kernels for n elements */
+int64_t vsiq_workspace_doubles(int64_t n);
+
+/*
+ * Per-tensor fake-quant forward (K1).
+ * Replaces quantizers/uniform.py:54-55 + :95 (discreate_tensor):
+ *   y = (clamp(rint(x/s + zp), qmin, qmax) - zp) * s      (fp32)
+ * s = fp32(scale), zp = fp32(zero_point), taken from
+ *   - qp_dev[VSIQ_QP_SCALE], qp_dev[VSIQ_QP_ZP]   if qp_dev != NULL (observer output), else
+ *   - *scale_dev (f64, a learnable 0-dim Parameter) if scale_dev != NULL, else scale_host;
+ *   - *zp_dev (f64) if zp_dev != NULL, else zp_host; zp_round != 0 applies
+ *     clamp(rint(zp), qmin, qmax) first (learnable tensor zp, uniform.py:98-102).
+ * codes (int8/uint8, nullable) and mask (uint8, nullable) are optional outputs.
+ * discrete != 0 writes the integer-valued fp32 clamp(round(x/s+zp)) into y instead
+ * (UniformQuantizer.discreate_tensor, uniform.py:81-96).
+ */
+int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint8_t *mask, int64_t n,
+                    const double *qp_dev, const double *scale_dev, double scale_host,
+                    const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
+                    int qmax, void *stream);
+
+/*
+ * Per-tensor observer (K2).
+ * Replaces observers/minmax.py:32-88 (observe + get_scale_zero_point, the two
+ * `.item()` reductions) and quantizers/quantization_manager.py:66-68 (the
+ * mean(|x|)/mean/std statistics) with ONE pass over x and an on-device float64
+ * epilogue (last workgroup to finish).
+ *   stats_out[VSIQ_ST_LEN]   this call's statistics (nullable)
+ *   run_minmax[2]            running (min_val, max_val) fp32 state, in/out (nullable: fresh 0/0)
+ *   qp_out[VSIQ_QP_LEN]      qparams from the updated running state (nullable)
+ *   qden = 2**(b-1)-1+eps (symmetric) or 2**b-1+eps (asymmetric), computed by the caller in
+ *   Python float64 exactly as minmax.py:72/75 writes it.
+ */
+int vsiq_observe_f32(const float *x, int64_t n, double *stats_out, float *run_minmax,
+                     double *qp_out, int symmetric, double qden, double eps,
+                     double *ws, int64_t ws_len, uint32_t *counter, void *stream);
+
+/*
+ * Observer epilogue alone, from a stats record that was reduced elsewhere (the
+ * multi-GPU observer: per-rank vsiq_observe_f32 with run_minmax = qp_out = NULL,
+ * RCCL all-reduce MAX over [-min, max] and SUM over the counts/sums, then this).
+ * Applies the minmax.py:42-47 running update (NaN count > 0 -> unchanged) and
+ * writes qp_out.  One lane, stream-ordered.
+ */
+int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out, int symmetric,
+                          double qden, double eps, void *stream);
+
+/*
+ * Per-channel fused observe + qparams + fake-quant forward (K3), axis 0 of a
+ * row-major [rows, rowlen] view (OIHW weight: rows = O, rowlen = I*H*W).
+ * Build-defined per-channel MinMax: row c is processed as
+ *   s_c, z_c = MinMaxObserver(sym).forward(W[c])          (minmax.py:76-88)
+ *   Y[c]     = UniformQuantizer(b, sym).quantize(W[c], s_c, z_c, False)  (uniform.py:34-56)
+ * run_min/run_max [rows] fp32 running state, in/out (zeros = fresh observers).
+ * scale_out/zp_out [rows] f64 (zp NaN where Python round() would raise).
+ * row_stats [rows][3] f64 (nullable): sum|x|, sum x, sum x^2 of each row, for the
+ * manager's mean(|x|)/mean/std records (quantization_manager.py:66-68).
+ * y == NULL observes only (codes/mask must then be NULL too).
+ * One read and one write of every element.
+ */
+int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint8_t *mask,
+                           int64_t rows, int64_t rowlen, float *run_min, float *run_max,
+                           double *scale_out, double *zp_out, double *row_stats, int symmetric,
+                           int qmin, int qmax, double qden, double eps, void *stream);
+
+/*
+ * Per-channel fake-quant forward with given per-row qparams (f64 [rows]).
+ * zp_round != 0 applies clamp(rint(zp)) first (learnable zp, uniform.py:98-102).
+ */
+int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint8_t *mask, int64_t rows,
+                       int64_t rowlen, const double *scale, const double *zp, int zp_round,
+                       int qmin, int qmax, void *stream);
+
+/*
+ * Straight-through backward for fixed (non-learnable) qparams, from the saved mask.
+ * Replaces the autograd chain MulBackward0 -> ClampBackward1 -> STE -> DivBackward0 of
+ * uniform.py:55,95 with a Python-float scale:
+ *   gx = (mask ? g*s : 0) / s      (fp32, bit-exact)
+ * s = fp32(scale_dev[i / rowlen]) if scale_dev != NULL (rowlen elements per entry), else
+ * fp32(scale_host).
+ */
+int vsiq_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t n,
+                     const double *scale_dev, int64_t rowlen, double scale_host, void *stream);
+
+/*
+ * Learnable (LSQ) backward (K4): grad_x plus the scale / zero-point gradients.
+ * Replaces autograd over uniform.py:47-56 (ScaleGradient, RoundStraightThrough,
+ * clamp, div, mul; uniform.py:242-271):
+ *   gx        = (mask ? g*s : 0) / s
+ *   grad_s    = gscale * [ sum g*(q-zp) + sum (-(mask?g*s:0)) * ((x/s)/s) ]
+ *   grad_zp   = gscale * [ sum (mask?g*s:0) + sum -(g*s) ] * zp_in_range      (zp_learn)
+ * sums of fp32 terms accumulated in float64, fixed reduction order (deterministic).
+ * grad_out[0] = grad_s, grad_out[1] = grad_zp (device f64, overwritten).
+ */
+int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
+                     const double *scale_dev, double scale_host, const double *zp_dev,
+                     double zp_host, int zp_learn, int qmin, int qmax, double gscale,
+                     double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+                     void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSIQ_H_ */

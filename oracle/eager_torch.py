@@ -1,0 +1,72 @@
+"""The reference's eager-PyTorch op sequence, restated (TEST INFRASTRUCTURE / CPU BASELINE).
+
+Used only by bench.py's ``cpu_baseline`` leg and by tests: it is what the
+reference costs on the host, op for op:
+  observers/minmax.py:42-47       x.min().item(), x.max().item()
+  observers/minmax.py:49-74       Python float64 qparams
+  quantizers/uniform.py:95        clamp(RoundSTE(x / s + zp), qmin, qmax)
+  quantizers/uniform.py:55        (x_int - zp) * s
+  quantizers/uniform.py:258-271   round with a straight-through gradient
+"""
+import torch
+
+from .fakequant_np import minmax_qparams, qrange
+
+
+class _RoundSTE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return torch.round(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def observe(x, min_val=0, max_val=0):
+    mn = x.min().item()
+    mx = x.max().item()
+    if mn < min_val:
+        min_val = mn
+    if mx > max_val:
+        max_val = mx
+    return min_val, max_val
+
+
+def fake_quant(x, scale, zero_point, qmin, qmax):
+    x_int = torch.clamp(_RoundSTE.apply(x / scale + zero_point), qmin, qmax)
+    return (x_int - zero_point) * scale
+
+
+def per_channel_step(w, g, symmetric=False, bits=8):
+    """Per-channel observe + fake-quant forward, then STE backward (reference classes looped)."""
+    qmin, qmax = qrange(bits, symmetric)
+    w = w.detach().requires_grad_(True)
+    ys = []
+    for c in range(w.shape[0]):
+        mn, mx = observe(w[c].detach())
+        s, z = minmax_qparams(mn, mx, symmetric, 8)
+        ys.append(fake_quant(w[c], s, z, qmin, qmax))
+    torch.stack(ys).backward(g)
+    return w.grad
+
+
+def lsq_step(x, g, scale=0.03, bits=8):
+    """Learnable symmetric fake-quant fwd + bwd (uniform.py:47-56 with ScaleGradient)."""
+    qmin, qmax = qrange(bits, True)
+    s = torch.nn.Parameter(torch.tensor(scale, dtype=torch.float64))
+    gscale = (qmax * x.numel()) ** -0.5
+    x = x.detach().requires_grad_(True)
+
+    class _ScaleGrad(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, v):
+            return v
+
+        @staticmethod
+        def backward(ctx, gv):
+            return gv * gscale
+
+    y = fake_quant(x, _ScaleGrad.apply(s), 0, qmin, qmax)
+    y.backward(g)
+    return x.grad, s.grad

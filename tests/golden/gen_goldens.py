@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""Generate golden input/output vectors by running the REFERENCE's own CPU path.
+
+This script is the only place that imports the reference implementation
+(`/root/reference`, tranngocduvnvp/VSIQuantization @ 2025-08-08, PyTorch
+2.10.0+rocm7.0 on CPU).  It runs in the build container only; the fixtures it
+writes (`tests/golden/*.npz` + `cases.json`) are plain numeric data and travel
+to the GPU box, the reference does not.
+
+Reference call sites exercised (file:line under /root/reference):
+  * observers/minmax.py:32-88          MinMaxObserver.observe / get_scale_zero_point / forward
+  * quantizers/uniform.py:34-56        UniformQuantizer.quantize (fixed + learnable)
+  * quantizers/uniform.py:81-96        discreate_tensor (the integer codes)
+  * quantizers/uniform.py:242-271      ScaleGradient / RoundStraightThrough (autograd)
+  * quantizers/quantization_manager.py:55-114  collect / quantize / learn-init sequence
+  * modules/fused.py:32-134 + modules/fuse.py:45-149  (toy fused model, host structure)
+
+Per-channel has no reference class: it is defined as the
+reference classes applied independently to each out-channel slice W[c].
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_goldens.py
+"""
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+REF = os.environ.get("VSIQ_REFERENCE", "/root/reference")
+sys.path.insert(0, REF)
+# modules/fused.py:2-3 has dead imports of tkinter/turtle (absent here).
+for _m, _attr in (("tkinter", "W"), ("turtle", "forward")):
+    if _m not in sys.modules:
+        _mod = types.ModuleType(_m)
+        setattr(_mod, _attr, None)
+        sys.modules[_m] = _mod
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from observers.minmax import MinMaxObserver  # noqa: E402
+from quantizers.uniform import UniformQuantizer  # noqa: E402
+from quantizers.quantization_manager import QuantizationManager  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+arrays = {}
+cases = []
+
+
+def put(key, t):
+    a = t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+    arrays[key] = np.ascontiguousarray(a)
+    return key
+
+
+def special_vector(n_rand, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n_rand, generator=g) * scale
+
+
+# ---------------------------------------------------------------------------
+# 1. Per-tensor observe + fake-quant (the §3.4 "observer + quantize" pair)
+#    MinMaxObserver(sym, num_bits=obs_bits).forward(x) -> (s, zp);
+#    UniformQuantizer(bits, sym).quantize(x, s, zp, False); backward with g.
+# ---------------------------------------------------------------------------
+def per_tensor_inputs():
+    ins = {}
+    g = torch.Generator().manual_seed(0)
+    ins["randn"] = torch.randn(2, 3, 5, 7, generator=g)
+    ins["pos"] = torch.rand(4, 33, generator=g) * 3.0 + 0.5
+    ins["neg"] = -(torch.rand(4, 33, generator=g) * 2.0 + 0.25)
+    ins["zeros"] = torch.zeros(3, 17)
+    t = torch.randn(257, generator=g)
+    t[5] = float("nan")
+    ins["nan"] = t
+    t = torch.randn(130, generator=g)
+    t[7] = float("inf")
+    ins["posinf"] = t
+    t = torch.randn(130, generator=g)
+    t[9] = float("-inf")
+    ins["neginf"] = t
+    t = torch.randn(1000, generator=g) * 0.05
+    t[0] = -0.0
+    t[1] = 0.0
+    t[2] = 1e-40   # denormal
+    t[3] = -1e-40
+    ins["mixed"] = t
+    return ins
+
+
+def run_observe_fq(x, sym, bits, obs_bits):
+    obs = MinMaxObserver(sym, obs_bits)
+    rec = {}
+    try:
+        s, zp = obs.forward(x)
+    except Exception as e:  # reference raises on non-finite zp (python round)
+        rec["raises"] = type(e).__name__
+        rec["min_val"] = float(obs.min_val)
+        rec["max_val"] = float(obs.max_val)
+        return rec, None
+    rec.update(min_val=float(obs.min_val), max_val=float(obs.max_val),
+               scale=float(s), zp=int(zp))
+    q = UniformQuantizer(bits, sym)
+    xr = x.clone().requires_grad_(True)
+    y = q.quantize(xr, s, zp, False)
+    x_int = q.discreate_tensor(x, s, zp, q.qmin, q.qmax)
+    gg = torch.randn(x.shape, generator=torch.Generator().manual_seed(1234))
+    y.backward(gg)
+    return rec, (y.detach(), x_int, gg, xr.grad.detach())
+
+
+idx = 0
+for name, x in per_tensor_inputs().items():
+    for sym in (True, False):
+        for bits in (2, 4, 8):
+            for obs_bits in ({8, bits} if bits != 8 else {8}):
+                rec, outs = run_observe_fq(x, sym, bits, obs_bits)
+                key = f"pt{idx}"
+                idx += 1
+                rec.update(kind="per_tensor_observe_fq", key=key, input=name,
+                           sym=sym, bits=bits, obs_bits=obs_bits,
+                           x=put(key + "_x", x))
+                if outs is not None:
+                    y, x_int, gg, gx = outs
+                    rec.update(y=put(key + "_y", y), x_int=put(key + "_xint", x_int),
+                               g=put(key + "_g", gg), grad_x=put(key + "_gx", gx))
+                cases.append(rec)
+
+# ---------------------------------------------------------------------------
+# 2. Fixed-qparam fake-quant with hand-picked scale/zp (ties, clamp edges).
+# ---------------------------------------------------------------------------
+fixed_idx = 0
+for sym in (True, False):
+    for bits in (2, 4, 8):
+        q = UniformQuantizer(bits, sym)
+        for s in (0.25, 0.1, 1.0e-3, 3.0517578125e-05):
+            for zp in ((0, 1) if sym else (0, 3, (q.qmax + 1) // 2)):
+                ks = torch.arange(q.qmin - 3, q.qmax + 4, dtype=torch.float64)
+                # exact ties (k+0.5)*s, integers and neighbours, in units of s
+                grid = torch.cat([ks, ks + 0.5, ks - 0.5, ks + 0.49999, ks + 0.50001])
+                x = ((grid - zp) * s).float()
+                g = torch.Generator().manual_seed(99)
+                x = torch.cat([x, torch.randn(200, generator=g) * s * (q.qmax - q.qmin) / 3,
+                               torch.tensor([float("nan"), float("inf"), -float("inf"), 0.0, -0.0])])
+                xr = x.clone().requires_grad_(True)
+                y = q.quantize(xr, s, zp, False)
+                x_int = q.discreate_tensor(x, s, zp, q.qmin, q.qmax)
+                gg = torch.randn(x.shape, generator=torch.Generator().manual_seed(7))
+                y.backward(gg)
+                key = f"fx{fixed_idx}"
+                fixed_idx += 1
+                cases.append(dict(kind="fixed_fq", key=key, sym=sym, bits=bits, scale=s, zp=zp,
+                                  x=put(key + "_x", x), y=put(key + "_y", y),
+                                  x_int=put(key + "_xint", x_int), g=put(key + "_g", gg),
+                                  grad_x=put(key + "_gx", xr.grad)))
+
+# ---------------------------------------------------------------------------
+# 3. Per-channel (axis 0 of OIHW): reference classes looped over out-channels.
+# ---------------------------------------------------------------------------
+def per_channel_weight(seed, special):
+    g = torch.Generator().manual_seed(seed)
+    w = torch.randn(8, 4, 3, 3, generator=g) * 0.05
+    if special:
+        w[1] = w[1].abs() + 0.01         # all positive
+        w[2] = -(w[2].abs() + 0.01)      # all negative
+        w[3] = 0.0                        # all zero -> scale 0
+        w[4, 0, 1, 1] = float("nan")     # NaN row: observer skips the call
+        w[5, 1, 0, 2] = float("inf")     # +inf
+    return w
+
+
+pc_idx = 0
+for special in (False, True):
+    for sym in (True, False):
+        for bits in (2, 4, 8):
+            w = per_channel_weight(11 + pc_idx, special)
+            if special and sym:
+                w[6, 2, 2, 2] = -float("inf")  # -inf only for sym (asym raises in round())
+            q = UniformQuantizer(bits, sym)
+            gg = torch.randn(w.shape, generator=torch.Generator().manual_seed(5))
+            ys, xis, gxs, scales, zps, mins, maxs = [], [], [], [], [], [], []
+            for c in range(w.shape[0]):
+                obs = MinMaxObserver(sym)  # fresh observer per channel per call, num_bits=8
+                s, zp = obs.forward(w[c])
+                xr = w[c].clone().requires_grad_(True)
+                y = q.quantize(xr, s, zp, False)
+                y.backward(gg[c])
+                ys.append(y.detach())
+                xis.append(q.discreate_tensor(w[c], s, zp, q.qmin, q.qmax))
+                gxs.append(xr.grad.detach())
+                scales.append(float(s))
+                zps.append(int(zp))
+                mins.append(float(obs.min_val))
+                maxs.append(float(obs.max_val))
+            key = f"pc{pc_idx}"
+            pc_idx += 1
+            cases.append(dict(kind="per_channel_observe_fq", key=key, sym=sym, bits=bits, obs_bits=8,
+                              special=special, x=put(key + "_x", w), y=put(key + "_y", torch.stack(ys)),
+                              x_int=put(key + "_xint", torch.stack(xis)), g=put(key + "_g", gg),
+                              grad_x=put(key + "_gx", torch.stack(gxs)),
+                              scale=put(key + "_scale", torch.tensor(scales, dtype=torch.float64)),
+                              zp=put(key + "_zp", torch.tensor(zps, dtype=torch.int64)),
+                              min_val=put(key + "_min", torch.tensor(mins, dtype=torch.float64)),
+                              max_val=put(key + "_max", torch.tensor(maxs, dtype=torch.float64))))
+
+# ---------------------------------------------------------------------------
+# 4. Learnable (LSQ) path: quantize(x, Parameter f64 scale, zp, True) fwd + bwd.
+# ---------------------------------------------------------------------------
+lsq_idx = 0
+for shape, seed in (((3, 4, 8, 8), 21), ((16, 3, 16, 16), 22)):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(shape, generator=g)
+    gg = torch.randn(shape, generator=torch.Generator().manual_seed(seed + 100))
+    for sym in (True, False):
+        for bits in ((2, 4, 8) if x.numel() < 5000 else (8,)):
+            q = UniformQuantizer(bits, sym)
+            scale = torch.nn.Parameter(torch.tensor(np.float64(0.03 if bits == 8 else 0.3)))
+            xr = x.clone().requires_grad_(True)
+            if sym:
+                zp = 0
+                y = q.quantize(xr, scale, zp, True)
+            else:
+                zp = torch.nn.Parameter(torch.tensor(np.float64(3.0 if bits > 2 else 1.0) + 1e-9))
+                y = q.quantize(xr, scale, zp, True)
+            y.backward(gg)
+            key = f"lsq{lsq_idx}"
+            lsq_idx += 1
+            rec = dict(kind="learnable_fq", key=key, sym=sym, bits=bits,
+                       scale=float(scale.detach()), scale_grad=float(scale.grad),
+                       x=put(key + "_x", x), g=put(key + "_g", gg),
+                       y=put(key + "_y", y), grad_x=put(key + "_gx", xr.grad))
+            if not sym:
+                rec.update(zp=float(zp.detach()), zp_grad=float(zp.grad))
+            else:
+                rec.update(zp=0)
+            cases.append(rec)
+
+# asym + learnable through the manager crashes in the reference (int zp -> torch.round(int)):
+try:
+    q = UniformQuantizer(8, False)
+    q.quantize(torch.randn(10), torch.nn.Parameter(torch.tensor(0.1, dtype=torch.float64)), 0, True)
+    crash = None
+except Exception as e:  # TypeError
+    crash = type(e).__name__
+cases.append(dict(kind="asym_learnable_int_zp", raises=crash))
+
+# ---------------------------------------------------------------------------
+# 5. QuantizationManager sequence: calibrate (observe only) -> learn-init -> learnable fwd/bwd
+# ---------------------------------------------------------------------------
+mg_idx = 0
+for bits, sym in ((4, True), (2, True), (8, False)):
+    qm = QuantizationManager("UniformQuantizer", "MinMaxObserver", bits, sym, is_learning_scale=True)
+    qm.is_observer_qparam, qm.is_learning_scale, qm.is_quantize = True, False, False
+    g = torch.Generator().manual_seed(300 + mg_idx)
+    xs = [torch.randn(4, 6, 5, 5, generator=g) * (0.5 + i) for i in range(3)]
+    outs = [qm.quantize(x) for x in xs]
+    identity_ok = all(torch.equal(o, x) for o, x in zip(outs, xs))
+    calib = dict(min_val=float(qm.observer.min_val), max_val=float(qm.observer.max_val),
+                 scale=float(qm.scale), zero_point=int(qm.zero_point),
+                 mean_abs_x=list(map(float, qm.mean_abs_x)), mean_x=list(map(float, qm.mean_x)),
+                 std=list(map(float, qm.std)))
+    # observe + quantize in the same call
+    qm.is_quantize = True
+    x_oq = torch.randn(4, 6, 5, 5, generator=g)
+    y_oq = qm.quantize(x_oq)
+    oq = dict(scale=float(qm.scale), zero_point=int(qm.zero_point))
+    # learn init + learnable step
+    qm.is_learning_scale = True
+    qm.init_scaling_factor_for_learning()
+    init_scale = float(qm.scale)
+    qm.make_learn_qparameter()
+    key = f"mg{mg_idx}"
+    mg_idx += 1
+    x4 = torch.randn(4, 6, 5, 5, generator=g)
+    gg = torch.randn(4, 6, 5, 5, generator=g)
+    rec = dict(kind="manager_sequence", key=key, bits=bits, sym=sym, identity_ok=identity_ok,
+               calib=calib, observe_quantize=oq, init_scale=init_scale,
+               xs=[put(f"{key}_x{i}", x) for i, x in enumerate(xs)],
+               x_oq=put(key + "_xoq", x_oq), y_oq=put(key + "_yoq", y_oq))
+    try:
+        xr = x4.clone().requires_grad_(True)
+        y4 = qm.quantize(xr)
+        y4.backward(gg)
+        rec.update(x4=put(key + "_x4", x4), g4=put(key + "_g4", gg), y4=put(key + "_y4", y4),
+                   gx4=put(key + "_gx4", xr.grad), scale_grad=float(qm.scale.grad),
+                   scale_param_dtype=str(qm.scale.dtype))
+    except Exception as e:
+        rec.update(learn_raises=type(e).__name__)
+    cases.append(rec)
+
+np.savez_compressed(os.path.join(OUT, "fakequant_goldens.npz"), **arrays)
+with open(os.path.join(OUT, "cases.json"), "w") as f:
+    json.dump({"generator": "tests/golden/gen_goldens.py", "torch": torch.__version__,
+               "reference": "tranngocduvnvp/VSIQuantization @ /root/reference", "cases": cases},
+              f, indent=1)
+print(f"{len(cases)} cases, {len(arrays)} arrays ->", OUT)

@@ -1,0 +1,46 @@
+"""Loader + comparison helpers for the reference golden vectors (tests/golden/)."""
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN_DIR = os.path.join(HERE, "golden")
+
+_cache = {}
+
+
+def load():
+    if "d" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "cases.json")) as f:
+            meta = json.load(f)
+        arrs = np.load(os.path.join(GOLDEN_DIR, "fakequant_goldens.npz"), allow_pickle=False)
+        _cache["d"] = (meta["cases"], {k: arrs[k] for k in arrs.files})
+    return _cache["d"]
+
+
+def cases(kind):
+    cs, _ = load()
+    return [c for c in cs if c.get("kind") == kind]
+
+
+def arr(key):
+    _, a = load()
+    return a[key]
+
+
+def assert_bitwise_f32(got, want, what=""):
+    """Bit-exact fp32 equality; NaNs must coincide (payload/sign of NaN ignored:
+    x86 produces the negative default NaN, CDNA the positive one)."""
+    got = np.asarray(got, dtype=np.float32)
+    want = np.asarray(want, dtype=np.float32)
+    assert got.shape == want.shape, f"{what}: shape {got.shape} vs {want.shape}"
+    gn, wn = np.isnan(got), np.isnan(want)
+    assert np.array_equal(gn, wn), f"{what}: NaN positions differ ({int((gn ^ wn).sum())} elems)"
+    gb = got.view(np.uint32)[~gn]
+    wb = want.view(np.uint32)[~wn]
+    bad = np.flatnonzero(gb != wb)
+    if bad.size:
+        i = bad[0]
+        raise AssertionError(f"{what}: {bad.size} of {gb.size} elements differ bitwise; first: "
+                             f"got {got[~gn][i]!r} want {want[~wn][i]!r}")

@@ -1,0 +1,75 @@
+"""The C-ABI library loads and exports every symbol include/vsiq.h declares (no GPU,
+no compute calls)."""
+import ctypes
+import os
+import re
+
+from vsiquantization_amd import _build
+from vsiquantization_amd import _hip as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vsiq.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vsiq_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_built():
+    assert os.path.exists(_build.OUT), "run __graft_entry__.build() first"
+
+
+def test_header_symbols_exported():
+    lib = ctypes.CDLL(_build.OUT)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    assert sorted(H.EXPORTED) == declared_symbols()
+
+
+def test_abi_version_and_errors():
+    lib = H.lib()
+    assert lib.vsiq_abi_version() == H.ABI_VERSION
+    assert lib.vsiq_error_string(0) == b"success"
+    assert b"invalid" in lib.vsiq_error_string(-1)
+    assert lib.vsiq_workspace_doubles(1 << 30) >= 8
+
+
+def test_argument_validation_without_gpu():
+    """Invalid arguments are rejected on the host before any launch (no device needed)."""
+    lib = H.lib()
+    null = None
+    # n < 0
+    assert lib.vsiq_fq_fwd_f32(null, null, null, null, -1, null, null, 1.0, null, 0.0, 0, 0, 0, 1,
+                               null) == -1
+    # qmin > qmax
+    assert lib.vsiq_fq_fwd_f32(null, null, null, null, 4, null, null, 1.0, null, 0.0, 0, 0, 5, 1,
+                               null) == -1
+    # n == 0 is a no-op
+    assert lib.vsiq_fq_fwd_f32(null, null, null, null, 0, null, null, 1.0, null, 0.0, 0, 0, 0, 1,
+                               null) == 0
+    assert lib.vsiq_observe_f32(null, 0, null, null, null, 1, 127.0, 1e-8, null, 0, null, null) == -1
+    assert lib.vsiq_pc_observe_fq_f32(null, null, null, null, 0, 9, null, null, null, null, null, 1,
+                                      -128, 127, 127.0, 1e-8, null) == 0
+    assert lib.vsiq_lsq_bwd_f32(null, null, null, 0, null, 1.0, null, 0.0, 0, -128, 127, 1.0, null,
+                                null, 0, null, null) == -1
+
+
+def test_no_cpu_fallback_in_product():
+    """The product package never imports the oracle."""
+    pkg = os.path.join(ROOT, "vsiquantization_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+def test_gfx950_code_object_present():
+    """The fat binary embeds an amdgcn gfx950 code object."""
+    data = open(_build.OUT, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data

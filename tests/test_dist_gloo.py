@@ -1,0 +1,73 @@
+"""Multi-rank observer reduction on CPU (gloo, world_size 2).
+
+The per-rank statistics records are produced here by the numpy oracle (the K2
+kernel needs a GPU); what is tested is the exchange: the all-reduce packing
+(MAX over [-min, max], SUM over counts/sums), the fp32-rounded means and the
+running-state replay — sharded results must equal the unsharded ones exactly for
+min/max/qparams and within 1e-6 for mean|x| / std.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd.distributed import allreduce_stats, finish_stats, replay_minmax
+from oracle import fakequant_np as O
+
+
+def record(x):
+    """Oracle stand-in for one K2 stats record (f64[ST_LEN])."""
+    x = np.asarray(x, np.float32)
+    r = np.zeros(H.ST_LEN)
+    nn = x[~np.isnan(x)]
+    r[H.ST_MIN] = nn.min() if nn.size else np.inf
+    r[H.ST_MAX] = nn.max() if nn.size else -np.inf
+    r[H.ST_NAN] = np.isnan(x).sum()
+    d = x.astype(np.float64)
+    r[H.ST_SUMABS], r[H.ST_SUM], r[H.ST_SUMSQ], r[H.ST_N] = np.abs(d).sum(), d.sum(), (d * d).sum(), x.size
+    return torch.from_numpy(r)
+
+
+def batches():
+    rng = np.random.default_rng(0)
+    out = [rng.standard_normal((8, 3, 5, 5)).astype(np.float32) * (1 + i) for i in range(4)]
+    out[2][5, 0, 0, 0] = np.nan        # one shard of call 2 holds a NaN: the whole call is skipped
+    return out
+
+
+def _worker(rank, world, port, ret):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        recs = torch.stack([record(np.array_split(b, world)[rank]) for b in batches()])
+        red = allreduce_stats(recs.clone())
+        ret[rank] = red.numpy().copy()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_observer_matches_single_rank(world):
+    port = 29500 + os.getpid() % 1000
+    ret = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, port, ret), nprocs=world, join=True)
+    full = finish_stats(torch.stack([record(b) for b in batches()])).numpy()
+    for r in range(world):
+        red = ret[r]
+        assert np.array_equal(red[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]],
+                              full[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]])
+        np.testing.assert_allclose(red[:, H.ST_MEANABS], full[:, H.ST_MEANABS], rtol=1e-6, equal_nan=True)
+        np.testing.assert_allclose(red[:, H.ST_STD], full[:, H.ST_STD], rtol=1e-6, equal_nan=True)
+    # running-state replay equals the reference's sequential observer on the full batches
+    mn, mx = 0, 0
+    for b in batches():
+        mn, mx = O.observe_minmax(b, mn, mx)
+    rmn, rmx = replay_minmax(0, 0, ret[0][:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
+    assert (rmn, rmx) == (mn, mx)
+    assert O.minmax_qparams(rmn, rmx, False) == O.minmax_qparams(mn, mx, False)
+    # the NaN call contributes nothing, its fp32 means are NaN like torch's
+    assert np.isnan(ret[0][2, H.ST_MEANABS])

@@ -1,0 +1,307 @@
+"""HIP kernels vs the reference goldens and the numpy oracle (MI355X only).
+
+Every test goes through the C ABI (vsiquantization_amd._hip -> _vsiq_hip.so).
+Bars: integer codes and fp32 outputs bit-exact (y, x_int, grad_x);
+scale / zero-point gradients <= 1e-4 relative to the reference's fp32 sums and
+<= 1e-9 relative to the oracle's float64 closed form.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import vsiquantization_amd as V
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import fakequant as FQ
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def cu(a, grad=False):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t.requires_grad_(grad) if grad else t
+
+
+def npy(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    H.lib()   # raises if the HIP library is missing: no silent fallback
+
+
+# --------------------------------------------------------------------------- goldens
+@pytest.mark.parametrize("case", G.cases("per_tensor_observe_fq"), ids=lambda c: c["key"])
+def test_golden_per_tensor_observe_fq(case):
+    x = cu(G.arr(case["x"]))
+    obs = V.MinMaxObserver(case["sym"], case["obs_bits"])
+    if "raises" in case:
+        with pytest.raises(Exception) as ei:
+            obs.forward(x)
+        assert type(ei.value).__name__ == case["raises"]
+        return
+    s, z = obs.forward(x)
+    assert (s, z) == (case["scale"], case["zp"]) or (math.isnan(s) and math.isnan(case["scale"]))
+    assert (obs.min_val, obs.max_val) == (case["min_val"], case["max_val"])
+    q = V.UniformQuantizer(case["bits"], case["sym"])
+    xg = cu(G.arr(case["x"]), grad=True)
+    y = q.quantize(xg, s, z, False)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    G.assert_bitwise_f32(npy(q.discreate_tensor(x, s, z, q.qmin, q.qmax)), G.arr(case["x_int"]), "x_int")
+    # sync-free device path: qparams from the observer kernel, read by pointer
+    obs2 = V.MinMaxObserver(case["sym"], case["obs_bits"])
+    qp, st = obs2.observe_device(x)
+    qph = npy(qp)
+    assert qph[H.QP_SCALE] == case["scale"] and qph[H.QP_ZP] == case["zp"]
+    y2 = q.quantize(x, qp[H.QP_SCALE], qp[H.QP_ZP], False)
+    G.assert_bitwise_f32(npy(y2), G.arr(case["y"]), "y(device qparams)")
+    codes = FQ.fake_quant(x, s, z, q.qmin, q.qmax, want_codes=True)[2]
+    xi = G.arr(case["x_int"])
+    ok = ~np.isnan(xi)
+    assert np.array_equal(npy(codes)[ok].astype(np.int64), xi[ok].astype(np.int64))
+
+
+@pytest.mark.parametrize("case", G.cases("fixed_fq"), ids=lambda c: c["key"])
+def test_golden_fixed_fq(case):
+    q = V.UniformQuantizer(case["bits"], case["sym"])
+    xg = cu(G.arr(case["x"]), grad=True)
+    y = q.quantize(xg, case["scale"], case["zp"], False)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    xi = q.discreate_tensor(cu(G.arr(case["x"])), case["scale"], case["zp"], q.qmin, q.qmax)
+    G.assert_bitwise_f32(npy(xi), G.arr(case["x_int"]), "x_int")
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("case", G.cases("per_channel_observe_fq"), ids=lambda c: c["key"])
+def test_golden_per_channel(case, fused):
+    w = G.arr(case["x"])
+    obs = V.PerChannelMinMaxObserver(case["sym"], case["obs_bits"])
+    q = V.PerChannelUniformQuantizer(case["bits"], case["sym"])
+    xg = cu(w, grad=True)
+    if fused:
+        y, rs = obs.observe_quantize(xg, q, want_row_stats=True)
+        s, z = obs.get_scale_zero_point()
+    else:
+        s, z = obs.forward(xg.detach())
+        y = q.quantize(xg, s, z, False)
+    assert np.array_equal(npy(s), G.arr(case["scale"]), equal_nan=True)
+    zg = G.arr(case["zp"]).astype(np.float64)
+    assert np.array_equal(npy(z), zg)
+    assert np.array_equal(npy(obs.min_val), G.arr(case["min_val"]))
+    assert np.array_equal(npy(obs.max_val), G.arr(case["max_val"]))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq"), ids=lambda c: c["key"])
+def test_golden_learnable(case):
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    qcls = V.UniformQuantizer if case["sym"] else V.LSQQuantizer
+    q = qcls(case["bits"], case["sym"])
+    scale = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64, device=DEV))
+    if case["sym"]:
+        zp = 0
+    else:
+        zp = torch.nn.Parameter(torch.tensor(case["zp"], dtype=torch.float64, device=DEV))
+    xg = cu(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    assert scale.grad.dtype == torch.float64
+    assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                              O.grad_scale(qmax, x.size), learn_zp=not case["sym"])
+    assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+    if not case["sym"]:
+        assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
+        assert float(zp.grad) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
+
+
+def test_asym_learnable_int_zero_point_raises_like_reference():
+    q = V.UniformQuantizer(8, False)
+    s = torch.nn.Parameter(torch.tensor(0.1, dtype=torch.float64, device=DEV))
+    with pytest.raises(TypeError):
+        q.quantize(torch.randn(10, device=DEV), s, 0, True)
+
+
+@pytest.mark.parametrize("case", G.cases("manager_sequence"), ids=lambda c: c["key"])
+def test_golden_manager_sequence(case):
+    qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", case["bits"], case["sym"], True)
+    qm.is_observer_qparam, qm.is_learning_scale, qm.is_quantize = True, False, False
+    outs = [(qm.quantize(cu(G.arr(k))), k) for k in case["xs"]]
+    assert all(np.array_equal(npy(o), G.arr(k)) for o, k in outs)
+    cal = case["calib"]
+    assert (qm.observer.min_val, qm.observer.max_val) == (cal["min_val"], cal["max_val"])
+    assert float(qm.scale) == cal["scale"] and float(qm.zero_point) == cal["zero_point"]
+    np.testing.assert_allclose(qm.mean_abs_x, cal["mean_abs_x"], rtol=1e-6)
+    np.testing.assert_allclose(qm.mean_x, cal["mean_x"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(qm.std, cal["std"], rtol=1e-6)
+    qm.is_quantize = True
+    y = qm.quantize(cu(G.arr(case["x_oq"])))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y_oq"]), "observe+quantize")
+    qm.is_learning_scale = True
+    qm.init_scaling_factor_for_learning()
+    assert qm.scale == pytest.approx(case["init_scale"], rel=1e-6)
+    qm.make_learn_qparameter()
+    assert isinstance(qm.scale, torch.nn.Parameter) and qm.scale.dtype == torch.float64
+    if "learn_raises" in case:
+        with pytest.raises(TypeError):
+            qm.quantize(cu(G.arr(case["xs"][0])))
+        return
+    # use the reference's exact init value so the learnable step is bit-comparable
+    with torch.no_grad():
+        qm.scale.copy_(torch.tensor(case["init_scale"], dtype=torch.float64))
+    qm.cuda()
+    xg = cu(G.arr(case["x4"]), grad=True)
+    y4 = qm.quantize(xg)
+    G.assert_bitwise_f32(npy(y4), G.arr(case["y4"]), "y4")
+    y4.backward(cu(G.arr(case["g4"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["gx4"]), "gx4")
+    assert float(qm.scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4)
+
+
+# --------------------------------------------------------------------------- oracle, seeded
+def _rand(shape, seed, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+@pytest.mark.parametrize("shape", [(1024, 1024, 3, 3), (16, 3, 3, 3), (64, 7, 5, 5), (3, 20000),
+                                   (256, 40), (5, 4, 1, 1)])
+@pytest.mark.parametrize("sym,bits", [(False, 8), (True, 8), (True, 4), (False, 2)])
+def test_per_channel_vs_oracle(shape, sym, bits):
+    """C2 (north-star shape) and odd shapes: vector / scalar / large-row kernels."""
+    w = _rand(shape, 7, 0.05)
+    q = V.PerChannelUniformQuantizer(bits, sym)
+    obs = V.PerChannelMinMaxObserver(sym)
+    y, _ = obs.observe_quantize(cu(w), q)
+    s, z = obs.get_scale_zero_point()
+    ref = O.per_channel_observe_fq(w, sym, bits, 8)
+    assert np.array_equal(npy(s), ref["scale"])
+    assert np.array_equal(npy(z), ref["zp"].astype(np.float64))
+    G.assert_bitwise_f32(npy(y), ref["y"], "y")
+    codes = FQ.per_channel_observe_fq(cu(w), symmetric=sym, qmin=q.qmin, qmax=q.qmax,
+                                      want_codes=True, want_mask=True)
+    assert np.array_equal(npy(codes["codes"]).astype(np.int64), ref["x_int"].astype(np.int64))
+    assert np.array_equal(npy(codes["mask"]).astype(bool), ref["mask"])
+
+
+def test_per_channel_fwd_bwd_c2_full():
+    """North-star step at full size: per-channel asym int8 observe+fq fwd + STE bwd."""
+    w = _rand((1024, 1024, 3, 3), 0, 0.05)
+    g = _rand((1024, 1024, 3, 3), 1)
+    q = V.PerChannelUniformQuantizer(8, False)
+    obs = V.PerChannelMinMaxObserver(False)
+    xg = cu(w, grad=True)
+    y, _ = obs.observe_quantize(xg, q)
+    y.backward(cu(g))
+    ref = O.per_channel_observe_fq(w, False, 8, 8)
+    G.assert_bitwise_f32(npy(y), ref["y"], "y")
+    G.assert_bitwise_f32(npy(xg.grad), O.per_channel_backward_fixed(g, ref["mask"], ref["scale"]), "gx")
+
+
+def test_per_channel_running_state_and_nan_rows():
+    """Two calls on one observer: running min/max per channel, NaN row leaves its state."""
+    w1 = _rand((6, 50), 3)
+    w2 = _rand((6, 50), 4) * 3
+    w2[2, 5] = np.nan
+    obs = V.PerChannelMinMaxObserver(False)
+    q = V.PerChannelUniformQuantizer(8, False)
+    obs.observe_quantize(cu(w1), q)
+    y2, _ = obs.observe_quantize(cu(w2), q)
+    r1 = O.per_channel_observe_fq(w1, False, 8, 8)
+    ref = O.per_channel_observe_fq(w2, False, 8, 8, run_min=r1["min_val"], run_max=r1["max_val"])
+    assert np.array_equal(npy(obs.min_val), ref["min_val"])
+    assert np.array_equal(npy(obs.max_val), ref["max_val"])
+    assert ref["min_val"][2] == r1["min_val"][2] and ref["max_val"][2] == r1["max_val"][2]
+    G.assert_bitwise_f32(npy(y2), ref["y"], "y2")
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1023, 4097, 1 << 20, (1 << 20) + 5])
+@pytest.mark.parametrize("sym", [True, False])
+def test_per_tensor_observe_fq_sizes(n, sym):
+    x = _rand(n, n % 97, 2.0)
+    obs = V.MinMaxObserver(sym)
+    qp, st = obs.observe_device(cu(x))
+    mn, mx = O.observe_minmax(x, 0, 0)
+    s, z = O.minmax_qparams(mn, mx, sym, 8)
+    qph = npy(qp)
+    assert qph[H.QP_SCALE] == s and qph[H.QP_ZP] == z
+    sth = npy(st)
+    ma, me, sd = O.collect_stats(x)
+    assert sth[H.ST_MEANABS] == pytest.approx(ma, rel=1e-6)
+    if n > 1:
+        assert sth[H.ST_STD] == pytest.approx(sd, rel=1e-6)
+    q = V.UniformQuantizer(4, sym)
+    y = q.quantize(cu(x), qp[H.QP_SCALE], qp[H.QP_ZP], False)
+    yo, _, _ = O.fq_forward(x, s, z, q.qmin, q.qmax)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+
+
+def test_misaligned_and_noncontiguous_inputs():
+    base = _rand(4099, 11)
+    xt = cu(base)[3:]                        # 12-byte offset: scalar kernel path
+    q = V.UniformQuantizer(8, True)
+    y = q.quantize(xt, 0.02, 0, False)
+    G.assert_bitwise_f32(npy(y), O.fq_forward(base[3:], 0.02, 0, -128, 127)[0], "misaligned")
+    m = _rand((64, 48), 12)
+    y2 = q.quantize(cu(m).t(), 0.02, 0, False)  # non-contiguous -> contiguous copy
+    G.assert_bitwise_f32(npy(y2), O.fq_forward(m.T.copy(), 0.02, 0, -128, 127)[0], "transposed")
+
+
+def test_empty_tensor():
+    q = V.UniformQuantizer(8, True)
+    assert q.quantize(torch.empty(0, device=DEV), 0.1, 0, False).numel() == 0
+    with pytest.raises(RuntimeError):
+        V.MinMaxObserver(True).forward(torch.empty(0, device=DEV))
+
+
+@pytest.mark.parametrize("sym", [True, False])
+def test_lsq_c3_full_size(sym):
+    """C3: 512x3x224x224 learnable fwd + STE bwd; grad_x bitwise, scale grad vs f64 closed form."""
+    shape = (512, 3, 224, 224)
+    x = _rand(shape, 0)
+    g = _rand(shape, 1)
+    qcls = V.UniformQuantizer if sym else V.LSQQuantizer
+    q = qcls(8, sym)
+    scale = torch.nn.Parameter(torch.tensor(0.03, dtype=torch.float64, device=DEV))
+    zp = 0 if sym else torch.nn.Parameter(torch.tensor(3.0, dtype=torch.float64, device=DEV))
+    xg = cu(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    y.backward(cu(g))
+    qmin, qmax = O.qrange(8, sym)
+    yo, gxo, gso, gzo = O.lsq_forward_backward(x, g, 0.03, 0 if sym else 3.0, qmin, qmax,
+                                               O.grad_scale(qmax, x.size), learn_zp=not sym)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(xg.grad), gxo, "grad_x")
+    assert float(scale.grad) == pytest.approx(gso, rel=1e-9)
+    if not sym:
+        assert float(zp.grad) == pytest.approx(gzo, rel=1e-9)
+
+
+def test_reductions_deterministic():
+    x = cu(_rand(3_000_001, 5))
+    g = cu(_rand(3_000_001, 6))
+    outs = []
+    for _ in range(3):
+        _, st = FQ.observe_tensor(x, symmetric=True)
+        _, grads = FQ.lsq_backward(g, x, 0.05, 0, -128, 127, 1e-3, False)
+        outs.append((npy(st).tobytes(), npy(grads).tobytes()))
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_cpu_tensor_fails_loudly():
+    with pytest.raises(H.VsiqError):
+        V.UniformQuantizer(8, True).quantize(torch.randn(8), 0.1, 0, False)

@@ -1,0 +1,118 @@
+"""Pin the numpy oracle against the reference goldens (CPU only, no GPU).
+
+The goldens were produced by running the reference itself
+(tests/golden/gen_goldens.py); passing here is what makes the oracle a
+trustworthy checker for the HIP kernels (tests/test_gpu_parity.py).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+
+@pytest.mark.parametrize("case", G.cases("per_tensor_observe_fq"), ids=lambda c: c["key"])
+def test_per_tensor_observe_fq(case):
+    x = G.arr(case["x"])
+    mn, mx = O.observe_minmax(x, 0, 0)
+    assert float(mn) == case["min_val"] and float(mx) == case["max_val"]
+    if "raises" in case:
+        with pytest.raises(Exception) as ei:
+            O.minmax_qparams(mn, mx, case["sym"], case["obs_bits"])
+        assert type(ei.value).__name__ == case["raises"]
+        return
+    s, z = O.minmax_qparams(mn, mx, case["sym"], case["obs_bits"])
+    assert (s == case["scale"]) or (math.isnan(s) and math.isnan(case["scale"]))
+    assert z == case["zp"]
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    y, q, mask = O.fq_forward(x, s, z, qmin, qmax)
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(q, G.arr(case["x_int"]), "x_int")
+    gx = O.fq_backward_fixed(G.arr(case["g"]), mask, s)
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("fixed_fq"), ids=lambda c: c["key"])
+def test_fixed_fq(case):
+    x = G.arr(case["x"])
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    y, q, mask = O.fq_forward(x, case["scale"], case["zp"], qmin, qmax)
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(q, G.arr(case["x_int"]), "x_int")
+    gx = O.fq_backward_fixed(G.arr(case["g"]), mask, case["scale"])
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("per_channel_observe_fq"), ids=lambda c: c["key"])
+def test_per_channel(case):
+    w = G.arr(case["x"])
+    r = O.per_channel_observe_fq(w, case["sym"], case["bits"], case["obs_bits"])
+    assert np.array_equal(r["scale"], G.arr(case["scale"]), equal_nan=True)
+    assert np.array_equal(r["zp"], G.arr(case["zp"]))
+    assert np.array_equal(r["min_val"], G.arr(case["min_val"]))
+    assert np.array_equal(r["max_val"], G.arr(case["max_val"]))
+    G.assert_bitwise_f32(r["y"], G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(r["x_int"], G.arr(case["x_int"]), "x_int")
+    gx = O.per_channel_backward_fixed(G.arr(case["g"]), r["mask"], r["scale"])
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq"), ids=lambda c: c["key"])
+def test_learnable(case):
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    gs = O.grad_scale(qmax, x.size)
+    y, gx, gsc, gzp = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax, gs,
+                                             learn_zp=not case["sym"])
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+    # reference sums in fp32 -> tolerance (SURVEY §8d parity gates: <=1e-4 relative)
+    assert gsc == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    if not case["sym"]:
+        assert gzp == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
+
+
+def test_asym_learnable_int_zp_raises_in_reference():
+    (c,) = G.cases("asym_learnable_int_zp")
+    assert c["raises"] == "TypeError"
+
+
+@pytest.mark.parametrize("case", G.cases("manager_sequence"), ids=lambda c: c["key"])
+def test_manager_sequence(case):
+    """QuantizationManager calibrate -> observe+quantize -> learn-init (qm.py:55-114)."""
+    bits, sym = case["bits"], case["sym"]
+    mn, mx = 0, 0
+    stats = []
+    for k in case["xs"]:
+        x = G.arr(k)
+        stats.append(O.collect_stats(x))
+        mn, mx = O.observe_minmax(x, mn, mx)
+    cal = case["calib"]
+    assert (mn, mx) == (cal["min_val"], cal["max_val"])
+    s, z = O.minmax_qparams(mn, mx, sym, 8)  # observer is always 8-bit (qm.py:42)
+    assert s == cal["scale"] and z == cal["zero_point"]
+    np.testing.assert_allclose([t[0] for t in stats], cal["mean_abs_x"], rtol=1e-6)
+    np.testing.assert_allclose([t[1] for t in stats], cal["mean_x"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose([t[2] for t in stats], cal["std"], rtol=1e-6)
+    # observe + quantize in the same call
+    xo = G.arr(case["x_oq"])
+    mn, mx = O.observe_minmax(xo, mn, mx)
+    s, z = O.minmax_qparams(mn, mx, sym, 8)
+    assert s == case["observe_quantize"]["scale"]
+    qmin, qmax = O.qrange(bits, sym)
+    y, _, _ = O.fq_forward(xo, s, z, qmin, qmax)
+    G.assert_bitwise_f32(y, G.arr(case["y_oq"]), "y_oq")
+    init = O.init_scale_for_learning([t[0] for t in stats] + [O.collect_stats(xo)[0]], bits)
+    assert init == pytest.approx(case["init_scale"], rel=1e-6)
+    if "learn_raises" in case:
+        assert case["learn_raises"] == "TypeError" and not sym
+        return
+    x4, g4 = G.arr(case["x4"]), G.arr(case["g4"])
+    s_ref = case["init_scale"]
+    gs = O.grad_scale(qmax, x4.size)
+    y4, gx4, gsc, _ = O.lsq_forward_backward(x4, g4, s_ref, 0, qmin, qmax, gs)
+    G.assert_bitwise_f32(y4, G.arr(case["y4"]), "y4")
+    G.assert_bitwise_f32(gx4, G.arr(case["gx4"]), "gx4")
+    assert gsc == pytest.approx(case["scale_grad"], rel=1e-4)

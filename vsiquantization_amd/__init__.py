@@ -1,0 +1,28 @@
+"""vsiquantization_amd — MI355X-native (gfx950) fake-quantization hot path of
+tranngocduvnvp/VSIQuantization behind the reference's own plugin API.
+
+Importing the package registers the quantizer/observer classes by name in
+``vsiquantization_amd.utils.registry.CLASS_REGISTRY``:
+
+  UniformQuantizer, MinMaxObserver                  (reference names, same behaviour)
+  LSQQuantizer, LSQObserver                         (names the reference README advertises)
+  PerChannelUniformQuantizer, PerChannelMinMaxObserver  (per-channel, axis 0)
+
+All arithmetic runs in the HIP kernels of ``csrc/vsiq_kernels.hip`` through the
+C ABI of ``include/vsiq.h``; there is no CPU path.
+"""
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+from .utils.registry import CLASS_REGISTRY, register_class  # noqa: F401
+from .quantizers.base import BaseQuantizer  # noqa: F401
+from .observers.base import BaseObserver  # noqa: F401
+from .quantizers.uniform import UniformQuantizer, ScaleGradient, RoundStraightThrough  # noqa: F401
+from .quantizers.lsq import LSQQuantizer  # noqa: F401
+from .quantizers.per_channel import PerChannelUniformQuantizer  # noqa: F401
+from .observers.minmax import MinMaxObserver  # noqa: F401
+from .observers.lsq import LSQObserver  # noqa: F401
+from .observers.per_channel import PerChannelMinMaxObserver  # noqa: F401
+from .quantizers.quantization_manager import QuantizationManager  # noqa: F401
+from .quantizers.fake_quantize import FakeQuantize  # noqa: F401
+
+__version__ = "0.1.0"

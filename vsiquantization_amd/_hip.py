@@ -1,0 +1,133 @@
+"""ctypes binding of the C ABI in include/vsiq.h (the drop-in boundary).
+
+The library is loaded AFTER torch so that its NEEDED `libamdhip64.so.7` resolves
+to the HIP runtime torch already mapped (same soname): one HIP runtime, one
+context, and torch's stream handles are valid inside the kernels' launches.
+
+Fails loudly: there is no CPU fallback anywhere in vsiquantization_amd.  A
+missing library, a CPU tensor, or a non-zero return code raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from . import _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+c_p = ctypes.c_void_p
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_d = ctypes.c_double
+
+ABI_VERSION = 1
+
+# record layouts (include/vsiq.h)
+ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)
+ST_LEN = 10
+QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
+QP_LEN = 4
+
+_SIGS = {
+    "vsiq_abi_version": ([], c_int),
+    "vsiq_error_string": ([c_int], ctypes.c_char_p),
+    "vsiq_workspace_doubles": ([c_i64], c_i64),
+    "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
+                        c_int),
+    "vsiq_observe_f32": ([c_p, c_i64, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p], c_int),
+    "vsiq_observe_finalize": ([c_p, c_p, c_p, c_int, c_d, c_d, c_p], c_int),
+    "vsiq_pc_observe_fq_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_int, c_int,
+                                c_int, c_d, c_d, c_p], c_int),
+    "vsiq_pc_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_p], c_int),
+    "vsiq_ste_bwd_f32": ([c_p, c_p, c_p, c_i64, c_p, c_i64, c_d, c_p], c_int),
+    "vsiq_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d, c_p, c_p,
+                          c_i64, c_p, c_p], c_int),
+}
+EXPORTED = tuple(_SIGS)
+
+
+class VsiqError(RuntimeError):
+    pass
+
+
+def library_path() -> str:
+    return _build.OUT
+
+
+def lib():
+    """Load (never build) the HIP library; raise if it is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = library_path()
+        if not os.path.exists(path):
+            raise VsiqError(
+                f"vsiquantization_amd HIP library missing at {path}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        handle = ctypes.CDLL(path)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = res
+        v = handle.vsiq_abi_version()
+        if v != ABI_VERSION:
+            raise VsiqError(f"vsiq ABI version {v} != expected {ABI_VERSION}; rebuild the library")
+        _LIB = handle
+    return _LIB
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().vsiq_error_string(rc)
+        raise VsiqError(f"{what} failed ({rc}): {msg.decode() if msg else '?'}")
+
+
+# --------------------------------------------------------------------------- tensor helpers
+def require_device_f32(x: torch.Tensor, what: str = "x") -> torch.Tensor:
+    if not isinstance(x, torch.Tensor):
+        raise TypeError(f"{what} must be a torch.Tensor, got {type(x).__name__}")
+    if x.device.type != "cuda":
+        raise VsiqError(
+            f"vsiquantization_amd runs on MI355X (HIP) only; {what} is on {x.device}. "
+            "There is no CPU path: move the model/tensors to the GPU.")
+    if x.dtype != torch.float32:
+        raise TypeError(f"{what}: only float32 is supported by the HIP fake-quant path, got {x.dtype}")
+    return x.contiguous()
+
+
+def ptr(t):
+    return None if t is None else c_p(t.data_ptr())
+
+
+def stream_of(device) -> c_p:
+    return c_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _Workspace:
+    """Per (device, stream) reduction workspace + self-resetting arrival counter."""
+
+    def __init__(self, device):
+        n = lib().vsiq_workspace_doubles(0)
+        self.ws = torch.empty(n, dtype=torch.float64, device=device)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
+        self.ws_len = n
+
+
+_WS = {}
+
+
+def workspace(device) -> _Workspace:
+    dev = torch.device(device)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    w = _WS.get(key)
+    if w is None:
+        w = _WS[key] = _Workspace(dev)
+    return w

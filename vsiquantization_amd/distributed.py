@@ -1,0 +1,89 @@
+"""Multi-GPU observer: batch-sharded activations, one process per GPU (RCCL over xGMI).
+
+The fake-quant itself is elementwise and needs no communication.  The only
+exchange is the per-tensor observer's statistics: every rank
+runs the K2 pass over its shard, then
+
+    all_reduce(MAX)  over [-min, max]                         (exact, order-free)
+    all_reduce(SUM)  over [nan_count, sum|x|, sum x, sum x^2, n]
+
+after which every rank holds the statistics of the whole batch and applies the
+reference's running update (observers/minmax.py:42-47) identically.  min/max and
+the qparams are therefore bit-identical to a 1-GPU run; the sums differ only in
+float64 summation order.
+
+Two modes:
+* per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): two tiny
+  all-reduces per observer call, needed when the same call also fake-quantizes
+  (observe+quantize mode, §3.4);
+* deferred  (``dist_defer`` True, calibration): each rank only records its local
+  per-call statistics; ``sync_calibration(model)`` all-reduces ALL records of ALL
+  layers in two collectives and replays the running min/max per layer.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _hip as H
+
+_SUM_SLICE = slice(H.ST_NAN, H.ST_N + 1)
+
+
+def finish_stats(stats: torch.Tensor) -> torch.Tensor:
+    """Recompute the fp32-rounded mean|x|, mean, std entries from the sums (in place)."""
+    n = stats[..., H.ST_N]
+    mean = stats[..., H.ST_SUM] / n
+    var = (stats[..., H.ST_SUMSQ] - stats[..., H.ST_SUM] * mean) / (n - 1.0)
+    has_nan = stats[..., H.ST_NAN] > 0
+    nan = torch.full_like(mean, float("nan"))
+    std = torch.where(n > 1, var.clamp_min(0.0).sqrt(), nan)
+    vals = [stats[..., H.ST_SUMABS] / n, mean, std]
+    for i, v in zip((H.ST_MEANABS, H.ST_MEAN, H.ST_STD), vals):
+        stats[..., i] = torch.where(has_nan, nan, v.to(torch.float32).to(torch.float64))
+    return stats
+
+
+def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
+    """All-reduce observer stats records ``[..., ST_LEN]`` across ranks, in place."""
+    mm = torch.stack([-stats[..., H.ST_MIN], stats[..., H.ST_MAX]], dim=-1).contiguous()
+    sums = stats[..., _SUM_SLICE].contiguous()
+    dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    stats[..., H.ST_MIN] = -mm[..., 0]
+    stats[..., H.ST_MAX] = mm[..., 1]
+    stats[..., _SUM_SLICE] = sums
+    return finish_stats(stats)
+
+
+def replay_minmax(min_val, max_val, records):
+    """Fold per-call [min, max, nan_count] records into the running state exactly like
+    observers/minmax.py:42-47 (a NaN call changes nothing; strict comparisons)."""
+    for mn, mx, nanc in records:
+        if nanc > 0:
+            continue
+        if mn < min_val:
+            min_val = mn
+        if mx > max_val:
+            max_val = mx
+    return min_val, max_val
+
+
+def _deferred_managers(model):
+    from .quantizers.quantization_manager import QuantizationManager
+    for m in model.modules():
+        if isinstance(m, QuantizationManager) and m._pending_records:
+            yield m
+
+
+def sync_calibration(model, group=None):
+    """Deferred calibration sync: two all-reduces for every recorded call of every layer."""
+    mgrs = list(_deferred_managers(model))
+    if not mgrs:
+        return 0
+    recs = [torch.stack(m._pending_records) for m in mgrs]
+    counts = [r.shape[0] for r in recs]
+    host = allreduce_stats(torch.cat(recs), group=group).cpu()
+    for m, part in zip(mgrs, host.split(counts)):
+        m._apply_synced_records(part)
+    return len(mgrs)

@@ -1,0 +1,305 @@
+"""torch-facing fake-quant ops over the HIP C ABI (no CPU path).
+
+Each op here is one (or two) kernel launches on the tensor's current HIP
+stream, no host synchronisation, and is the MI355X replacement of one chain of
+eager torch ops in the reference:
+
+  fake_quant               quantizers/uniform.py:54-55,95   (K1)
+  observe_tensor           observers/minmax.py:32-88 + quantization_manager.py:66-68 (K2)
+  per_channel_observe_fq   per-channel MinMax + UniformQuantizer (K3)
+  FakeQuantFixedFn         autograd of uniform.py:55,95 with fixed qparams (STE)
+  FakeQuantLearnFn         autograd of uniform.py:47-56 (LSQ: ScaleGradient, STE) (K4)
+"""
+from __future__ import annotations
+
+import numbers
+
+import numpy as np
+import torch
+
+from . import _hip as H
+
+
+# --------------------------------------------------------------------------- scalars
+def qden(symmetric: bool, num_bits: int, eps: float) -> float:
+    """Denominator of minmax.py:72 / :75, evaluated with Python floats like the reference."""
+    return (2 ** (num_bits - 1) - 1 + eps) if symmetric else (2 ** num_bits - 1 + eps)
+
+
+def _as_f64_device(t: torch.Tensor, device) -> torch.Tensor:
+    t = t.detach()
+    if t.numel() != 1:
+        raise ValueError(f"expected a scalar (1-element) qparam tensor, got shape {tuple(t.shape)}")
+    if t.device != device:
+        t = t.to(device, non_blocking=True)
+    if t.dtype != torch.float64:
+        t = t.to(torch.float64)
+    return t.contiguous()
+
+
+def scalar_source(v, device):
+    """Resolve a scale / zero-point argument into (device f64 tensor | None, host float).
+
+    Python numbers and CPU tensors are read on the host (no GPU sync); CUDA
+    tensors are passed by pointer so the kernel reads the current value."""
+    if isinstance(v, torch.Tensor):
+        if v.device.type == "cuda":
+            return _as_f64_device(v, device), 0.0
+        return None, float(v.detach().reshape(()).item())
+    if isinstance(v, (numbers.Real, np.floating, np.integer)):
+        return None, float(v)
+    raise TypeError(f"unsupported qparam type {type(v).__name__}")
+
+
+def _i64(n):
+    return H.c_i64(int(n))
+
+
+# --------------------------------------------------------------------------- forward (K1)
+def fake_quant(x: torch.Tensor, scale, zero_point, qmin: int, qmax: int, *, zp_round: bool = False,
+               qp: torch.Tensor | None = None, want_mask: bool = False, want_codes: bool = False,
+               discrete: bool = False):
+    """y = (clamp(rint(x/s + zp), qmin, qmax) - zp) * s  (uniform.py:55,95), fp32, bit-exact.
+
+    qp: optional observer record (f64[QP_LEN] on x.device) used instead of scale/zero_point.
+    discrete: return the integer-valued fp32 codes in y instead (discreate_tensor).
+    Returns (y, mask|None, codes|None); codes int8 (qmin<0) or uint8."""
+    x = H.require_device_f32(x)
+    dev = x.device
+    y = torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if want_mask else None
+    codes = None
+    if want_codes:
+        codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
+    if qp is not None:
+        sd, sh, zd, zh = None, 0.0, None, 0.0
+    else:
+        sd, sh = scalar_source(scale, dev)
+        zd, zh = scalar_source(zero_point, dev)
+    rc = H.lib().vsiq_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(x.numel()),
+                                 H.ptr(qp), H.ptr(sd), sh, H.ptr(zd), zh, int(bool(zp_round)),
+                                 int(bool(discrete)), int(qmin), int(qmax), H.stream_of(dev))
+    H.check(rc, "vsiq_fq_fwd_f32")
+    return y, mask, codes
+
+
+def ste_backward(g: torch.Tensor, mask: torch.Tensor, scale, rowlen: int = 0) -> torch.Tensor:
+    """gx = (mask ? g*s : 0) / s  — autograd of uniform.py:55,95 with a fixed scale."""
+    g = H.require_device_f32(g, "grad_output")
+    dev = g.device
+    gx = torch.empty_like(g)
+    if isinstance(scale, torch.Tensor) and scale.device.type == "cuda" and scale.numel() > 1:
+        sd, sh = scale.detach().to(torch.float64).contiguous(), 0.0
+    else:
+        sd, sh = scalar_source(scale, dev)
+        rowlen = 0
+    rc = H.lib().vsiq_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(gx), _i64(g.numel()), H.ptr(sd),
+                                  _i64(rowlen), sh, H.stream_of(dev))
+    H.check(rc, "vsiq_ste_bwd_f32")
+    return gx
+
+
+class FakeQuantFixedFn(torch.autograd.Function):
+    """Fixed-qparam fake quant with the reference's STE gradient (x only)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, qp):
+        y, mask, _ = fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, want_mask=True)
+        ctx.save_for_backward(mask)
+        if qp is not None:
+            ctx.scale = qp[H.QP_SCALE:H.QP_SCALE + 1]
+        else:
+            ctx.scale = scale.detach() if isinstance(scale, torch.Tensor) else scale
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (mask,) = ctx.saved_tensors
+        return ste_backward(gy.contiguous(), mask, ctx.scale), None, None, None, None, None
+
+
+def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None):
+    if x.requires_grad and torch.is_grad_enabled():
+        return FakeQuantFixedFn.apply(x, scale, zero_point, qmin, qmax, qp)
+    return fake_quant(x, scale, zero_point, qmin, qmax, qp=qp)[0]
+
+
+# --------------------------------------------------------------------------- learnable (K4)
+def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+    g = H.require_device_f32(g, "grad_output")
+    dev = g.device
+    gx = torch.empty_like(g)
+    grads = torch.empty(2, dtype=torch.float64, device=dev)
+    sd, sh = scalar_source(scale, dev)
+    zd, zh = scalar_source(zero_point, dev)
+    w = H.workspace(dev)
+    rc = H.lib().vsiq_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), H.ptr(sd), sh,
+                                  H.ptr(zd), zh, int(bool(learn_zp)), int(qmin), int(qmax),
+                                  float(gscale), H.ptr(grads), H.ptr(w.ws), _i64(w.ws_len),
+                                  H.ptr(w.counter), H.stream_of(dev))
+    H.check(rc, "vsiq_lsq_bwd_f32")
+    return gx, grads
+
+
+class FakeQuantLearnFn(torch.autograd.Function):
+    """Learnable-scale (and, asymmetric, learnable zero-point) fake quant.
+
+    Forward = uniform.py:47-56; backward = the reference's autograd graph in closed
+    form (ScaleGradient x gscale on scale and zp, ClampBackward1 mask, STE)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+        x = H.require_device_f32(x)
+        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp)
+        ctx.save_for_backward(x)
+        ctx.scale, ctx.zp = scale, zero_point
+        ctx.args = (qmin, qmax, gscale, learn_zp)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        qmin, qmax, gscale, learn_zp = ctx.args
+        s, z = ctx.scale, ctx.zp
+        gx, grads = lsq_backward(gy.contiguous(), x, s, z, qmin, qmax, gscale, learn_zp)
+        gs = gz = None
+        if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
+            gs = grads[0].to(device=s.device, dtype=s.dtype).reshape(s.shape)
+        if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
+            gz = grads[1].to(device=z.device, dtype=z.dtype).reshape(z.shape)
+        return gx, gs, gz, None, None, None, None
+
+
+# --------------------------------------------------------------------------- observer (K2)
+def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: float = 1e-8,
+                   run_minmax: torch.Tensor | None = None, want_qp: bool = True,
+                   want_stats: bool = True):
+    """One pass over x: min/max/NaN/sums -> running state update -> f64 qparams (no sync).
+
+    Returns (qp f64[QP_LEN] | None, stats f64[ST_LEN] | None)."""
+    x = H.require_device_f32(x)
+    if x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    dev = x.device
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev) if want_qp else None
+    st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev) if want_stats else None
+    w = H.workspace(dev)
+    rc = H.lib().vsiq_observe_f32(H.ptr(x), _i64(x.numel()), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
+                                  int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps),
+                                  H.ptr(w.ws), _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
+    H.check(rc, "vsiq_observe_f32")
+    return qp, st
+
+
+def observe_finalize(stats: torch.Tensor, run_minmax, *, symmetric, num_bits=8, eps=1e-8):
+    """Running update + qparams from an (all-reduced) stats record; returns qp f64[QP_LEN]."""
+    dev = stats.device
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev)
+    rc = H.lib().vsiq_observe_finalize(H.ptr(stats), H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
+                                       qden(symmetric, num_bits, eps), float(eps), H.stream_of(dev))
+    H.check(rc, "vsiq_observe_finalize")
+    return qp
+
+
+# --------------------------------------------------------------------------- per-channel (K3)
+def per_channel_observe_fq(x: torch.Tensor, *, symmetric: bool, qmin: int, qmax: int,
+                           obs_bits: int = 8, eps: float = 1e-8, run_min=None, run_max=None,
+                           quantize: bool = True, want_mask: bool = False, want_codes: bool = False,
+                           want_row_stats: bool = False):
+    """Fused per-channel (axis 0) MinMax observe + f64 qparams + fake quant, one pass (K3).
+
+    quantize=False observes only (state, qparams, stats; y is None).
+    Returns dict(y, scale f64[C], zp f64[C], run_min, run_max, mask, codes, row_stats f64[C,3])."""
+    x = H.require_device_f32(x)
+    dev = x.device
+    C = x.shape[0] if x.dim() > 0 else 1
+    rowlen = x.numel() // max(C, 1)
+    if run_min is None:
+        run_min = torch.zeros(C, dtype=torch.float32, device=dev)
+    if run_max is None:
+        run_max = torch.zeros(C, dtype=torch.float32, device=dev)
+    if run_min.numel() != C or run_max.numel() != C:
+        raise ValueError(f"running state has {run_min.numel()} channels, tensor has {C}")
+    y = torch.empty_like(x) if quantize else None
+    scale = torch.empty(C, dtype=torch.float64, device=dev)
+    zp = torch.empty(C, dtype=torch.float64, device=dev)
+    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if (want_mask and quantize) else None
+    codes = (torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
+             if (want_codes and quantize) else None)
+    rstats = torch.empty(C, 3, dtype=torch.float64, device=dev) if want_row_stats else None
+    rc = H.lib().vsiq_pc_observe_fq_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(C),
+                                        _i64(rowlen), H.ptr(run_min), H.ptr(run_max), H.ptr(scale),
+                                        H.ptr(zp), H.ptr(rstats), int(bool(symmetric)), int(qmin),
+                                        int(qmax), qden(symmetric, obs_bits, eps), float(eps),
+                                        H.stream_of(dev))
+    H.check(rc, "vsiq_pc_observe_fq_f32")
+    return dict(y=y, scale=scale, zp=zp, run_min=run_min, run_max=run_max, mask=mask, codes=codes,
+                row_stats=rstats)
+
+
+def stats_from_row_sums(row_stats: torch.Tensor, numel: int) -> torch.Tensor:
+    """[C,3] per-row (sum|x|, sum x, sum x^2) -> f64[3] fp32-rounded (mean|x|, mean, std)
+    (quantization_manager.py:66-68), on the device, no sync."""
+    tot = row_stats.sum(0)
+    n = float(numel)
+    mean = tot[1] / n
+    var = (tot[2] - tot[1] * mean) / (n - 1.0) if numel > 1 else torch.full_like(mean, float("nan"))
+    out = torch.stack([tot[0] / n, mean, var.clamp_min(0.0).sqrt()])
+    return out.to(torch.float32).to(torch.float64)
+
+
+def per_channel_fake_quant(x, scale: torch.Tensor, zp: torch.Tensor, qmin, qmax, *, zp_round=False,
+                           want_mask=False, want_codes=False):
+    """Per-channel fake quant with given f64 [C] qparams."""
+    x = H.require_device_f32(x)
+    dev = x.device
+    C = x.shape[0]
+    y = torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if want_mask else None
+    codes = (torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
+             if want_codes else None)
+    s = scale.detach().to(dev, torch.float64).contiguous()
+    z = zp.detach().to(dev, torch.float64).contiguous()
+    rc = H.lib().vsiq_pc_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(C),
+                                    _i64(x.numel() // C), H.ptr(s), H.ptr(z), int(bool(zp_round)),
+                                    int(qmin), int(qmax), H.stream_of(dev))
+    H.check(rc, "vsiq_pc_fq_fwd_f32")
+    return y, mask, codes
+
+
+class PerChannelFQFn(torch.autograd.Function):
+    """Per-channel fake quant with given f64 [C] qparams and the STE backward."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zp, qmin, qmax):
+        y, mask, _ = per_channel_fake_quant(x, scale, zp, qmin, qmax, want_mask=True)
+        s = scale.detach().to(x.device, torch.float64).contiguous()
+        ctx.save_for_backward(mask, s)
+        ctx.rowlen = x.numel() // x.shape[0]
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        mask, scale = ctx.saved_tensors
+        return ste_backward(gy.contiguous(), mask, scale, ctx.rowlen), None, None, None, None
+
+
+class PerChannelObserveFQFn(torch.autograd.Function):
+    """Per-channel observe + fake quant with the STE backward (row c uses fp32(scale_c))."""
+
+    @staticmethod
+    def forward(ctx, x, symmetric, qmin, qmax, obs_bits, eps, run_min, run_max, want_row_stats):
+        r = per_channel_observe_fq(x, symmetric=symmetric, qmin=qmin, qmax=qmax, obs_bits=obs_bits,
+                                   eps=eps, run_min=run_min, run_max=run_max, want_mask=True,
+                                   want_row_stats=want_row_stats)
+        ctx.save_for_backward(r["mask"], r["scale"])
+        ctx.rowlen = x.numel() // x.shape[0]
+        rs = r["row_stats"] if want_row_stats else r["scale"].new_zeros(0)
+        ctx.mark_non_differentiable(r["scale"], r["zp"], rs)
+        return r["y"], r["scale"], r["zp"], rs
+
+    @staticmethod
+    def backward(ctx, gy, _gs, _gz, _gr):
+        mask, scale = ctx.saved_tensors
+        gx = ste_backward(gy.contiguous(), mask, scale, ctx.rowlen)
+        return gx, None, None, None, None, None, None, None, None

@@ -1,0 +1,121 @@
+"""MinMaxObserver on MI355X (reference: observers/minmax.py:6-88).
+
+Same registry name, constructor ``(symmetric=True, num_bits=8, eps=1e-8)``,
+attributes (``symmetric, eps, num_bits, min_val, max_val``) and methods
+(``observe``, ``get_scale_zero_point``, ``forward``).
+
+The running ``(min_val, max_val)`` state lives on the device as fp32[2] and is
+updated by one pass of the K2 kernel per ``observe`` (the reference runs two
+full reductions and two ``.item()`` syncs, minmax.py:42-43).  fp32 state is
+exact: every value it can hold is an element of an fp32 tensor or the initial 0.
+``min_val``/``max_val`` read it back lazily (one sync), returning the int ``0``
+the reference starts with until a strictly smaller/larger value arrives.
+
+``get_scale_zero_point``/``forward`` keep the reference's host semantics (Python
+float scale, int zero point, ValueError/OverflowError from ``round`` on a
+non-finite value).  ``observe_device`` is the sync-free path used by
+QuantizationManager: it returns the f64 qparams record computed on the device.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _hip as H
+from ..fakequant import observe_tensor
+from ..utils.registry import register_class
+from .base import BaseObserver
+
+
+def _host_number(v: float):
+    # 0 can only mean "never updated" (strict compares, minmax.py:44-47): reference keeps int 0
+    return 0 if v == 0.0 else v
+
+
+@register_class
+class MinMaxObserver(BaseObserver):
+    def __init__(self, symmetric=True, num_bits=8, eps=1e-8):
+        self.symmetric = symmetric
+        self.eps = eps
+        self.num_bits = num_bits
+        self._state = None          # device fp32[2]: running (min_val, max_val)
+        self._host = [0, 0]         # host mirror, valid when not self._dirty
+        self._dirty = False
+
+    # ------------------------------------------------------------------ state
+    def _sync(self):
+        if self._dirty:
+            mn, mx = self._state.tolist()
+            self._host = [_host_number(mn), _host_number(mx)]
+            self._dirty = False
+
+    @property
+    def min_val(self):
+        self._sync()
+        return self._host[0]
+
+    @min_val.setter
+    def min_val(self, v):
+        self._set(0, v)
+
+    @property
+    def max_val(self):
+        self._sync()
+        return self._host[1]
+
+    @max_val.setter
+    def max_val(self, v):
+        self._set(1, v)
+
+    def _set(self, i, v):
+        self._sync()
+        self._host[i] = v
+        if self._state is not None:
+            self._state[i] = 0.0 if v is None else float(v)
+
+    def device_state(self, device) -> torch.Tensor:
+        """fp32[2] running (min, max) on ``device`` (created from the host values)."""
+        device = torch.device(device)
+        if self._state is None or self._state.device != device:
+            self._sync()
+            vals = [0.0 if v is None else float(v) for v in self._host]
+            self._state = torch.tensor(vals, dtype=torch.float32, device=device)
+        return self._state
+
+    def reset(self):
+        self._state = None
+        self._host = [0, 0]
+        self._dirty = False
+
+    # ------------------------------------------------------------------ protocol
+    def observe_device(self, x, want_stats=True, want_qp=True):
+        """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device."""
+        state = self.device_state(H.require_device_f32(x).device)
+        qp, st = observe_tensor(x, symmetric=self.symmetric, num_bits=self.num_bits, eps=self.eps,
+                                run_minmax=state, want_qp=want_qp, want_stats=want_stats)
+        self._dirty = True
+        return qp, st
+
+    def observe(self, x):
+        """Update min/max from ``x`` (minmax.py:32-47)."""
+        self.observe_device(x, want_stats=False, want_qp=False)
+
+    def get_scale_zero_point(self):
+        """Host float64 qparams (minmax.py:49-74)."""
+        mn, mx = self.min_val, self.max_val
+        if self.symmetric:
+            max_abs = max(abs(mn), abs(mx))
+            scale = max_abs / (2 ** (self.num_bits - 1) - 1 + self.eps)
+            zero_point = 0
+        else:
+            scale = (mx - mn) / (2 ** self.num_bits - 1 + self.eps)
+            zero_point = round(-mn / (scale + self.eps))
+        return scale, zero_point
+
+    def forward(self, x):
+        """observe + get_scale_zero_point (minmax.py:76-88); one device->host read."""
+        self.observe(x)
+        return self.get_scale_zero_point()
+
+    def __repr__(self):
+        return (f"MinMaxObserver(symmetric={self.symmetric}, num_bits={self.num_bits}, "
+                f"eps={self.eps})")

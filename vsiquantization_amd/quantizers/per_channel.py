@@ -1,0 +1,39 @@
+"""PerChannelUniformQuantizer — UniformQuantizer arithmetic (quantizers/uniform.py:34-56)
+with one (scale, zero point) per out-channel (axis 0), build-defined.
+
+``quantize(x, scale, zero_point, is_learning_scale)`` takes float64 [C] device
+tensors (PerChannelMinMaxObserver's output).  Scalars fall back to the
+per-tensor UniformQuantizer behaviour.  A learnable per-channel scale is the
+"next" row of SURVEY §8f (LSQFakeQuantize-style) and raises for now.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..fakequant import PerChannelFQFn, per_channel_fake_quant
+from ..utils.registry import register_class
+from .uniform import UniformQuantizer
+
+
+def _per_channel(v) -> bool:
+    return isinstance(v, torch.Tensor) and v.dim() == 1 and v.numel() > 1
+
+
+@register_class
+class PerChannelUniformQuantizer(UniformQuantizer):
+    axis = 0
+
+    def quantize(self, x, scale, zero_point, is_learning_scale):
+        if not (_per_channel(scale) or _per_channel(zero_point)):
+            return super().quantize(x, scale, zero_point, is_learning_scale)
+        if is_learning_scale:
+            raise NotImplementedError("learnable per-channel scale: planned (SURVEY §8f row 2)")
+        C = x.shape[0]
+        s = scale if isinstance(scale, torch.Tensor) else torch.full((C,), float(scale), dtype=torch.float64)
+        z = zero_point if isinstance(zero_point, torch.Tensor) else torch.full((C,), float(zero_point),
+                                                                                dtype=torch.float64)
+        if s.numel() != C or z.numel() != C:
+            raise ValueError(f"per-channel qparams have {s.numel()}/{z.numel()} entries, x has {C} channels")
+        if x.requires_grad and torch.is_grad_enabled():
+            return PerChannelFQFn.apply(x, s, z, self.qmin, self.qmax)
+        return per_channel_fake_quant(x, s, z, self.qmin, self.qmax)[0]

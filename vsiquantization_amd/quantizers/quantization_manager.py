@@ -1,0 +1,203 @@
+"""QuantizationManager (reference: quantizers/quantization_manager.py:10-145).
+
+nn.Module owning one quantizer and one observer, built by registry name
+(qm.py:41-42), with the reference's mode flags, attributes and methods:
+``quantizer, observer, scale, zero_point, is_observer_qparam, is_learning_scale,
+is_quantize, is_symmetric (hard-coded True, qm.py:50), bits_width, mean_abs_x,
+mean_x, std``; ``collect_qparameter, quantize, make_learn_qparameter,
+init_scaling_factor_for_learning, winsorized_mean``.
+
+MI355X differences (behaviour-preserving):
+* With this package's observers, ``collect_qparameter`` is sync-free: the observer
+  kernel writes the f64 qparams record on the device and ``self.scale`` /
+  ``self.zero_point`` become 0-dim device tensors that the quantizer kernel reads
+  by pointer (the reference performs five ``.item()`` syncs per call, qm.py:66-69).
+* ``mean_abs_x / mean_x / std`` are kept as device records and materialised into
+  the reference's Python lists of floats on first read (one sync).
+* Per-channel observer + per-channel quantizer in observe+quantize mode run as ONE
+  fused kernel (observe, f64 qparams and fake quant in one read of ``x``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import _hip as H
+from ..fakequant import observe_finalize, observe_tensor, stats_from_row_sums
+from ..observers.minmax import MinMaxObserver
+from ..observers.per_channel import PerChannelMinMaxObserver
+from ..utils.registry import CLASS_REGISTRY
+from .per_channel import PerChannelUniformQuantizer
+
+_STAT_NAMES = ("mean_abs_x", "mean_x", "std")
+
+
+class _StatList:
+    """Property backing one of mean_abs_x / mean_x / std (a Python list of floats)."""
+
+    def __init__(self, idx):
+        self.idx = idx
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return self
+        obj._materialize_stats()
+        return obj._host_stats[self.idx]
+
+    def __set__(self, obj, value):
+        obj._materialize_stats()
+        obj._host_stats[self.idx] = value
+
+
+class QuantizationManager(nn.Module):
+    mean_abs_x = _StatList(0)
+    mean_x = _StatList(1)
+    std = _StatList(2)
+
+    def __init__(self, quantizer_name: str, observer_name: str, bits_width: int, is_symmetric: bool,
+                 is_learning_scale: bool = True) -> None:
+        super().__init__()
+        self.quantizer = CLASS_REGISTRY[quantizer_name](bits_width, is_symmetric)
+        self.observer = CLASS_REGISTRY[observer_name](is_symmetric)
+        self.is_learning_scale = is_learning_scale
+        self.bits_width = bits_width
+        self.scale = 1
+        self.zero_point = 0
+        self.is_observer_qparam = True
+        self.is_quantize = True
+        self.is_symmetric = True   # reference quirk (qm.py:50): observer/quantizer keep their own flag
+        self._dev_stats = []       # pending device records f64[3] (mean|x|, mean, std)
+        self._host_stats = [[], [], []]
+        # multi-GPU observer (vsiquantization_amd.distributed): process group, deferred mode
+        self.dist_group = None
+        self.dist_defer = False
+        self._pending_records = []   # deferred: local per-call stats records f64[ST_LEN]
+        self._calib_init = None
+        self.mean_abs_x = []
+        self.mean_x = []
+        self.std = []
+
+    # ------------------------------------------------------------------ stats records
+    def _materialize_stats(self):
+        pend = self.__dict__.get("_dev_stats")
+        if pend:
+            rows = torch.stack(pend).cpu().tolist()
+            self.__dict__["_dev_stats"] = []
+            for r in rows:
+                for i in range(3):
+                    self._host_stats[i].append(r[i])
+
+    def _record_stats(self, st3: torch.Tensor):
+        self._dev_stats.append(st3)
+
+    # ------------------------------------------------------------------ observe
+    def _device_observer(self, x) -> bool:
+        return (isinstance(x, torch.Tensor) and x.device.type == "cuda"
+                and isinstance(self.observer, (MinMaxObserver, PerChannelMinMaxObserver)))
+
+    def collect_qparameter(self, x):
+        """Observe ``x`` and refresh scale/zero_point when calibrating (qm.py:55-71)."""
+        if self.is_learning_scale or not self.is_observer_qparam:
+            return
+        if self._device_observer(x):
+            if isinstance(self.observer, PerChannelMinMaxObserver):
+                rs = self.observer.observe(x, want_row_stats=True)
+                self._record_stats(stats_from_row_sums(rs, x.numel()))
+                self.scale, self.zero_point = self.observer.get_scale_zero_point()
+            elif self.dist_group is not None:
+                self._collect_distributed(x)
+            else:
+                qp, st = self.observer.observe_device(x)
+                self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+                self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+            return
+        # third-party observer: the reference's host path
+        xd = x.detach()
+        self._materialize_stats()
+        self._host_stats[0].append(torch.mean(torch.abs(xd)).cpu().item())
+        self._host_stats[1].append(torch.mean(xd).cpu().item())
+        self._host_stats[2].append(torch.std(xd).cpu().item())
+        self.scale, self.zero_point = self.observer.forward(x)
+
+    # ------------------------------------------------------------------ multi-GPU observer
+    def _collect_distributed(self, x):
+        from ..distributed import allreduce_stats
+        obs = self.observer
+        _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
+                               run_minmax=None, want_qp=False, want_stats=True)
+        if self.dist_defer:
+            if self.is_quantize:
+                raise RuntimeError("deferred observer sync (dist_defer) needs is_quantize=False "
+                                   "(calibration); use per-call mode to quantize while observing")
+            if not self._pending_records:
+                self._calib_init = (obs.min_val, obs.max_val)
+            self._pending_records.append(st)
+            return
+        allreduce_stats(st, group=self.dist_group)
+        state = obs.device_state(x.device)
+        qp = observe_finalize(st, state, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps)
+        obs._dirty = True
+        self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+        self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+
+    def _apply_synced_records(self, recs):
+        """recs: CPU f64 [k, ST_LEN], already all-reduced; replay the running state."""
+        from ..distributed import replay_minmax
+        mn, mx = self._calib_init
+        mn, mx = replay_minmax(mn, mx, recs[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
+        self.observer.min_val, self.observer.max_val = mn, mx
+        self._materialize_stats()
+        for i, col in enumerate((H.ST_MEANABS, H.ST_MEAN, H.ST_STD)):
+            self._host_stats[i].extend(recs[:, col].tolist())
+        self._pending_records = []
+        self._calib_init = None
+        self.scale, self.zero_point = self.observer.get_scale_zero_point()
+
+    def quantize(self, x):
+        """collect_qparameter, then fake-quantize when enabled (qm.py:73-90)."""
+        if (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
+                and isinstance(self.observer, PerChannelMinMaxObserver)
+                and isinstance(self.quantizer, PerChannelUniformQuantizer) and self._device_observer(x)):
+            # fused per-channel observe + quantize: one read, one write of x
+            y, rs = self.observer.observe_quantize(x, self.quantizer, want_row_stats=True)
+            self._record_stats(stats_from_row_sums(rs, x.numel()))
+            self.scale, self.zero_point = self.observer.get_scale_zero_point()
+            return y
+        self.collect_qparameter(x)
+        if self.is_quantize:
+            return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale)
+        return x
+
+    # ------------------------------------------------------------------ learnable qparams
+    def make_learn_qparameter(self):
+        """scale -> nn.Parameter (qm.py:92-103); float64 when it came from the learn init."""
+        s = self.scale
+        s = s.detach().clone() if isinstance(s, torch.Tensor) else torch.tensor(s)
+        self.scale = nn.Parameter(s, requires_grad=True)
+        learn_zp = (not self.is_symmetric) or getattr(self.quantizer, "learns_zero_point", False)
+        if learn_zp:
+            z = self.zero_point
+            z = (z.detach().to(torch.float64).clone() if isinstance(z, torch.Tensor)
+                 else torch.tensor(float(z), dtype=torch.float64))
+            self.zero_point = nn.Parameter(z + 1e-9, requires_grad=True)
+        else:
+            self.zero_point = 0
+
+    def init_scaling_factor_for_learning(self):
+        """scale = 2 * mean(mean_abs_x) / sqrt(2^(b-1) - 1)  (qm.py:105-112)."""
+        self.scale = 2 * np.mean(self.mean_abs_x) / np.sqrt(2 ** (self.bits_width - 1) - 1)
+
+    def winsorized_mean(self, x, lower=5, upper=95, sample_size=1000000):
+        """Trimmed mean of x between two percentiles (qm.py:116-145; unused by the reference)."""
+        flat = x.flatten()
+        sample = flat[torch.randperm(flat.numel(), device=flat.device)[:sample_size]] \
+            if flat.numel() > sample_size else flat
+        lo = torch.quantile(sample, lower / 100)
+        hi = torch.quantile(sample, upper / 100)
+        return flat[(flat >= lo) & (flat <= hi)].mean()
+
+    def extra_repr(self):
+        return (f"quantizer={self.quantizer!r}, observer={self.observer!r}, bits={self.bits_width}, "
+                f"observe={self.is_observer_qparam}, learn={self.is_learning_scale}, "
+                f"quantize={self.is_quantize}")

@@ -1,0 +1,113 @@
+"""UniformQuantizer on MI355X (reference: quantizers/uniform.py:7-102, 242-271).
+
+Same registry name, constructor ``(num_bits=8, symmetric=True)``, attributes
+(``num_bits, symmetric, qmin, qmax, calib_grad_scale``) and ``quantize``
+protocol as the reference; the arithmetic runs in the HIP kernels of
+``vsiquantization_amd.fakequant`` (bit-exact with the reference's CPU path):
+
+* fixed qparams (``is_learning_scale=False``): one launch (K1), STE backward
+  from a saved uint8 mask;
+* learnable (``is_learning_scale=True``): forward K1 reading the f64 scale
+  Parameter on the device, backward K4 (grad_x + f64 scale/zp gradients with the
+  reference's ScaleGradient factor).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..fakequant import FakeQuantLearnFn, fake_quant, fake_quant_fixed
+from ..utils.registry import register_class
+from .base import BaseQuantizer
+
+
+class ScaleGradient(torch.autograd.Function):
+    """Identity forward; backward multiplies the gradient by ``scale`` (uniform.py:242-255)."""
+
+    @staticmethod
+    def forward(ctx, x, scale):
+        ctx.scale = scale
+        return x
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad * ctx.scale, None
+
+
+class RoundStraightThrough(torch.autograd.Function):
+    """round() forward, identity backward (uniform.py:258-271)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return torch.round(x)
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad
+
+
+def _reduce_gscale(g):
+    """calib_grad_scale may be a per-channel tensor (utils/estimate_bn.py:136); the
+    reference then reduces ScaleGradient's tensor-valued gradient onto the 0-dim
+    scale (sum_to), i.e. the effective factor is the sum."""
+    if isinstance(g, torch.Tensor):
+        return float(g.detach().to(torch.float64).sum().item())
+    return float(g)
+
+
+@register_class
+class UniformQuantizer(BaseQuantizer):
+    #: zero point becomes a learnable tensor in QuantizationManager.make_learn_qparameter
+    #: only for quantizers that set this (the reference manager never does: qm.py:50,100-103)
+    learns_zero_point = False
+
+    def __init__(self, num_bits=8, symmetric=True):
+        self.num_bits = num_bits
+        self.symmetric = symmetric
+        if symmetric:
+            self.qmin, self.qmax = -(2 ** (num_bits - 1)), 2 ** (num_bits - 1) - 1
+        else:
+            self.qmin, self.qmax = 0, 2 ** num_bits - 1
+        self.calib_grad_scale = 1
+
+    # ------------------------------------------------------------------ protocol
+    def quantize(self, x, scale, zero_point, is_learning_scale):
+        """Fake-quantize ``x`` (uniform.py:34-56): ``(clamp(round(x/s+zp)) - zp) * s``."""
+        if not is_learning_scale:
+            return fake_quant_fixed(x, scale, zero_point, self.qmin, self.qmax)
+        gscale = _reduce_gscale(self.calculate_grad_scale(x) * self.calib_grad_scale)
+        learn_zp = not self.symmetric
+        if learn_zp and not isinstance(zero_point, torch.Tensor):
+            zero_point = self._int_zero_point_learnable(zero_point)
+            learn_zp = isinstance(zero_point, torch.Tensor)
+        if not learn_zp and isinstance(zero_point, torch.Tensor) and zero_point.requires_grad:
+            raise NotImplementedError("a gradient-requiring zero point with a symmetric learnable "
+                                      "quantizer is not supported")
+        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp)
+
+    def _int_zero_point_learnable(self, zero_point):
+        # Reference behaviour (uniform.py:50-52 -> :100 -> :267): torch.round(<int>) raises.
+        raise TypeError(
+            "round(): argument 'input' must be Tensor, not int — the reference UniformQuantizer "
+            "cannot learn an integer zero point (asymmetric + is_learning_scale); use LSQQuantizer")
+
+    def calculate_grad_scale(self, quant_tensor):
+        """(qmax * numel) ** -0.5 (uniform.py:58-71)."""
+        return (self.qmax * quant_tensor.numel()) ** -0.5
+
+    def scale_grad_func(self):
+        return ScaleGradient.apply
+
+    def discretizer(self):
+        return RoundStraightThrough.apply
+
+    def discreate_tensor(self, x, scale, zero_point, quant_min, quant_max):
+        """Integer codes as an fp32 tensor: clamp(round(x/s+zp), qmin, qmax) (uniform.py:81-96)."""
+        return fake_quant(x, scale, zero_point, quant_min, quant_max, discrete=True)[0]
+
+    def zero_point_rounding(self, zero_point):
+        """clamp(round(zp), qmin, qmax) with a straight-through gradient (uniform.py:98-102)."""
+        return torch.clamp(RoundStraightThrough.apply(zero_point), self.qmin, self.qmax)
+
+    def __repr__(self):
+        return (f"{type(self).__name__}(num_bits={self.num_bits}, symmetric={self.symmetric}, "
+                f"qmin={self.qmin}, qmax={self.qmax})")

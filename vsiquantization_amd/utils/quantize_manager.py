@@ -1,0 +1,69 @@
+"""QAT lifecycle switches (reference: utils/quantize_manager.py:4-117).
+
+Layers are found by duck typing (``hasattr(module, "weight_quantizer")`` /
+``"activation_quantizer"``) exactly like the reference, and the three manager
+flags select the kernel branch:
+
+  calibrate_qat_model       observe only        (K2 / K3 observe, no fake quant)
+  activate_learning_qparam  learn-init + Parameters  (K1 fwd + K4 bwd from then on)
+  activate_quantizer        fake quant on
+"""
+
+
+def _managers(module):
+    for attr in ("weight_quantizer", "activation_quantizer"):
+        if hasattr(module, attr):
+            yield getattr(module, attr)
+
+
+def calibrate_qat_model(model, dataloader, data_calib, device=None):
+    """Observe-only mode on every manager, eval(), then ``data_calib(model, dataloader, device)``."""
+    for module in model.modules():
+        for qm in _managers(module):
+            qm.is_observer_qparam = True
+            qm.is_learning_scale = False
+            qm.is_quantize = False
+    model.eval()
+    data_calib(model, dataloader, device)
+
+
+def activate_learning_qparam(model, layer_names=None, use_init=True, active=True):
+    """Set ``is_learning_scale``; optionally re-init scale from mean|x|; make Parameters."""
+    for name, module in model.named_modules():
+        if layer_names is not None and name not in layer_names:
+            continue
+        for qm in _managers(module):
+            qm.is_learning_scale = active
+            if use_init:
+                qm.init_scaling_factor_for_learning()
+            if active:
+                qm.make_learn_qparameter()
+
+
+def deactivate_learning_qparam(model, layer_names=None):
+    activate_learning_qparam(model, layer_names=layer_names, active=False)
+
+
+def activate_quantizer(model, layer_names=None, active=True):
+    for name, module in model.named_modules():
+        if layer_names is not None and name not in layer_names:
+            continue
+        for qm in _managers(module):
+            qm.is_quantize = active
+
+
+def deactivate_quantizer(model, layer_names=None):
+    activate_quantizer(model, layer_names=layer_names, active=False)
+
+
+def data_calib(model, calib_loader, device, num_batches=16):
+    """Restatement of yolov8_qat.py:42-52: eval, <=16 batches of uint8 images / 255, train().
+
+    ``calib_loader`` yields ``(imgs, targets)`` with uint8 NCHW images."""
+    model.eval()
+    model.to(device)
+    for i, (imgs, _targets) in enumerate(calib_loader):
+        model(imgs.to(device, non_blocking=True).float() / 255.0)
+        if i == num_batches - 1:
+            break
+    model.train()
