@@ -103,10 +103,10 @@ class C2PerChannel:
         """Cheap self-check of slot 0 against the observer-free closed form (no oracle import)."""
         s = self.slots[0]
         x = s["x"].reshape(self.shape[0], -1)
-        mn = torch.minimum(x.min(1).values, torch.zeros(()).to(x))
-        mx = torch.maximum(x.max(1).values, torch.zeros(()).to(x))
-        scale = (mx.double() - mn.double()) / (255 + 1e-8)
-        return bool(torch.equal(scale, s["scale"]))
+        mn = torch.clamp(x.min(1).values, max=0.0).double().cpu()
+        mx = torch.clamp(x.max(1).values, min=0.0).double().cpu()
+        scale = (mx - mn) / (255 + 1e-8)   # host f64 division (torch-GPU would use a reciprocal)
+        return bool(torch.equal(scale, s["scale"].cpu()))
 
 
 class C3Lsq:

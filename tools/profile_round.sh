@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of bench.py (both workloads), then separate PMC passes
+# for FETCH_SIZE and WRITE_SIZE (never combined with other trace domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+TAG=${TAG:-r01}
+run() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a gpurun_out/steps.log
+  return $rc
+}
+export TMPDIR=/tmp
+for W in ${WORKLOADS:-c2 c3}; do
+  run bench_$W 600 python3 -u bench.py --workload $W --steps 200 --warmup 20 ${BENCH_EXTRA:-} || exit $?
+  run prof_$W 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$W -o run --output-format csv \
+      -- python3 -u bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline || exit $?
+  for C in FETCH_SIZE WRITE_SIZE; do
+    run pmc_${W}_$C 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${TAG}_${W}_$C -o run --output-format csv \
+        -- python3 -u bench.py --workload $W --steps 40 --warmup 5 --no-cpu-baseline || exit $?
+  done
+done
+exit 0
