@@ -74,7 +74,7 @@ class C2PerChannel:
             gen.manual_seed(seed_base + 2 * i + 1)
             g = torch.randn(self.shape, device=dev, generator=gen)
             s = dict(x=x, g=g, y=torch.empty_like(x), gx=torch.empty_like(x),
-                     mask=torch.empty(self.shape, dtype=torch.uint8, device=dev),
+                     mask=H.mask_buffer(C, self.n // C, dev),
                      rmin=torch.zeros(C, device=dev), rmax=torch.zeros(C, device=dev),
                      scale=torch.empty(C, dtype=torch.float64, device=dev),
                      zp=torch.empty(C, dtype=torch.float64, device=dev))
@@ -85,18 +85,27 @@ class C2PerChannel:
             self.slots.append(s)
         self.f_fwd = lib.vsiq_pc_observe_fq_f32
         self.f_bwd = lib.vsiq_ste_bwd_f32
-        self.kernels = {"pc_observe_fq_fwd": 9 * n, "ste_bwd": 9 * n}   # algorithmic bytes / launch
+        mbytes = 8 * int(lib.vsiq_mask_words(C, self.rowlen))   # 1 bit / element
+        # algorithmic bytes per launch: fwd reads W, writes Y + mask bits; bwd reads G + mask bits,
+        # writes dW (per-row qparams/state: 1024 x 24 B, negligible and not counted)
+        self.kernels = {"pc_observe_fq_fwd": 8 * n + mbytes, "ste_bwd": 8 * n + mbytes}
 
-    def launch(self, i, ev=None):
+    def launch(self, i):
         s = self.slots[i % len(self.slots)]
-        if ev is not None:
-            ev[0].record()
-        rc = self.f_fwd(*s["fwd"])
-        if ev is not None:
-            ev[1].record()
-        rc |= self.f_bwd(*s["bwd"])
-        if ev is not None:
-            ev[2].record()
+        return self.f_fwd(*s["fwd"]) | self.f_bwd(*s["bwd"])
+
+    def launch_group(self, i0, cnt, ev):
+        """cnt steps (slots i0..i0+cnt-1): all forwards, then all backwards (each slot's
+        backward still follows its forward on the stream); events bracket each kernel run."""
+        ns = len(self.slots)
+        rc = 0
+        ev[0].record()
+        for j in range(cnt):
+            rc |= self.f_fwd(*self.slots[(i0 + j) % ns]["fwd"])
+        ev[1].record()
+        for j in range(cnt):
+            rc |= self.f_bwd(*self.slots[(i0 + j) % ns]["bwd"])
+        ev[2].record()
         return rc
 
     def check(self):
@@ -147,6 +156,7 @@ class C3Lsq:
         self.kernels = {"fq_fwd": 8 * n, "lsq_bwd": 12 * n}
 
     launch = C2PerChannel.launch
+    launch_group = C2PerChannel.launch_group
 
     def check(self):
         return True
@@ -215,14 +225,16 @@ def main():
     torch.cuda.synchronize()
     ok = W.check()
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    ns = len(W.slots)
+    groups = [(g0, min(ns, a.steps - g0)) for g0 in range(0, a.steps, ns)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in groups]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rc = 0
-    for i in range(a.steps):
-        rc |= W.launch(i, evs[i])
+    for (g0, cnt), ev in zip(groups, evs):
+        rc |= W.launch_group(g0, cnt, ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

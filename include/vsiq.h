@@ -23,9 +23,15 @@
  *     that is 0 before the first call; every reducing kernel resets it to 0
  *     when it finishes (stream-ordered reuse is safe, concurrent reuse on two
  *     streams is not).
- *   - Masks are uint8 (1 = value was inside [qmin, qmax] after rounding,
- *     ClampBackward1 semantics), codes are int8 (symmetric) or uint8
- *     (asymmetric) holding clamp(round(x/s+zp)); NaN inputs give code 0.
+ *   - Straight-through masks are ONE BIT per element (1 = the rounded value was
+ *     inside [qmin, qmax], ClampBackward1 semantics), packed in uint64 words:
+ *     a tensor is viewed as `rows` rows of `rowlen` elements (per-tensor: one
+ *     row of n); row r owns words [r*W, (r+1)*W) with W = 4*ceil(rowlen/256);
+ *     element e of a row lives in word 4*(e/256) + (e%4), bit (e%256)/4.
+ *     (That is the wave64 ballot of "element j of each lane's 4-group".)
+ *     vsiq_mask_words(rows, rowlen) gives the word count; 8-byte alignment.
+ *   - Codes are int8 (symmetric) or uint8 (asymmetric) holding
+ *     clamp(round(x/s+zp)); NaN inputs give code 0.
  */
 #ifndef VSIQ_H_
 #define VSIQ_H_
@@ -68,6 +74,25 @@ const char *vsiq_error_string(int code);
 /* float64 workspace entries needed by the reducing kernels for n elements */
 int64_t vsiq_workspace_doubles(int64_t n);
 
+/* uint64 words of a 1-bit mask for `rows` rows of `rowlen` elements */
+int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
+
+/* Performance knobs (process-wide; results are identical for every setting). */
+#define VSIQ_TUNE_PC_ROWS_PER_BLOCK 1  /* K3 rows per workgroup, 0 = auto */
+#define VSIQ_TUNE_NONTEMPORAL 2        /* 1 = nontemporal streamed loads/stores (default) */
+#define VSIQ_TUNE_FLAT_GRID_CAP 3      /* max workgroups of flat streaming kernels (8192) */
+#define VSIQ_TUNE_LSQ_PREFETCH 4       /* 1 = K4 software prefetch (default) */
+int vsiq_set_tuning(int key, int value);
+
+/*
+ * Self-test of the kernels' correctly rounded division x / s (reciprocal +
+ * two Newton-Markstein corrections, IEEE fallback outside the proven range):
+ * for each of `count` divisors, every one of the 2^32 fp32 dividends is divided
+ * both ways and mismatches[k] (uint64, zeroed by the caller) += bitwise differences.
+ */
+int vsiq_selftest_div(const float *divisors, int count, unsigned long long *mismatches,
+                      void *stream);
+
 /*
  * Per-tensor fake-quant forward (K1).
  * Replaces quantizers/uniform.py:54-55 + :95 (discreate_tensor):
@@ -77,11 +102,12 @@ int64_t vsiq_workspace_doubles(int64_t n);
  *   - *scale_dev (f64, a learnable 0-dim Parameter) if scale_dev != NULL, else scale_host;
  *   - *zp_dev (f64) if zp_dev != NULL, else zp_host; zp_round != 0 applies
  *     clamp(rint(zp), qmin, qmax) first (learnable tensor zp, uniform.py:98-102).
- * codes (int8/uint8, nullable) and mask (uint8, nullable) are optional outputs.
+ * codes (int8/uint8, nullable) and mask (1-bit words, one row of n, nullable) are
+ * optional outputs.
  * discrete != 0 writes the integer-valued fp32 clamp(round(x/s+zp)) into y instead
  * (UniformQuantizer.discreate_tensor, uniform.py:81-96).
  */
-int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint8_t *mask, int64_t n,
+int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t n,
                     const double *qp_dev, const double *scale_dev, double scale_host,
                     const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
                     int qmax, void *stream);
@@ -125,7 +151,7 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
  * y == NULL observes only (codes/mask must then be NULL too).
  * One read and one write of every element.
  */
-int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint8_t *mask,
+int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint64_t *mask,
                            int64_t rows, int64_t rowlen, float *run_min, float *run_max,
                            double *scale_out, double *zp_out, double *row_stats, int symmetric,
                            int qmin, int qmax, double qden, double eps, void *stream);
@@ -134,7 +160,7 @@ int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint8_t *mask,
  * Per-channel fake-quant forward with given per-row qparams (f64 [rows]).
  * zp_round != 0 applies clamp(rint(zp)) first (learnable zp, uniform.py:98-102).
  */
-int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint8_t *mask, int64_t rows,
+int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
                        int64_t rowlen, const double *scale, const double *zp, int zp_round,
                        int qmin, int qmax, void *stream);
 
@@ -144,9 +170,9 @@ int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint8_t *mask, int
  * uniform.py:55,95 with a Python-float scale:
  *   gx = (mask ? g*s : 0) / s      (fp32, bit-exact)
  * s = fp32(scale_dev[i / rowlen]) if scale_dev != NULL (rowlen elements per entry), else
- * fp32(scale_host).
+ * fp32(scale_host) and one row of n.  `mask` uses the same rows/rowlen layout.
  */
-int vsiq_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t n,
+int vsiq_ste_bwd_f32(const float *g, const uint64_t *mask, float *gx, int64_t n,
                      const double *scale_dev, int64_t rowlen, double scale_host, void *stream);
 
 /*

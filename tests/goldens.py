@@ -44,3 +44,13 @@ def assert_bitwise_f32(got, want, what=""):
         i = bad[0]
         raise AssertionError(f"{what}: {bad.size} of {gb.size} elements differ bitwise; first: "
                              f"got {got[~gn][i]!r} want {want[~wn][i]!r}")
+
+
+def unpack_mask(words, rows, rowlen):
+    """1-bit straight-through mask (include/vsiq.h layout) -> bool [rows, rowlen]."""
+    W = 4 * -(-rowlen // 256)
+    w = np.asarray(words).view(np.uint64)[: rows * W].reshape(rows, W)
+    e = np.arange(rowlen)
+    word = 4 * (e // 256) + (e % 4)
+    bit = ((e % 256) // 4).astype(np.uint64)
+    return ((w[:, word] >> bit) & np.uint64(1)).astype(bool)

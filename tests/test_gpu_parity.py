@@ -195,7 +195,9 @@ def test_per_channel_vs_oracle(shape, sym, bits):
     codes = FQ.per_channel_observe_fq(cu(w), symmetric=sym, qmin=q.qmin, qmax=q.qmax,
                                       want_codes=True, want_mask=True)
     assert np.array_equal(npy(codes["codes"]).astype(np.int64), ref["x_int"].astype(np.int64))
-    assert np.array_equal(npy(codes["mask"]).astype(bool), ref["mask"])
+    C = shape[0]
+    m = G.unpack_mask(npy(codes["mask"]), C, w.size // C)
+    assert np.array_equal(m, ref["mask"].reshape(C, -1))
 
 
 def test_per_channel_fwd_bwd_c2_full():
@@ -300,6 +302,34 @@ def test_reductions_deterministic():
         _, grads = FQ.lsq_backward(g, x, 0.05, 0, -128, 127, 1e-3, False)
         outs.append((npy(st).tobytes(), npy(grads).tobytes()))
     assert outs[0] == outs[1] == outs[2]
+
+
+def test_fast_division_exhaustive():
+    """The kernels' reciprocal + Newton-Markstein division equals IEEE x/s for ALL 2^32 x."""
+    rng = np.random.default_rng(3)
+    divs = [1.0, 3.0, 0.1, 0.03, 1.9999999, 1.0000001, 2.0 ** -60, 2.0 ** 60, 7.0e-3,
+            np.float32(np.nextafter(np.float32(2), np.float32(0))), 255.00001, 0.0, -0.5,
+            float("inf"), 1e-30, 3.4e38] + list(rng.uniform(1e-4, 10.0, 8))
+    b = torch.tensor(np.asarray(divs, np.float32), device=DEV)
+    bad = torch.zeros(len(divs), dtype=torch.int64, device=DEV)
+    H.check(H.lib().vsiq_selftest_div(H.ptr(b), len(divs), H.ptr(bad), H.stream_of(b.device)),
+            "vsiq_selftest_div")
+    assert npy(bad).tolist() == [0] * len(divs)
+
+
+def test_tail_groups_and_mask_bits_per_tensor():
+    """n % 4 != 0 and n % 256 != 0: scalar groups, partial ballots."""
+    for n in (5, 255, 257, 1001, 4099):
+        x = _rand(n, n, 3.0)
+        g = _rand(n, n + 1)
+        q = V.UniformQuantizer(4, False)
+        y, mask, codes = FQ.fake_quant(cu(x), 0.4, 3, q.qmin, q.qmax, want_mask=True, want_codes=True)
+        yo, qo, mo = O.fq_forward(x, 0.4, 3, q.qmin, q.qmax)
+        G.assert_bitwise_f32(npy(y), yo, "y")
+        assert np.array_equal(G.unpack_mask(npy(mask), 1, n)[0], mo)
+        assert np.array_equal(npy(codes).astype(np.int64), qo.astype(np.int64))
+        gx = FQ.ste_backward(cu(g), mask, 0.4)
+        G.assert_bitwise_f32(npy(gx), O.fq_backward_fixed(g, mo, 0.4), "gx")
 
 
 def test_cpu_tensor_fails_loudly():

@@ -32,11 +32,15 @@ ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, 
 ST_LEN = 10
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
+TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_FLAT_GRID_CAP, TUNE_LSQ_PREFETCH = 1, 2, 3, 4
 
 _SIGS = {
     "vsiq_abi_version": ([], c_int),
     "vsiq_error_string": ([c_int], ctypes.c_char_p),
     "vsiq_workspace_doubles": ([c_i64], c_i64),
+    "vsiq_mask_words": ([c_i64, c_i64], c_i64),
+    "vsiq_set_tuning": ([c_int, c_int], c_int),
+    "vsiq_selftest_div": ([c_p, c_int, c_p, c_p], c_int),
     "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
                         c_int),
     "vsiq_observe_f32": ([c_p, c_i64, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p], c_int),
@@ -101,6 +105,16 @@ def require_device_f32(x: torch.Tensor, what: str = "x") -> torch.Tensor:
     if x.dtype != torch.float32:
         raise TypeError(f"{what}: only float32 is supported by the HIP fake-quant path, got {x.dtype}")
     return x.contiguous()
+
+
+def mask_buffer(rows: int, rowlen: int, device) -> torch.Tensor:
+    """1-bit straight-through mask storage (uint64 words, layout in include/vsiq.h)."""
+    words = int(lib().vsiq_mask_words(int(rows), int(rowlen)))
+    return torch.empty(max(words, 1), dtype=torch.int64, device=device)
+
+
+def set_tuning(key: int, value: int):
+    check(lib().vsiq_set_tuning(int(key), int(value)), "vsiq_set_tuning")
 
 
 def ptr(t):

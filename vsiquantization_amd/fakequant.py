@@ -67,7 +67,7 @@ def fake_quant(x: torch.Tensor, scale, zero_point, qmin: int, qmax: int, *, zp_r
     x = H.require_device_f32(x)
     dev = x.device
     y = torch.empty_like(x)
-    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if want_mask else None
+    mask = H.mask_buffer(1, x.numel(), dev) if want_mask else None
     codes = None
     if want_codes:
         codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
@@ -223,7 +223,7 @@ def per_channel_observe_fq(x: torch.Tensor, *, symmetric: bool, qmin: int, qmax:
     y = torch.empty_like(x) if quantize else None
     scale = torch.empty(C, dtype=torch.float64, device=dev)
     zp = torch.empty(C, dtype=torch.float64, device=dev)
-    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if (want_mask and quantize) else None
+    mask = H.mask_buffer(C, rowlen, dev) if (want_mask and quantize) else None
     codes = (torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
              if (want_codes and quantize) else None)
     rstats = torch.empty(C, 3, dtype=torch.float64, device=dev) if want_row_stats else None
@@ -255,7 +255,7 @@ def per_channel_fake_quant(x, scale: torch.Tensor, zp: torch.Tensor, qmin, qmax,
     dev = x.device
     C = x.shape[0]
     y = torch.empty_like(x)
-    mask = torch.empty(x.shape, dtype=torch.uint8, device=dev) if want_mask else None
+    mask = H.mask_buffer(C, x.numel() // C, dev) if want_mask else None
     codes = (torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
              if want_codes else None)
     s = scale.detach().to(dev, torch.float64).contiguous()
