@@ -26,17 +26,19 @@ def measure(W, steps=64):
 res = {}
 c2 = bench.C2PerChannel(dev, 8, 0)
 for rnd in range(3):
-    for rpb, nt in itertools.product((1, 2, 4), (0, 1)):
+    for bs, rpb, nt in itertools.product((256, 512, 1024), (1, 2), (0, 1)):
+        H.set_tuning(H.TUNE_PC_BLOCK, bs)
         H.set_tuning(H.TUNE_PC_ROWS_PER_BLOCK, rpb)
         H.set_tuning(H.TUNE_NONTEMPORAL, nt)
-        res.setdefault(f"c2 rpb{rpb} nt{nt}", []).append(measure(c2))
+        res.setdefault(f"c2 bs{bs} rpb{rpb} nt{nt}", []).append(measure(c2))
+H.set_tuning(H.TUNE_PC_BLOCK, 0)
 H.set_tuning(H.TUNE_PC_ROWS_PER_BLOCK, 0)
 H.set_tuning(H.TUNE_NONTEMPORAL, 1)
 del c2
 torch.cuda.empty_cache()
 c3 = bench.C3Lsq(dev, 2, 0)
 for rnd in range(3):
-    for pf, nt, cap in itertools.product((0, 1), (0, 1), (2048, 8192)):
+    for pf, nt, cap in itertools.product((0, 1), (1,), (2048,)):
         H.set_tuning(H.TUNE_LSQ_PREFETCH, pf)
         H.set_tuning(H.TUNE_NONTEMPORAL, nt)
         H.set_tuning(H.TUNE_FLAT_GRID_CAP, cap)

@@ -1,7 +1,9 @@
 """Build the in-tree HIP shared library (gfx950) — `python -m vsiquantization_amd._build`.
 
-One translation unit, compiled by hipcc straight into `_vsiq_hip.so` next to this
-file, so the built library travels with the repository snapshot to the GPU box.
+The kernels are split over a few translation units (csrc/*.hip) that hipcc
+compiles in parallel to objects under build/, then links into `_vsiq_hip.so`
+next to this file, so the built library travels with the repository snapshot to
+the GPU box.
 Flags that matter for parity with the reference's CPU arithmetic:
   -ffp-contract=off                       no FMA contraction of (q - zp) * s etc.
   -fhip-fp32-correctly-rounded-divide-sqrt   IEEE x / s
@@ -10,14 +12,17 @@ Flags that matter for parity with the reference's CPU arithmetic:
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "vsiq_kernels.hip")
+CSRC = os.path.join(HERE, "csrc")
+OBJDIR = os.path.join(ROOT, "build", "vsiq")
 OUT = os.path.join(HERE, "_vsiq_hip.so")
 ARCH = os.environ.get("VSIQ_OFFLOAD_ARCH", "gfx950")
 
@@ -26,7 +31,6 @@ FLAGS = [
     "-O3",
     "-std=c++17",
     "-fPIC",
-    "-shared",
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fno-gpu-flush-denormals-to-zero",
@@ -42,18 +46,46 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build vsiquantization_amd)")
 
 
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _deps():
+    return (sources() + glob.glob(os.path.join(CSRC, "*.cuh"))
+            + [os.path.join(ROOT, "include", "vsiq.h"), os.path.abspath(__file__)])
+
+
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [SRC, os.path.join(ROOT, "include", "vsiq.h"), __file__]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    return any(os.path.getmtime(d) > t for d in _deps() if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), *FLAGS, "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC]
+    os.makedirs(OBJDIR, exist_ok=True)
+    cc = hipcc()
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    newest_dep = max(os.path.getmtime(d) for d in _deps() if d.endswith((".cuh", ".h", ".py")))
+
+    def compile_one(src):
+        obj = os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
+        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
+                and os.path.getmtime(obj) > newest_dep):
+            return obj
+        cmd = [cc, *FLAGS, *inc, "-c", "-o", obj + ".tmp", src]
+        if verbose:
+            print("[vsiq build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+        return obj
+
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     if verbose:
         print("[vsiq build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

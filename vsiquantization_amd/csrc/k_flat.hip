@@ -1,0 +1,467 @@
+// k_flat.hip — per-tensor kernels: K1 fake-quant forward, K2 observer, K4 LSQ
+// backward, the division self-test, and the library-level C ABI entry points.
+#include "vsiq_common.cuh"
+
+namespace vsiq {
+
+Tuning g_tune;
+
+// ----------------------------------------------------------------------------
+// K1: per-tensor fake-quant forward (flat, grid-stride over 4-element groups)
+// ----------------------------------------------------------------------------
+template <bool VEC, bool NT, bool CODES, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
+                                                   uint8_t *__restrict__ codes,
+                                                   uint64_t *__restrict__ mask, int64_t n,
+                                                   QPSrc src) {
+  const QP p = load_qp(src);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t stride = (int64_t)gridDim.x * kBlock;   // multiple of 64: lanes stay chunk-aligned
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x % kWave < ng;
+       i += stride) {
+    const bool in = i < ng;
+    Elem e0{}, e1{}, e2{}, e3{};
+    if (in) {
+      const f4 v = load_group<VEC, NT>(x, i, n);
+      e0 = fq_elem(v.x, p);
+      e1 = fq_elem(v.y, p);
+      e2 = fq_elem(v.z, p);
+      e3 = fq_elem(v.w, p);
+      f4 o;
+      o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
+      store_group<VEC, NT>(y, i, n, o);
+      if (CODES) {
+        const uint32_t c = e0.code | (e1.code << 8) | (e2.code << 16) | (e3.code << 24);
+        if (VEC) reinterpret_cast<uint32_t *>(codes)[i] = c;
+        else
+          for (int j = 0; j < valid_in_group(i, n); ++j) codes[4 * i + j] = (uint8_t)(c >> (8 * j));
+      }
+    }
+    if (MASK) {
+      const int nv = in ? valid_in_group(i, n) : 0;
+      store_mask_chunk(mask + 4 * (i / kWave), e0.m && nv > 0, e1.m && nv > 1, e2.m && nv > 2,
+                       e3.m && nv > 3);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K2: per-tensor observer (min, max, NaN count, sum|x|, sum x, sum x^2)
+// ----------------------------------------------------------------------------
+struct ObsAcc {
+  float mn, mx;
+  uint32_t nan;
+  double sa, s1, s2;
+};
+
+__device__ __forceinline__ void obs_init(ObsAcc &a) {
+  a.mn = __builtin_inff();
+  a.mx = -__builtin_inff();
+  a.nan = 0;
+  a.sa = a.s1 = a.s2 = 0.0;
+}
+
+// fminf/fmaxf skip NaN operands; NaNs are counted separately.  nv valid lanes.
+__device__ __forceinline__ void obs_add4(ObsAcc &a, f4 v, int nv) {
+  if (nv < 4) {   // tail group: replicate element 0 for min/max, zero for the sums
+    const float z0 = v.x;
+    v.y = nv > 1 ? v.y : z0;
+    v.z = nv > 2 ? v.z : z0;
+    v.w = nv > 3 ? v.w : z0;
+  }
+  a.mn = fminf(fminf(a.mn, v.x), fminf(fminf(v.y, v.z), v.w));
+  a.mx = fmaxf(fmaxf(a.mx, v.x), fmaxf(fmaxf(v.y, v.z), v.w));
+  const float wy = nv > 1 ? 1.f : 0.f, wz = nv > 2 ? 1.f : 0.f, ww = nv > 3 ? 1.f : 0.f;
+  a.nan += (v.x != v.x) + (nv > 1 && v.y != v.y) + (nv > 2 && v.z != v.z) + (nv > 3 && v.w != v.w);
+  // fp32 partial over the 4 lanes of the group, float64 across groups
+  const float vy = v.y * wy, vz = v.z * wz, vw = v.w * ww;   // NaN*0 stays NaN: sums go NaN, fine
+  const float pa = (__builtin_fabsf(v.x) + __builtin_fabsf(vy)) +
+                   (__builtin_fabsf(vz) + __builtin_fabsf(vw));
+  const float p1 = (v.x + vy) + (vz + vw);
+  const double dx = v.x, dy = vy, dz = vz, dw = vw;
+  a.sa += (double)pa;
+  a.s1 += (double)p1;
+  a.s2 += __builtin_fma(dx, dx, __builtin_fma(dy, dy, __builtin_fma(dz, dz, dw * dw)));
+}
+
+__device__ __forceinline__ void obs_block_reduce(ObsAcc &a) {
+  __shared__ float s_mn[kWaves], s_mx[kWaves];
+  __shared__ uint32_t s_nan[kWaves];
+  __shared__ double s_sa[kWaves], s_s1[kWaves], s_s2[kWaves];
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  const int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
+  if (l == 0) {
+    s_mn[w] = a.mn; s_mx[w] = a.mx; s_nan[w] = a.nan;
+    s_sa[w] = a.sa; s_s1[w] = a.s1; s_s2[w] = a.s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kWaves; ++i) {
+      a.mn = fminf(a.mn, s_mn[i]); a.mx = fmaxf(a.mx, s_mx[i]); a.nan += s_nan[i];
+      a.sa += s_sa[i]; a.s1 += s_s1[i]; a.s2 += s_s2[i];
+    }
+  }
+  __syncthreads();
+}
+
+template <bool VEC, bool NT>
+__global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x, int64_t n,
+                                                    double *__restrict__ stats_out,
+                                                    float *__restrict__ run_minmax,
+                                                    double *__restrict__ qp_out, int sym,
+                                                    double qden, double eps,
+                                                    double *__restrict__ ws,
+                                                    uint32_t *__restrict__ counter) {
+  ObsAcc a;
+  obs_init(a);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  constexpr int U = 4;
+  for (int64_t base = t0; base < ng; base += stride * U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * stride < ng) v[u] = load_group<VEC, NT>(x, base + u * stride, n);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * stride < ng) obs_add4(a, v[u], valid_in_group(base + u * stride, n));
+  }
+  obs_block_reduce(a);
+  if (threadIdx.x == 0) {
+    double *r = ws + (int64_t)blockIdx.x * kPartials;
+    r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan;
+    r[3] = a.sa; r[4] = a.s1; r[5] = a.s2;
+  }
+  if (!arrive_last(counter)) return;
+
+  // ---- epilogue in the last block: fixed-order combine of the partials ----
+  obs_init(a);
+  double nanc = 0.0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
+    const double *r = ws + (int64_t)b * kPartials;
+    a.mn = fminf(a.mn, (float)r[0]);
+    a.mx = fmaxf(a.mx, (float)r[1]);
+    nanc += r[2];
+    a.sa += r[3]; a.s1 += r[4]; a.s2 += r[5];
+  }
+  {
+    __shared__ double s_nanc[kWaves];
+    nanc = wave_reduce(nanc, AddD());
+    if (threadIdx.x % kWave == 0) s_nanc[threadIdx.x / kWave] = nanc;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 1; i < kWaves; ++i) nanc += s_nanc[i];
+  }
+  obs_block_reduce(a);
+  if (threadIdx.x == 0) {
+    const double dn = (double)n;
+    const bool has_nan = nanc > 0.0;
+    if (stats_out) {
+      stats_out[VSIQ_ST_MIN] = (double)a.mn;   // NaN-ignoring; see VSIQ_ST_NAN
+      stats_out[VSIQ_ST_MAX] = (double)a.mx;
+      stats_out[VSIQ_ST_NAN] = nanc;
+      stats_out[VSIQ_ST_SUMABS] = a.sa;
+      stats_out[VSIQ_ST_SUM] = a.s1;
+      stats_out[VSIQ_ST_SUMSQ] = a.s2;
+      stats_out[VSIQ_ST_N] = dn;
+      // NaN inputs make torch's fp32 mean/std NaN as well
+      const double mean = a.s1 / dn;
+      const double var = (a.s2 - a.s1 * mean) / (dn - 1.0);
+      stats_out[VSIQ_ST_MEANABS] = has_nan ? __builtin_nan("") : (double)(float)(a.sa / dn);
+      stats_out[VSIQ_ST_MEAN] = has_nan ? __builtin_nan("") : (double)(float)mean;
+      stats_out[VSIQ_ST_STD] = (has_nan || n < 2)
+                                   ? __builtin_nan("")
+                                   : (double)(float)__builtin_sqrt(var > 0.0 ? var : 0.0);
+    }
+    observer_update(a.mn, a.mx, has_nan, run_minmax, qp_out, sym, qden, eps);
+    *counter = 0u;   // ready for the next stream-ordered launch
+  }
+}
+
+// Finalize from an externally reduced stats record (multi-GPU: stats all-reduced
+// over RCCL with MAX on [-min, max] and SUM on the counts, then this 1-lane kernel).
+__global__ void k_observe_finalize(const double *__restrict__ stats, float *__restrict__ run_minmax,
+                                   double *__restrict__ qp_out, int sym, double qden, double eps) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  observer_update((float)stats[VSIQ_ST_MIN], (float)stats[VSIQ_ST_MAX], stats[VSIQ_ST_NAN] > 0.0,
+                  run_minmax, qp_out, sym, qden, eps);
+}
+
+
+// ----------------------------------------------------------------------------
+// K4: learnable (LSQ) backward, grad_x + f64 scale / zp gradient sums
+// ----------------------------------------------------------------------------
+struct LsqAcc {
+  double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
+};
+
+template <bool ZPL>
+__device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
+  const float u = fdiv(x, p.d);
+  const float r = __builtin_rintf(u + p.z);
+  const float q = fq_clamp(r, p.lo, p.hi);
+  const bool m = (r >= p.lo && r <= p.hi);
+  const float gq = g * p.s;                 // MulBackward0 (self)
+  const float gm = m ? gq : 0.0f;           // ClampBackward1
+  const float t1 = g * (q - p.z);           // MulBackward0 (other)
+  const float xs = fdiv(u, p.d);            // (self / other) / other
+  const float t2 = (-gm) * xs;              // DivBackward0 (other)
+  if (valid) {
+    acc.t += (double)t1 + (double)t2;
+    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
+  }
+  return fdiv(gm, p.d);                     // DivBackward0 (self)
+}
+
+__device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
+  __shared__ double s[2][kWaves];
+  c.t = wave_reduce(c.t, AddD());
+  c.z = wave_reduce(c.z, AddD());
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) { s[0][w] = c.t; s[1][w] = c.z; }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int i = 1; i < kWaves; ++i) { c.t += s[0][i]; c.z += s[1][i]; }
+  __syncthreads();
+}
+
+template <bool VEC, bool NT, bool ZPL>
+__device__ __forceinline__ void lsq_group(const float *x, const float *g, float *gx, int64_t i,
+                                          int64_t n, f4 xv, f4 gv, const QP &p, LsqAcc &c) {
+  const int nv = valid_in_group(i, n);
+  f4 o;
+  o.x = lsq_elem<ZPL>(xv.x, gv.x, p, c, true);
+  o.y = lsq_elem<ZPL>(xv.y, gv.y, p, c, nv > 1);
+  o.z = lsq_elem<ZPL>(xv.z, gv.z, p, c, nv > 2);
+  o.w = lsq_elem<ZPL>(xv.w, gv.w, p, c, nv > 3);
+  store_group<VEC, NT>(gx, i, n, o);
+}
+
+template <bool VEC, bool NT, bool ZPL>
+__global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
+                                                    const float *__restrict__ x,
+                                                    float *__restrict__ gx, int64_t n,
+                                                    QPSrc src, double gscale, int prefetch,
+                                                    double *__restrict__ grad_out,
+                                                    double *__restrict__ ws,
+                                                    uint32_t *__restrict__ counter) {
+  const QP p = load_qp(src);
+  LsqAcc c{0.0, 0.0};
+  const int64_t ng = cdiv(n, 4);
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (prefetch) {
+    // software pipeline: the next tile's loads are in flight while this one computes
+    f4 xa{}, ga{};
+    if (i < ng) { xa = load_group<VEC, NT>(x, i, n); ga = load_group<VEC, NT>(g, i, n); }
+    while (i < ng) {
+      const int64_t j = i + stride;
+      f4 xb{}, gb{};
+      if (j < ng) { xb = load_group<VEC, NT>(x, j, n); gb = load_group<VEC, NT>(g, j, n); }
+      lsq_group<VEC, NT, ZPL>(x, g, gx, i, n, xa, ga, p, c);
+      xa = xb;
+      ga = gb;
+      i = j;
+    }
+  } else {
+    for (; i < ng; i += stride)
+      lsq_group<VEC, NT, ZPL>(x, g, gx, i, n, load_group<VEC, NT>(x, i, n),
+                              load_group<VEC, NT>(g, i, n), p, c);
+  }
+  lsq_block_reduce(c);
+  if (threadIdx.x == 0) {
+    double *r = ws + (int64_t)blockIdx.x * kPartials;
+    r[0] = c.t; r[1] = c.z;
+  }
+  if (!arrive_last(counter)) return;
+  c = LsqAcc{0.0, 0.0};
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
+    const double *r = ws + (int64_t)b * kPartials;
+    c.t += r[0]; c.z += r[1];
+  }
+  lsq_block_reduce(c);
+  if (threadIdx.x == 0) {
+    grad_out[0] = c.t * gscale;
+    double gz = 0.0;
+    if (ZPL) {
+      // ClampBackward of zero_point_rounding (uniform.py:101): in-range test on round(zp)
+      const double zr = __builtin_rint(src.zdev ? *src.zdev : src.zhost);   // NaN -> not in range
+      const bool zin = zr >= (double)p.lo && zr <= (double)p.hi;
+      gz = zin ? c.z * gscale : 0.0;
+    }
+    grad_out[1] = gz;
+    *counter = 0u;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// exhaustive check of fdiv against the IEEE division: every 32-bit pattern a,
+// for each divisor b[k]; counts bitwise mismatches (NaNs compare by NaN-ness)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_selftest_div(const float *__restrict__ bs, int nb,
+                                                         unsigned long long *__restrict__ bad) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (int k = 0; k < nb; ++k) {
+    const FastDiv d = make_fastdiv(bs[k]);
+    uint32_t cnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < (1ull << 32); i += stride) {
+      const float a = __uint_as_float((uint32_t)i);
+      const float q = fdiv(a, d), w = a / d.b;
+      const bool same = (__float_as_uint(q) == __float_as_uint(w)) || (q != q && w != w);
+      cnt += same ? 0u : 1u;
+    }
+    cnt = wave_reduce(cnt, AddU());
+    if (threadIdx.x % kWave == 0 && cnt) atomicAdd(bad + k, (unsigned long long)cnt);
+  }
+}
+
+
+template <bool VEC, bool NT>
+void launch_fq_fwd(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
+                   const QPSrc &src, hipStream_t st) {
+  const dim3 grid(flat_grid(cdiv(n, 4))), block(kBlock);
+  if (codes && mask)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else if (codes)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else if (mask)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, codes, mask, n, src);
+}
+
+
+template <bool VEC, bool NT>
+void launch_lsq(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
+                double gscale, double *grad_out, double *ws, uint32_t *counter, int grid,
+                hipStream_t st) {
+  const int pf = g_tune.lsq_prefetch;
+  if (zpl)
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true>), dim3(grid), dim3(kBlock), 0, st, g, x, gx, n, src,
+                       gscale, pf, grad_out, ws, counter);
+  else
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false>), dim3(grid), dim3(kBlock), 0, st, g, x, gx, n, src,
+                       gscale, pf, grad_out, ws, counter);
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int vsiq_abi_version(void) { return VSIQ_ABI_VERSION; }
+
+const char *vsiq_error_string(int code) {
+  switch (code) {
+    case 0: return "success";
+    case VSIQ_E_ARG: return "vsiq: invalid argument";
+    case VSIQ_E_ALIGN: return "vsiq: misaligned pointer";
+    case VSIQ_E_WS: return "vsiq: workspace too small";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "vsiq: unknown error";
+  }
+}
+
+int64_t vsiq_workspace_doubles(int64_t n) {
+  (void)n;
+  return (int64_t)kMaxReduceGrid * kPartials;
+}
+
+int64_t vsiq_mask_words(int64_t rows, int64_t rowlen) {
+  if (rows < 0 || rowlen < 0) return VSIQ_E_ARG;
+  return rows * mask_words_per_row(rowlen);
+}
+
+int vsiq_set_tuning(int key, int value) {
+  switch (key) {
+    case VSIQ_TUNE_PC_ROWS_PER_BLOCK: g_tune.pc_rows_per_block = value; return 0;
+    case VSIQ_TUNE_NONTEMPORAL: g_tune.nontemporal = value; return 0;
+    case VSIQ_TUNE_FLAT_GRID_CAP: g_tune.flat_grid_cap = value; return 0;
+    case VSIQ_TUNE_LSQ_PREFETCH: g_tune.lsq_prefetch = value; return 0;
+    case VSIQ_TUNE_PC_BLOCK:
+      if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
+      g_tune.pc_block = value;
+      return 0;
+    default: return VSIQ_E_ARG;
+  }
+}
+
+int vsiq_selftest_div(const float *divisors, int count, unsigned long long *mismatches,
+                      void *stream) {
+  if (count < 0 || (count > 0 && (!divisors || !mismatches))) return VSIQ_E_ARG;
+  if (count == 0) return 0;
+  hipLaunchKernelGGL(k_selftest_div, dim3(256 * 16), dim3(kBlock), 0, (hipStream_t)stream,
+                     divisors, count, mismatches);
+  return launch_rc();
+}
+
+int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t n,
+                    const double *qp_dev, const double *scale_dev, double scale_host,
+                    const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
+                    int qmax, void *stream) {
+  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y))) return VSIQ_E_ARG;
+  if (n == 0) return 0;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  QPSrc src{qp_dev, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax,
+            qp_dev ? 0 : zp_round, discrete ? 1 : 0};
+  const bool vec = (n % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
+  const bool nt = g_tune.nontemporal != 0;
+  uint8_t *c = (uint8_t *)codes;
+  VSIQ_B2(launch_fq_fwd, vec, nt, x, y, c, mask, n, src, st);
+  return launch_rc();
+}
+
+int vsiq_observe_f32(const float *x, int64_t n, double *stats_out, float *run_minmax,
+                     double *qp_out, int symmetric, double qden, double eps, double *ws,
+                     int64_t ws_len, uint32_t *counter, void *stream) {
+  if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
+  const bool vec = aligned16(x) && n % 4 == 0;
+  const int grid = reduce_grid(cdiv(n, 4), 4);
+  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g(grid), b(kBlock);
+  if (vec && g_tune.nontemporal)
+    hipLaunchKernelGGL((k_observe<true, true>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
+                       symmetric, qden, eps, ws, counter);
+  else if (vec)
+    hipLaunchKernelGGL((k_observe<true, false>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
+                       symmetric, qden, eps, ws, counter);
+  else
+    hipLaunchKernelGGL((k_observe<false, false>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
+                       symmetric, qden, eps, ws, counter);
+  return launch_rc();
+}
+
+int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out, int symmetric,
+                          double qden, double eps, void *stream) {
+  if (!stats) return VSIQ_E_ARG;
+  hipLaunchKernelGGL(k_observe_finalize, dim3(1), dim3(kWave), 0, (hipStream_t)stream, stats,
+                     run_minmax, qp_out, symmetric, qden, eps);
+  return launch_rc();
+}
+
+int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
+                     const double *scale_dev, double scale_host, const double *zp_dev,
+                     double zp_host, int zp_learn, int qmin, int qmax, double gscale,
+                     double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+                     void *stream) {
+  if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax) return VSIQ_E_ARG;
+  const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
+  const int grid = reduce_grid(cdiv(n, 4), 4);
+  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
+  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
+  const bool nt = g_tune.nontemporal != 0;
+  VSIQ_B2(launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
+          (hipStream_t)stream);
+  return launch_rc();
+}
+
+}  // extern "C"

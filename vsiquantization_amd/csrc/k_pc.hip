@@ -1,0 +1,152 @@
+// k_pc.hip — K3 dispatch + per-channel fake-quant with given qparams, and their C ABI.
+#include "k_pc.cuh"
+
+namespace vsiq {
+
+extern template bool launch_pc_bs<true, true, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+
+template <bool VEC, bool NT, bool STATS>
+int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
+  const int64_t ng = cdiv(a.rowlen, 4);
+  // workgroup size: enough lanes that a row fits in <= 5 groups per lane where possible
+  int bs = g_tune.pc_block;
+  if (bs <= 0) bs = ng > 4 * 512 ? 1024 : (ng > 2 * 256 ? 512 : 256);
+  // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
+  int rpb = g_tune.pc_rows_per_block;
+  if (rpb <= 0) rpb = 1;
+  const int grid = (int)std::max<int64_t>(1, cdiv(a.rows, rpb));
+  bool ok = false;
+  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, a, grid, st);
+  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, a, grid, st);
+  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, a, grid, st);
+  if (!ok)
+    hipLaunchKernelGGL((k_pc_observe_fq_long<VEC, NT>), dim3((unsigned)a.rows), dim3(kBlock), 0, st, x,
+                       y, c, m, a);
+  return launch_rc();
+}
+
+
+// ----------------------------------------------------------------------------
+// per-channel fake-quant with given per-row qparams: grid (rows, chunks)
+// ----------------------------------------------------------------------------
+struct PCFixed {
+  int64_t rowlen;
+  const double *scale, *zp;
+  int zp_round;
+  float lo, hi;
+};
+
+__device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
+  QPSrc s{nullptr, a.scale + row, a.zp + row, 0.0, 0.0, a.lo, a.hi, a.zp_round, 0};
+  return load_qp(s);
+}
+
+template <bool VEC, bool NT, bool CODES, bool MASK>
+__global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
+                                                      uint8_t *__restrict__ codes,
+                                                      uint64_t *__restrict__ mask, PCFixed a) {
+  const int64_t row = blockIdx.x;
+  const QP p = pc_fixed_qp(a, row);
+  const int64_t ng = cdiv(a.rowlen, 4);
+  const float *xr = x + row * a.rowlen;
+  float *yr = y + row * a.rowlen;
+  for (int64_t i = (int64_t)blockIdx.y * kBlock + threadIdx.x; i - threadIdx.x % kWave < ng;
+       i += (int64_t)gridDim.y * kBlock) {
+    const bool in = i < ng;
+    Elem e0{}, e1{}, e2{}, e3{};
+    if (in) {
+      const f4 v = load_group<VEC, NT>(xr, i, a.rowlen);
+      e0 = fq_elem(v.x, p); e1 = fq_elem(v.y, p); e2 = fq_elem(v.z, p); e3 = fq_elem(v.w, p);
+      f4 o;
+      o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
+      store_group<VEC, NT>(yr, i, a.rowlen, o);
+      if (CODES) {
+        const uint32_t c = e0.code | (e1.code << 8) | (e2.code << 16) | (e3.code << 24);
+        uint8_t *cr = codes + row * a.rowlen;
+        if (VEC) reinterpret_cast<uint32_t *>(cr)[i] = c;
+        else
+          for (int j = 0; j < valid_in_group(i, a.rowlen); ++j) cr[4 * i + j] = (uint8_t)(c >> (8 * j));
+      }
+    }
+    if (MASK) {
+      const int nv = in ? valid_in_group(i, a.rowlen) : 0;
+      store_mask_chunk(mask + row * mask_words_per_row(a.rowlen) + 4 * (i / kWave), e0.m && nv > 0,
+                       e1.m && nv > 1, e2.m && nv > 2, e3.m && nv > 3);
+    }
+  }
+}
+
+
+template <bool VEC, bool NT>
+void launch_pc_fixed(const float *x, float *y, uint8_t *c, uint64_t *m, const PCFixed &a, int64_t rows,
+                     hipStream_t st) {
+  const dim3 grid((unsigned)rows, (unsigned)chunk_grid(a.rowlen, rows)), block(kBlock);
+  if (c && m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, c, m, a);
+  else if (c) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, c, m, a);
+  else if (m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, c, m, a);
+  else hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, c, m, a);
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
+                           int64_t rowlen, float *run_min, float *run_max, double *scale_out,
+                           double *zp_out, double *row_stats, int symmetric, int qmin, int qmax,
+                           double qden, double eps, void *stream) {
+  if (rows < 0 || rowlen <= 0 || qmin > qmax) return VSIQ_E_ARG;
+  if (rows == 0) return 0;
+  if (!x || !run_min || !run_max || !scale_out || !zp_out) return VSIQ_E_ARG;
+  if (!y && (codes || mask)) return VSIQ_E_ARG;
+  if (rows > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  PCArgs a{rows, rowlen, run_min, run_max, scale_out, zp_out, row_stats, symmetric, (float)qmin,
+           (float)qmax, qden, eps};
+  const bool vec = (rowlen % 4 == 0) && aligned16(x) && (!y || aligned16(y)) && (!codes || aligned4(codes));
+  const bool nt = g_tune.nontemporal != 0;
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t *c = (uint8_t *)codes;
+  if (row_stats) {
+    if (vec) return nt ? launch_pc<true, true, true>(x, y, c, mask, a, st) : launch_pc<true, false, true>(x, y, c, mask, a, st);
+    return launch_pc<false, false, true>(x, y, c, mask, a, st);
+  }
+  if (vec) return nt ? launch_pc<true, true, false>(x, y, c, mask, a, st) : launch_pc<true, false, false>(x, y, c, mask, a, st);
+  return launch_pc<false, false, false>(x, y, c, mask, a, st);
+}
+
+int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
+                       int64_t rowlen, const double *scale, const double *zp, int zp_round,
+                       int qmin, int qmax, void *stream) {
+  if (rows < 0 || rowlen <= 0 || qmin > qmax) return VSIQ_E_ARG;
+  if (rows == 0) return 0;
+  if (!x || !y || !scale || !zp || rows > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  PCFixed a{rowlen, scale, zp, zp_round, (float)qmin, (float)qmax};
+  const bool vec = (rowlen % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
+  const bool nt = g_tune.nontemporal != 0;
+  uint8_t *c = (uint8_t *)codes;
+  VSIQ_B2(launch_pc_fixed, vec, nt, x, y, c, mask, a, rows, (hipStream_t)stream);
+  return launch_rc();
+}
+
+}  // extern "C"

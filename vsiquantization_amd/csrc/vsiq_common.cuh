@@ -1,0 +1,368 @@
+#pragma once
+// vsiq_common.cuh — MI355X (gfx950 / CDNA4) kernels for VSIQuantization's
+// fake-quantize hot path, exported through the C ABI in include/vsiq.h.
+//
+// Design (DESIGN.md has the full rationale and roofline numbers):
+//   * Everything here is HBM-bound elementwise + reduction work: no MFMA.
+//     Loads/stores are 16 B per lane (float4) wherever the layout allows, one
+//     read and one write of every element per pass, streamed with nontemporal
+//     hints (the tensors are touched once per pass).
+//   * fp32 arithmetic is IEEE and in the reference's operation order
+//     (quantizers/uniform.py:55,95): true division x/s (correctly rounded; the
+//     build uses -fhip-fp32-correctly-rounded-divide-sqrt, -ffp-contract=off,
+//     denormals kept), rint (half-to-even), NaN-propagating clamp that keeps
+//     -0.0.  This is bit-identical to the reference's PyTorch CPU kernels.
+//   * qparams (observers/minmax.py:49-74) are computed in float64 on the
+//     device from the fp32 min/max, so no `.item()` host round trip is needed.
+//   * The straight-through mask travels between forward and backward as ONE BIT
+//     per element (ballot words), not a byte: 1/32 of the fp32 traffic.
+//   * Reductions are deterministic: fixed per-thread order (grid depends only
+//     on n), fixed tree in the workgroup, partials reduced in block order by the
+//     last workgroup to arrive (agent-scope release/acquire hand-off,
+//     cdna_hip_programming.md G16).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "vsiq.h"
+
+
+namespace vsiq {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kWaves = kBlock / kWave;
+constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
+constexpr int kPartials = 8;           // doubles per partial record
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// tuning knobs (vsiq_set_tuning); -1 / 0 = automatic
+struct Tuning {
+  int pc_rows_per_block = 0;   // K3 rows per workgroup (0 = auto)
+  int pc_block = 0;            // K3 workgroup size 256/512/1024 (0 = auto)
+  int nontemporal = 1;         // nt hints on streamed loads/stores
+  int flat_grid_cap = 8192;    // max workgroups of the flat streaming kernels
+  int lsq_prefetch = 1;        // K4 software prefetch of the next tile
+};
+extern Tuning g_tune;
+
+__host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ----------------------------------------------------------------------------
+// Correctly rounded fp32 division by a uniform divisor without v_div_* .
+//
+// The compiler's IEEE sequence (v_div_scale / v_rcp / v_div_fmas / v_div_fixup)
+// funnels every division through VCC, which serialises all divisions of a wave;
+// the hot kernels divide 1-3 times per element by the SAME scale.  With
+// r = RN(1/b) computed once, two Newton-Markstein corrections give RN(a/b):
+//   q0 = RN(a r); q1 = RN(q0 + RN(a - q0 b) r)     (q1 is faithful)
+//   q2 = RN(q1 + (a - q1 b) r)                     (Markstein: a - q1 b exact,
+//                                                   q2 = RN(a/b))
+// valid without underflow/overflow, i.e. for |a|, |b| in [2^-63, 2^63]; a == 0
+// returns a*r (signed zero, as IEEE); any other a (NaN, inf, tiny, huge) takes
+// the IEEE division.  vsiq_selftest_div() checks this exhaustively against the
+// IEEE division for all 2^32 dividends (tests/test_gpu_parity.py).
+// ----------------------------------------------------------------------------
+struct FastDiv {
+  float b, r;
+  int fast;   // b in the safe range (uniform)
+};
+
+__device__ __forceinline__ FastDiv make_fastdiv(float b) {
+  FastDiv d;
+  d.b = b;
+  d.r = 1.0f / b;   // IEEE, once per thread
+  const uint32_t ub = __float_as_uint(b) & 0x7fffffffu;
+  d.fast = (ub - 0x20000000u) <= 0x3f000000u;   // |b| in [2^-63, 2^63]
+  return d;
+}
+
+__device__ __forceinline__ float fdiv(float a, const FastDiv &d) {
+  if (!d.fast) return a / d.b;
+  const float q0 = a * d.r;
+  const float e0 = __builtin_fmaf(-q0, d.b, a);
+  const float q1 = __builtin_fmaf(e0, d.r, q0);
+  const float e1 = __builtin_fmaf(-q1, d.b, a);
+  float q = __builtin_fmaf(e1, d.r, q1);
+  const uint32_t ua = __float_as_uint(a) & 0x7fffffffu;
+  if (ua == 0u) q = q0;                                  // +-0 / b
+  else if ((ua - 0x20000000u) > 0x3f000000u) q = a / d.b;   // rare: IEEE path
+  return q;
+}
+
+// ----------------------------------------------------------------------------
+// element arithmetic (quantizers/uniform.py:95, 55)
+// ----------------------------------------------------------------------------
+struct QP {
+  float s, z, lo, hi;
+  int discrete;
+  FastDiv d;
+};
+
+__device__ __forceinline__ float fq_round(float x, const QP &p) {
+  float u = fdiv(x, p.d);   // fp32 true division x / fp32(scale), correctly rounded
+  u = u + p.z;              // + fp32(zero_point); -0.0 + 0.0 -> +0.0 like torch.add
+  return __builtin_rintf(u);   // torch.round: half to even
+}
+
+// torch.clamp(v, lo, hi): NaN propagates, -0.0 survives
+__device__ __forceinline__ float fq_clamp(float r, float lo, float hi) {
+  return r < lo ? lo : (r > hi ? hi : r);
+}
+
+__device__ __forceinline__ uint32_t fq_code_byte(float q) {
+  // int8 (sym) / uint8 (asym) share the low byte of the integer; NaN -> 0
+  return (q == q) ? (uint32_t)((int)q) & 0xffu : 0u;
+}
+
+struct Elem {
+  float y;
+  uint32_t code;
+  bool m;
+};
+
+__device__ __forceinline__ Elem fq_elem(float x, const QP &p) {
+  const float r = fq_round(x, p);
+  const float q = fq_clamp(r, p.lo, p.hi);
+  Elem e;
+  e.y = p.discrete ? q : (q - p.z) * p.s;
+  e.code = fq_code_byte(q);
+  e.m = (r >= p.lo && r <= p.hi);   // ClampBackward1: inclusive, on the rounded value
+  return e;
+}
+
+// where qparams come from (one struct, passed by value -> kernarg / SGPRs)
+struct QPSrc {
+  const double *qp;     // observer record [scale, zp, ...] or null
+  const double *sdev;   // learnable f64 scale or null (then shost)
+  const double *zdev;   // f64 zp on the device or null (then zhost)
+  double shost, zhost;
+  float lo, hi;
+  int zround;           // learnable zp: clamp(rint(zp)) (uniform.py:98-102)
+  int discrete;         // write clamp(round(x/s+zp)) itself (discreate_tensor) instead of y
+};
+
+__device__ __forceinline__ QP load_qp(const QPSrc &a) {
+  double s, z;
+  if (a.qp) {
+    s = a.qp[VSIQ_QP_SCALE];
+    z = a.qp[VSIQ_QP_ZP];
+  } else {
+    s = a.sdev ? *a.sdev : a.shost;
+    z = a.zdev ? *a.zdev : a.zhost;
+    if (a.zround) {
+      // quantizers/uniform.py:98-102: clamp(round(zp), qmin, qmax) in f64, NaN propagates
+      const double zr = __builtin_rint(z);
+      z = zr < (double)a.lo ? (double)a.lo : (zr > (double)a.hi ? (double)a.hi : zr);
+    }
+  }
+  QP p;
+  p.s = (float)s;
+  p.z = (float)z;
+  p.lo = a.lo;
+  p.hi = a.hi;
+  p.discrete = a.discrete;
+  p.d = make_fastdiv(p.s);
+  return p;
+}
+
+// ----------------------------------------------------------------------------
+// streamed memory access: 16 B per lane, optional nontemporal hint
+// ----------------------------------------------------------------------------
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float *p) {
+  const f4 *q = reinterpret_cast<const f4 *>(p);
+  if (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float *p, f4 v) {
+  f4 *q = reinterpret_cast<f4 *>(p);
+  if (NT) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
+// A group of 4 consecutive elements of a row starting at element 4*i.
+// VEC: one 16-B access (row length % 4 == 0, 16-B aligned).  Otherwise 4 scalar
+// accesses with per-element bounds ("virtual float4"); invalid lanes replicate
+// element 0 so min/max/NaN see no fake values.
+template <bool VEC, bool NT>
+__device__ __forceinline__ f4 load_group(const float *row, int64_t i, int64_t len) {
+  if (VEC) return ld4<NT>(row + 4 * i);
+  const int64_t e = 4 * i;
+  f4 v;
+  v.x = row[e];
+  v.y = e + 1 < len ? row[e + 1] : v.x;
+  v.z = e + 2 < len ? row[e + 2] : v.x;
+  v.w = e + 3 < len ? row[e + 3] : v.x;
+  return v;
+}
+
+template <bool VEC, bool NT>
+__device__ __forceinline__ void store_group(float *row, int64_t i, int64_t len, f4 v) {
+  if (VEC) {
+    st4<NT>(row + 4 * i, v);
+    return;
+  }
+  const int64_t e = 4 * i;
+  row[e] = v.x;
+  if (e + 1 < len) row[e + 1] = v.y;
+  if (e + 2 < len) row[e + 2] = v.z;
+  if (e + 3 < len) row[e + 3] = v.w;
+}
+
+__device__ __forceinline__ int valid_in_group(int64_t i, int64_t len) {
+  const int64_t r = len - 4 * i;
+  return r >= 4 ? 4 : (r > 0 ? (int)r : 0);
+}
+
+// ----------------------------------------------------------------------------
+// 1-bit straight-through masks (include/vsiq.h: mask layout)
+//   row r owns words [r*W, (r+1)*W), W = 4*ceil(rowlen/256); element e of the
+//   row -> chunk c = e/256, word 4c + (e%4), bit (e%256)/4.
+// Thread with group index i (4 elements 4i..4i+3) in a wave whose 64 lanes hold
+// groups 64c..64c+63: lane = i%64, and the four ballots ARE the chunk's words.
+// ----------------------------------------------------------------------------
+__host__ __device__ inline int64_t mask_words_per_row(int64_t rowlen) { return 4 * cdiv(rowlen, 256); }
+
+__device__ __forceinline__ void store_mask_chunk(uint64_t *words, bool m0, bool m1, bool m2, bool m3) {
+  const uint64_t b0 = __ballot(m0), b1 = __ballot(m1), b2 = __ballot(m2), b3 = __ballot(m3);
+  const int lane = threadIdx.x % kWave;
+  if (lane < 4) words[lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+}
+
+__device__ __forceinline__ uint32_t load_mask_nibble(const uint64_t *words, int lane) {
+  const uint64_t w0 = words[0], w1 = words[1], w2 = words[2], w3 = words[3];
+  return (uint32_t)((w0 >> lane) & 1u) | ((uint32_t)((w1 >> lane) & 1u) << 1) |
+         ((uint32_t)((w2 >> lane) & 1u) << 2) | ((uint32_t)((w3 >> lane) & 1u) << 3);
+}
+
+// ----------------------------------------------------------------------------
+// wave / block reductions (wave64)
+// ----------------------------------------------------------------------------
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v = op(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+struct MinOp {
+  __device__ float operator()(float a, float b) const { return fminf(a, b); }
+};
+struct MaxOp {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+struct AddD {
+  __device__ double operator()(double a, double b) const { return a + b; }
+};
+struct OrU {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; }
+};
+struct AddU {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+
+// Last-workgroup-done hand-off.  Every block's thread 0 has stored its partial
+// record; returns true (block-uniform) in the block that arrives last, after an
+// agent-scope acquire so its plain loads see every other block's partials.
+__device__ __forceinline__ bool arrive_last(uint32_t *counter) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// f64 qparams from the running min/max (observers/minmax.py:49-74).
+// min_val <= 0 <= max_val always holds (state starts at 0/0, minmax.py:28-29).
+__device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, double qden,
+                                               double eps, double *scale, double *zp) {
+  if (sym) {
+    const double a = __builtin_fabs(mn), b = __builtin_fabs(mx);
+    const double max_abs = b > a ? b : a;   // Python max(): first unless strictly greater
+    *scale = max_abs / qden;
+    *zp = 0.0;
+  } else {
+    const double s = (mx - mn) / qden;
+    const double v = -mn / (s + eps);
+    double z = __builtin_rint(v);           // Python round(): half to even
+    if (!__builtin_isfinite(z)) z = __builtin_nan("");   // Python raises here
+    if (z == 0.0) z = 0.0;                  // Python int 0 -> +0.0, never -0.0
+    *scale = s;
+    *zp = z;
+  }
+}
+
+// Running-state update + qparams (observers/minmax.py:42-47 then :49-74).  A call
+// whose tensor holds a NaN changes nothing: `nan < v` is False in Python.
+__device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_nan,
+                                                float *run_minmax, double *qp_out, int sym,
+                                                double qden, double eps) {
+  float mn = 0.f, mx = 0.f;
+  if (run_minmax) { mn = run_minmax[0]; mx = run_minmax[1]; }
+  if (!has_nan) {
+    if (cmn < mn) mn = cmn;
+    if (cmx > mx) mx = cmx;
+  }
+  if (run_minmax) { run_minmax[0] = mn; run_minmax[1] = mx; }
+  if (qp_out) {
+    double s, z;
+    minmax_qparams((double)mn, (double)mx, sym, qden, eps, &s, &z);
+    qp_out[VSIQ_QP_SCALE] = s;
+    qp_out[VSIQ_QP_ZP] = z;
+    qp_out[VSIQ_QP_MIN] = mn;
+    qp_out[VSIQ_QP_MAX] = mx;
+  }
+}
+
+
+// ----------------------------------------------------------------------------
+// host helpers
+// ----------------------------------------------------------------------------
+inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+inline bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
+inline bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
+
+inline int reduce_grid(int64_t groups, int per_thread) {
+  int64_t b = cdiv(groups, (int64_t)kBlock * per_thread);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxReduceGrid));
+}
+
+inline int flat_grid(int64_t groups) {
+  const int64_t b = cdiv(groups, (int64_t)kBlock);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, std::max(256, g_tune.flat_grid_cap)));
+}
+
+// blocks per row for the (row, chunk) kernels: one block per 1024 groups, at most
+// ~32 blocks per CU over the whole grid and at most 65535 (chunks are grid-strided)
+inline int64_t chunk_grid(int64_t rowlen, int64_t rows) {
+  int64_t c = cdiv(cdiv(rowlen, 4), (int64_t)kBlock * 4);
+  const int64_t cap = std::max<int64_t>(1, (256 * 32) / std::max<int64_t>(rows, 1));
+  return std::max<int64_t>(1, std::min<int64_t>(std::min(c, cap), 65535));
+}
+
+inline int launch_rc() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+// dispatch helpers: runtime flags -> template instantiations
+#define VSIQ_B2(F, A, B, ...)                                 \
+  ((A) ? ((B) ? F<true, true>(__VA_ARGS__) : F<true, false>(__VA_ARGS__)) \
+       : ((B) ? F<false, true>(__VA_ARGS__) : F<false, false>(__VA_ARGS__)))
+
+}  // namespace vsiq
