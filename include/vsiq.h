@@ -80,8 +80,6 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 /* Performance knobs (process-wide; results are identical for every setting). */
 #define VSIQ_TUNE_PC_ROWS_PER_BLOCK 1  /* K3 rows per workgroup, 0 = auto */
 #define VSIQ_TUNE_NONTEMPORAL 2        /* 1 = nontemporal streamed loads/stores (default) */
-#define VSIQ_TUNE_FLAT_GRID_CAP 3      /* max workgroups of flat streaming kernels (8192) */
-#define VSIQ_TUNE_LSQ_PREFETCH 4       /* 1 = K4 software prefetch (default) */
 #define VSIQ_TUNE_PC_BLOCK 5           /* K3 workgroup size 256 / 512 / 1024, 0 = auto */
 int vsiq_set_tuning(int key, int value);
 

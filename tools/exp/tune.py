@@ -38,11 +38,9 @@ del c2
 torch.cuda.empty_cache()
 c3 = bench.C3Lsq(dev, 2, 0)
 for rnd in range(3):
-    for pf, nt, cap in itertools.product((0, 1), (1,), (2048,)):
-        H.set_tuning(H.TUNE_LSQ_PREFETCH, pf)
+    for nt in (0, 1):
         H.set_tuning(H.TUNE_NONTEMPORAL, nt)
-        H.set_tuning(H.TUNE_FLAT_GRID_CAP, cap)
-        res.setdefault(f"c3 pf{pf} nt{nt} cap{cap}", []).append(measure(c3, steps=16))
+        res.setdefault(f"c3 nt{nt}", []).append(measure(c3, steps=16))
 for k, v in res.items():
     f = sorted(x[0] for x in v)[len(v) // 2]
     b = sorted(x[1] for x in v)[len(v) // 2]

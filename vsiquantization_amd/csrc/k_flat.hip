@@ -16,17 +16,18 @@ __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, 
                                                    QPSrc src) {
   const QP p = load_qp(src);
   const int64_t ng = cdiv(n, 4);
-  const int64_t stride = (int64_t)gridDim.x * kBlock;   // multiple of 64: lanes stay chunk-aligned
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i - threadIdx.x % kWave < ng;
-       i += stride) {
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;   // lanes chunk-aligned
+  f4 v[kFlatU];
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int64_t i = base + u * kBlock;
+    if (i - threadIdx.x % kWave >= ng) break;   // whole wave past the end (uniform)
     const bool in = i < ng;
-    Elem e0{}, e1{}, e2{}, e3{};
+    Elem e0, e1, e2, e3;
+    fq_group(v[u], p, e0, e1, e2, e3);
     if (in) {
-      const f4 v = load_group<VEC, NT>(x, i, n);
-      e0 = fq_elem(v.x, p);
-      e1 = fq_elem(v.y, p);
-      e2 = fq_elem(v.z, p);
-      e3 = fq_elem(v.w, p);
       f4 o;
       o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
       store_group<VEC, NT>(y, i, n, o);
@@ -123,11 +124,13 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   constexpr int U = 4;
-  for (int64_t base = t0; base < ng; base += stride * U) {
+  const int64_t iters = block_iters(ng, (int64_t)blockIdx.x * kBlock, stride * U);
+  for (int64_t it = 0; it < iters; ++it) {
+    const int64_t base = t0 + it * stride * U;
     f4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (base + u * stride < ng) v[u] = load_group<VEC, NT>(x, base + u * stride, n);
+      v[u] = load_group_c<VEC, NT>(x, base + u * stride, ng, n);
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (base + u * stride < ng) obs_add4(a, v[u], valid_in_group(base + u * stride, n));
@@ -201,22 +204,32 @@ struct LsqAcc {
   double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
 };
 
-template <bool ZPL>
+// one element of the learnable backward; returns grad_x, adds the f64 gradient terms
+template <bool ZPL, bool IEEE>
 __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
-  const float u = fdiv(x, p.d);
+  const float u = fdiv_t<IEEE>(x, p.d);
   const float r = __builtin_rintf(u + p.z);
   const float q = fq_clamp(r, p.lo, p.hi);
   const bool m = (r >= p.lo && r <= p.hi);
   const float gq = g * p.s;                 // MulBackward0 (self)
   const float gm = m ? gq : 0.0f;           // ClampBackward1
   const float t1 = g * (q - p.z);           // MulBackward0 (other)
-  const float xs = fdiv(u, p.d);            // (self / other) / other
+  const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
   const float t2 = (-gm) * xs;              // DivBackward0 (other)
   if (valid) {
     acc.t += (double)t1 + (double)t2;
     if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
   }
-  return fdiv(gm, p.d);                     // DivBackward0 (self)
+  return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
+}
+
+// all three divisions of an element inside the fast-division range?
+__device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
+  const float u = fdiv_fast(x, p.d);
+  const float r = __builtin_rintf(u + p.z);
+  const bool m = (r >= p.lo && r <= p.hi);
+  const float gm = m ? g * p.s : 0.0f;
+  return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
 }
 
 __device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
@@ -232,15 +245,24 @@ __device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
 }
 
 template <bool VEC, bool NT, bool ZPL>
-__device__ __forceinline__ void lsq_group(const float *x, const float *g, float *gx, int64_t i,
-                                          int64_t n, f4 xv, f4 gv, const QP &p, LsqAcc &c) {
-  const int nv = valid_in_group(i, n);
+__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xv, f4 gv,
+                                          const QP &p, LsqAcc &c) {
+  const int nv = i < ng ? valid_in_group(i, n) : 0;
+  const uint32_t ok = lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
+                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p);
   f4 o;
-  o.x = lsq_elem<ZPL>(xv.x, gv.x, p, c, true);
-  o.y = lsq_elem<ZPL>(xv.y, gv.y, p, c, nv > 1);
-  o.z = lsq_elem<ZPL>(xv.z, gv.z, p, c, nv > 2);
-  o.w = lsq_elem<ZPL>(xv.w, gv.w, p, c, nv > 3);
-  store_group<VEC, NT>(gx, i, n, o);
+  if (ok) {
+    o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
+    o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);
+    o.z = lsq_elem<ZPL, false>(xv.z, gv.z, p, c, nv > 2);
+    o.w = lsq_elem<ZPL, false>(xv.w, gv.w, p, c, nv > 3);
+  } else {   // rare (divergent): an element outside the fast-division range
+    o.x = lsq_elem<ZPL, true>(xv.x, gv.x, p, c, nv > 0);
+    o.y = lsq_elem<ZPL, true>(xv.y, gv.y, p, c, nv > 1);
+    o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
+    o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
+  }
+  if (nv > 0) store_group<VEC, NT>(gx, i, n, o);
 }
 
 template <bool VEC, bool NT, bool ZPL>
@@ -254,26 +276,17 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   const QP p = load_qp(src);
   LsqAcc c{0.0, 0.0};
   const int64_t ng = cdiv(n, 4);
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (prefetch) {
-    // software pipeline: the next tile's loads are in flight while this one computes
-    f4 xa{}, ga{};
-    if (i < ng) { xa = load_group<VEC, NT>(x, i, n); ga = load_group<VEC, NT>(g, i, n); }
-    while (i < ng) {
-      const int64_t j = i + stride;
-      f4 xb{}, gb{};
-      if (j < ng) { xb = load_group<VEC, NT>(x, j, n); gb = load_group<VEC, NT>(g, j, n); }
-      lsq_group<VEC, NT, ZPL>(x, g, gx, i, n, xa, ga, p, c);
-      xa = xb;
-      ga = gb;
-      i = j;
-    }
-  } else {
-    for (; i < ng; i += stride)
-      lsq_group<VEC, NT, ZPL>(x, g, gx, i, n, load_group<VEC, NT>(x, i, n),
-                              load_group<VEC, NT>(g, i, n), p, c);
+  (void)prefetch;
+  // one-shot: kFlatU groups of x and g per lane, all loads issued before any math
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;
+  f4 xv[kFlatU], gv[kFlatU];
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    xv[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+    gv[u] = load_group_c<VEC, NT>(g, base + u * kBlock, ng, n);
   }
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) lsq_group<VEC, NT, ZPL>(gx, base + u * kBlock, ng, n, xv[u], gv[u], p, c);
   lsq_block_reduce(c);
   if (threadIdx.x == 0) {
     double *r = ws + (int64_t)blockIdx.x * kPartials;
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_selftest_div(const float *__restrict
 template <bool VEC, bool NT>
 void launch_fq_fwd(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
                    const QPSrc &src, hipStream_t st) {
-  const dim3 grid(flat_grid(cdiv(n, 4))), block(kBlock);
+  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4))), block(kBlock);
   if (codes && mask)
     hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, codes, mask, n, src);
   else if (codes)
@@ -339,14 +352,14 @@ void launch_fq_fwd(const float *x, float *y, uint8_t *codes, uint64_t *mask, int
 
 template <bool VEC, bool NT>
 void launch_lsq(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
-                double gscale, double *grad_out, double *ws, uint32_t *counter, int grid,
+                double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                 hipStream_t st) {
-  const int pf = g_tune.lsq_prefetch;
+  const int pf = 0;
   if (zpl)
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true>), dim3(grid), dim3(kBlock), 0, st, g, x, gx, n, src,
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, n, src,
                        gscale, pf, grad_out, ws, counter);
   else
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false>), dim3(grid), dim3(kBlock), 0, st, g, x, gx, n, src,
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, n, src,
                        gscale, pf, grad_out, ws, counter);
 }
 
@@ -369,8 +382,8 @@ const char *vsiq_error_string(int code) {
 }
 
 int64_t vsiq_workspace_doubles(int64_t n) {
-  (void)n;
-  return (int64_t)kMaxReduceGrid * kPartials;
+  const int64_t g = std::max<int64_t>(kMaxReduceGrid, oneshot_grid(cdiv(std::max<int64_t>(n, 0), 4)));
+  return g * kPartials;
 }
 
 int64_t vsiq_mask_words(int64_t rows, int64_t rowlen) {
@@ -382,8 +395,6 @@ int vsiq_set_tuning(int key, int value) {
   switch (key) {
     case VSIQ_TUNE_PC_ROWS_PER_BLOCK: g_tune.pc_rows_per_block = value; return 0;
     case VSIQ_TUNE_NONTEMPORAL: g_tune.nontemporal = value; return 0;
-    case VSIQ_TUNE_FLAT_GRID_CAP: g_tune.flat_grid_cap = value; return 0;
-    case VSIQ_TUNE_LSQ_PREFETCH: g_tune.lsq_prefetch = value; return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;
@@ -454,7 +465,8 @@ int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
                      void *stream) {
   if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax) return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
-  const int grid = reduce_grid(cdiv(n, 4), 4);
+  const int64_t grid = oneshot_grid(cdiv(n, 4));
+  if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
   // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};

@@ -102,7 +102,7 @@ __device__ __forceinline__ void pc_load_row(f4 (&v)[NV], const float *x, int64_t
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int64_t i = threadIdx.x + k * BS;
-    if (i < ng) v[k] = load_group<VEC, NT>(xr, i, a.rowlen);
+    v[k] = load_group_c<VEC, NT>(xr, i, ng, a.rowlen);
   }
 }
 
@@ -136,10 +136,9 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
     // whole waves past the row end skip; a partially valid wave still ballots
     if (i - threadIdx.x % kWave >= ng) continue;
     const bool in = i < ng;
-    Elem e0{}, e1{}, e2{}, e3{};
+    Elem e0, e1, e2, e3;
+    fq_group(v[k], p, e0, e1, e2, e3);
     if (in) {
-      e0 = fq_elem(v[k].x, p); e1 = fq_elem(v[k].y, p);
-      e2 = fq_elem(v[k].z, p); e3 = fq_elem(v[k].w, p);
       f4 o;
       o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
       store_group<VEC, NT>(yr, i, a.rowlen, o);
@@ -159,40 +158,30 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
   }
 }
 
-// Persistent over rows b, b+G, b+2G, ... with a one-row register prefetch.
-template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS>
+// RPB rows per workgroup (rows RPB*b .. RPB*b + RPB-1), straight-line code: every
+// row's loads are issued up front, so a workgroup's writes of row k overlap its
+// reads of row k+1 and hipcc's s_waitcnt counts stay exact (no loop).
+template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS, int RPB>
 __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ x,
-                                                          float *__restrict__ y,
-                                                          uint8_t *__restrict__ codes,
-                                                          uint64_t *__restrict__ mask, PCArgs a) {
-  const int64_t G = gridDim.x;
-  int64_t row = blockIdx.x;
-  f4 A[NV], B[NV];
-  pc_load_row<NV, VEC, NT, BS>(A, x, row, a);
-  float amn = a.run_min[row], amx = a.run_max[row];
-  int par = 0;
-  while (true) {
-    int64_t nxt = row + G;
-    float bmn = 0.f, bmx = 0.f;
-    if (nxt < a.rows) {
-      pc_load_row<NV, VEC, NT, BS>(B, x, nxt, a);
-      bmn = a.run_min[nxt];
-      bmx = a.run_max[nxt];
-    }
-    pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(A, amn, amx, row, par, y, codes, mask, a);
-    if (nxt >= a.rows) break;
-    row = nxt;
-    par ^= 1;
-    nxt = row + G;
-    if (nxt < a.rows) {
-      pc_load_row<NV, VEC, NT, BS>(A, x, nxt, a);
-      amn = a.run_min[nxt];
-      amx = a.run_max[nxt];
-    }
-    pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(B, bmn, bmx, row, par, y, codes, mask, a);
-    if (nxt >= a.rows) break;
-    row = nxt;
-    par ^= 1;
+                                                      float *__restrict__ y,
+                                                      uint8_t *__restrict__ codes,
+                                                      uint64_t *__restrict__ mask, PCArgs a) {
+  const int64_t row0 = (int64_t)blockIdx.x * RPB;
+  const int64_t last = a.rows - 1;
+  f4 v[RPB][NV];
+  float rmn[RPB], rmx[RPB];
+#pragma unroll
+  for (int r = 0; r < RPB; ++r) {
+    const int64_t row = row0 + r < last ? row0 + r : last;
+    pc_load_row<NV, VEC, NT, BS>(v[r], x, row, a);
+    rmn[r] = a.run_min[row];
+    rmx[r] = a.run_max[row];
+  }
+#pragma unroll
+  for (int r = 0; r < RPB; ++r) {
+    if (row0 + r > last) break;   // uniform
+    pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[r], rmn[r], rmx[r], row0 + r, r & 1, y,
+                                                        codes, mask, a);
   }
 }
 
@@ -225,10 +214,9 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
   for (int64_t base = 0; base < ng; base += kBlock) {
     const int64_t i = base + threadIdx.x;
     const bool in = i < ng;
-    Elem e0{}, e1{}, e2{}, e3{};
+    Elem e0, e1, e2, e3;
+    fq_group(load_group_c<VEC, NT>(xr, i, ng, a.rowlen), p, e0, e1, e2, e3);
     if (in) {
-      const f4 w = load_group<VEC, NT>(xr, i, a.rowlen);
-      e0 = fq_elem(w.x, p); e1 = fq_elem(w.y, p); e2 = fq_elem(w.z, p); e3 = fq_elem(w.w, p);
       f4 o;
       o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
       store_group<VEC, NT>(yr, i, a.rowlen, o);
@@ -247,31 +235,43 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
 }
 
 
-template <int NV, bool VEC, bool NT, bool STATS, int BS>
-void launch_pc_nv(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int grid,
-                  hipStream_t st) {
-  const dim3 g(grid), b(BS);
+template <int NV, bool VEC, bool NT, bool STATS, int BS, int RPB>
+void launch_pc_rpb(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
+  const dim3 g((unsigned)cdiv(a.rows, RPB)), b(BS);
   if (c && m)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, true, BS>), g, b, 0, st, x, y, c, m, a);
+    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, true, BS, RPB>), g, b, 0, st, x, y, c, m, a);
   else if (c)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, true, BS>), g, b, 0, st, x, y, c, m, a);
+    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, true, BS, RPB>), g, b, 0, st, x, y, c, m, a);
   else if (m)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, false, BS>), g, b, 0, st, x, y, c, m, a);
+    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, false, BS, RPB>), g, b, 0, st, x, y, c, m, a);
   else
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, false, BS>), g, b, 0, st, x, y, c, m, a);
+    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, false, BS, RPB>), g, b, 0, st, x, y, c, m, a);
+}
+
+template <int NV, bool VEC, bool NT, bool STATS, int BS>
+void launch_pc_nv(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int rpb,
+                  hipStream_t st) {
+  // two rows per workgroup only where the register file allows it
+  if constexpr (NV <= 9) {
+    if (rpb >= 2) {
+      launch_pc_rpb<NV, VEC, NT, STATS, BS, 2>(x, y, c, m, a, st);
+      return;
+    }
+  }
+  launch_pc_rpb<NV, VEC, NT, STATS, BS, 1>(x, y, c, m, a, st);
 }
 
 // groups per lane -> register-resident instantiation; false if the row is too long
 template <bool VEC, bool NT, bool STATS, int BS>
-bool launch_pc_bs(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int grid,
+bool launch_pc_bs(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int rpb,
                   hipStream_t st) {
   const int64_t per_lane = cdiv(cdiv(a.rowlen, 4), BS);
-  if (per_lane <= 1) launch_pc_nv<1, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
-  else if (per_lane <= 2) launch_pc_nv<2, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
-  else if (per_lane <= 3) launch_pc_nv<3, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
-  else if (per_lane <= 5) launch_pc_nv<5, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
-  else if (per_lane <= 9) launch_pc_nv<9, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
-  else if (per_lane <= 12) launch_pc_nv<12, VEC, NT, STATS, BS>(x, y, c, m, a, grid, st);
+  if (per_lane <= 1) launch_pc_nv<1, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  else if (per_lane <= 2) launch_pc_nv<2, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  else if (per_lane <= 3) launch_pc_nv<3, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  else if (per_lane <= 5) launch_pc_nv<5, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  else if (per_lane <= 9) launch_pc_nv<9, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  else if (per_lane <= 12) launch_pc_nv<12, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
   else return false;
   return true;
 }

@@ -31,11 +31,10 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
   // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
   int rpb = g_tune.pc_rows_per_block;
   if (rpb <= 0) rpb = 1;
-  const int grid = (int)std::max<int64_t>(1, cdiv(a.rows, rpb));
   bool ok = false;
-  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, a, grid, st);
-  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, a, grid, st);
-  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, a, grid, st);
+  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, a, rpb, st);
+  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, a, rpb, st);
+  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, a, rpb, st);
   if (!ok)
     hipLaunchKernelGGL((k_pc_observe_fq_long<VEC, NT>), dim3((unsigned)a.rows), dim3(kBlock), 0, st, x,
                        y, c, m, a);
@@ -61,19 +60,26 @@ __device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
 template <bool VEC, bool NT, bool CODES, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
-                                                      uint64_t *__restrict__ mask, PCFixed a) {
-  const int64_t row = blockIdx.x;
+                                                      uint64_t *__restrict__ mask, uint32_t chunks,
+                                                      PCFixed a) {
+  const int64_t row = blockIdx.x / chunks;
+  const int64_t chunk = blockIdx.x % chunks;
   const QP p = pc_fixed_qp(a, row);
   const int64_t ng = cdiv(a.rowlen, 4);
   const float *xr = x + row * a.rowlen;
   float *yr = y + row * a.rowlen;
-  for (int64_t i = (int64_t)blockIdx.y * kBlock + threadIdx.x; i - threadIdx.x % kWave < ng;
-       i += (int64_t)gridDim.y * kBlock) {
+  const int64_t base = chunk * kBlock * kFlatU + threadIdx.x;
+  f4 v[kFlatU];
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(xr, base + u * kBlock, ng, a.rowlen);
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int64_t i = base + u * kBlock;
+    if (i - threadIdx.x % kWave >= ng) break;
     const bool in = i < ng;
-    Elem e0{}, e1{}, e2{}, e3{};
+    Elem e0, e1, e2, e3;
+    fq_group(v[u], p, e0, e1, e2, e3);
     if (in) {
-      const f4 v = load_group<VEC, NT>(xr, i, a.rowlen);
-      e0 = fq_elem(v.x, p); e1 = fq_elem(v.y, p); e2 = fq_elem(v.z, p); e3 = fq_elem(v.w, p);
       f4 o;
       o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
       store_group<VEC, NT>(yr, i, a.rowlen, o);
@@ -97,11 +103,13 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
 template <bool VEC, bool NT>
 void launch_pc_fixed(const float *x, float *y, uint8_t *c, uint64_t *m, const PCFixed &a, int64_t rows,
                      hipStream_t st) {
-  const dim3 grid((unsigned)rows, (unsigned)chunk_grid(a.rowlen, rows)), block(kBlock);
-  if (c && m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, c, m, a);
-  else if (c) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, c, m, a);
-  else if (m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, c, m, a);
-  else hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, c, m, a);
+  const int64_t chunks = oneshot_grid(cdiv(a.rowlen, 4));
+  const dim3 grid((unsigned)(rows * chunks)), block(kBlock);
+  const uint32_t ch = (uint32_t)chunks;
+  if (c && m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, c, m, ch, a);
+  else if (c) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, c, m, ch, a);
+  else if (m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, c, m, ch, a);
+  else hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, c, m, ch, a);
 }
 
 }  // namespace vsiq
@@ -139,7 +147,7 @@ int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, in
                        int qmin, int qmax, void *stream) {
   if (rows < 0 || rowlen <= 0 || qmin > qmax) return VSIQ_E_ARG;
   if (rows == 0) return 0;
-  if (!x || !y || !scale || !zp || rows > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (!x || !y || !scale || !zp || rows * oneshot_grid(cdiv(rowlen, 4)) > 0x7fffffffLL) return VSIQ_E_ARG;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
   PCFixed a{rowlen, scale, zp, zp_round, (float)qmin, (float)qmax};
   const bool vec = (rowlen % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));

@@ -35,6 +35,7 @@ constexpr int kWave = 64;
 constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
 constexpr int kPartials = 8;           // doubles per partial record
+constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -43,12 +44,17 @@ struct Tuning {
   int pc_rows_per_block = 0;   // K3 rows per workgroup (0 = auto)
   int pc_block = 0;            // K3 workgroup size 256/512/1024 (0 = auto)
   int nontemporal = 1;         // nt hints on streamed loads/stores
-  int flat_grid_cap = 8192;    // max workgroups of the flat streaming kernels
-  int lsq_prefetch = 1;        // K4 software prefetch of the next tile
 };
 extern Tuning g_tune;
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid-stride trip count of a workgroup whose first item is `first` (uniform: it
+// depends on blockIdx only, so loops on it are scalar branches and hipcc's
+// s_waitcnt insertion stays exact; lanes past the end predicate their stores).
+__device__ __forceinline__ int64_t block_iters(int64_t n, int64_t first, int64_t stride) {
+  return first < n ? (n - first + stride - 1) / stride : 0;
+}
 
 // ----------------------------------------------------------------------------
 // Correctly rounded fp32 division by a uniform divisor without v_div_* .
@@ -67,7 +73,7 @@ __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 
 // ----------------------------------------------------------------------------
 struct FastDiv {
   float b, r;
-  int fast;   // b in the safe range (uniform)
+  uint32_t fast;   // 0 when b itself is outside the safe range (then every element falls back)
 };
 
 __device__ __forceinline__ FastDiv make_fastdiv(float b) {
@@ -75,21 +81,34 @@ __device__ __forceinline__ FastDiv make_fastdiv(float b) {
   d.b = b;
   d.r = 1.0f / b;   // IEEE, once per thread
   const uint32_t ub = __float_as_uint(b) & 0x7fffffffu;
-  d.fast = (ub - 0x20000000u) <= 0x3f000000u;   // |b| in [2^-63, 2^63]
+  d.fast = (ub - 0x20000000u) <= 0x3f000000u ? 1u : 0u;   // |b| in [2^-63, 2^63]
   return d;
 }
 
-__device__ __forceinline__ float fdiv(float a, const FastDiv &d) {
-  if (!d.fast) return a / d.b;
+// branch-free: RN(a/b) whenever fdiv_ok(a, d); garbage otherwise
+__device__ __forceinline__ float fdiv_fast(float a, const FastDiv &d) {
   const float q0 = a * d.r;
   const float e0 = __builtin_fmaf(-q0, d.b, a);
   const float q1 = __builtin_fmaf(e0, d.r, q0);
   const float e1 = __builtin_fmaf(-q1, d.b, a);
-  float q = __builtin_fmaf(e1, d.r, q1);
+  const float q2 = __builtin_fmaf(e1, d.r, q1);
+  return (__float_as_uint(a) & 0x7fffffffu) ? q2 : q0;   // +-0 / b = a * r (signed zero)
+}
+
+// 1 when fdiv_fast(a, d) is RN(a/b); bitwise-combinable without branches
+__device__ __forceinline__ uint32_t fdiv_ok(float a, const FastDiv &d) {
   const uint32_t ua = __float_as_uint(a) & 0x7fffffffu;
-  if (ua == 0u) q = q0;                                  // +-0 / b
-  else if ((ua - 0x20000000u) > 0x3f000000u) q = a / d.b;   // rare: IEEE path
-  return q;
+  return d.fast & (((ua - 0x20000000u) <= 0x3f000000u) | (ua == 0u));
+}
+
+// IEEE when asked, else the fast path (used by the rare per-group fallback)
+template <bool IEEE>
+__device__ __forceinline__ float fdiv_t(float a, const FastDiv &d) {
+  return IEEE ? a / d.b : fdiv_fast(a, d);
+}
+
+__device__ __forceinline__ float fdiv(float a, const FastDiv &d) {
+  return fdiv_ok(a, d) ? fdiv_fast(a, d) : a / d.b;
 }
 
 // ----------------------------------------------------------------------------
@@ -101,10 +120,11 @@ struct QP {
   FastDiv d;
 };
 
+template <bool IEEE>
 __device__ __forceinline__ float fq_round(float x, const QP &p) {
-  float u = fdiv(x, p.d);   // fp32 true division x / fp32(scale), correctly rounded
-  u = u + p.z;              // + fp32(zero_point); -0.0 + 0.0 -> +0.0 like torch.add
-  return __builtin_rintf(u);   // torch.round: half to even
+  float u = fdiv_t<IEEE>(x, p.d);   // fp32 true division x / fp32(scale), correctly rounded
+  u = u + p.z;                      // + fp32(zero_point); -0.0 + 0.0 -> +0.0 like torch.add
+  return __builtin_rintf(u);        // torch.round: half to even
 }
 
 // torch.clamp(v, lo, hi): NaN propagates, -0.0 survives
@@ -123,14 +143,31 @@ struct Elem {
   bool m;
 };
 
+template <bool IEEE>
 __device__ __forceinline__ Elem fq_elem(float x, const QP &p) {
-  const float r = fq_round(x, p);
+  const float r = fq_round<IEEE>(x, p);
   const float q = fq_clamp(r, p.lo, p.hi);
   Elem e;
   e.y = p.discrete ? q : (q - p.z) * p.s;
   e.code = fq_code_byte(q);
   e.m = (r >= p.lo && r <= p.hi);   // ClampBackward1: inclusive, on the rounded value
   return e;
+}
+
+// the 4 elements of a group; the IEEE division is taken (divergently, rarely) only
+// for lanes holding an element outside the fast-division range
+__device__ __forceinline__ void fq_group(f4 v, const QP &p, Elem &e0, Elem &e1, Elem &e2, Elem &e3) {
+  e0 = fq_elem<false>(v.x, p);
+  e1 = fq_elem<false>(v.y, p);
+  e2 = fq_elem<false>(v.z, p);
+  e3 = fq_elem<false>(v.w, p);
+  const uint32_t ok = fdiv_ok(v.x, p.d) & fdiv_ok(v.y, p.d) & fdiv_ok(v.z, p.d) & fdiv_ok(v.w, p.d);
+  if (!ok) {
+    e0 = fq_elem<true>(v.x, p);
+    e1 = fq_elem<true>(v.y, p);
+    e2 = fq_elem<true>(v.z, p);
+    e3 = fq_elem<true>(v.w, p);
+  }
 }
 
 // where qparams come from (one struct, passed by value -> kernarg / SGPRs)
@@ -191,13 +228,22 @@ __device__ __forceinline__ void st4(float *p, f4 v) {
 template <bool VEC, bool NT>
 __device__ __forceinline__ f4 load_group(const float *row, int64_t i, int64_t len) {
   if (VEC) return ld4<NT>(row + 4 * i);
-  const int64_t e = 4 * i;
+  // unconditional (clamped) scalar loads keep the vmcnt bookkeeping exact
+  const int64_t e = 4 * i, l = len - 1;
   f4 v;
   v.x = row[e];
-  v.y = e + 1 < len ? row[e + 1] : v.x;
-  v.z = e + 2 < len ? row[e + 2] : v.x;
-  v.w = e + 3 < len ? row[e + 3] : v.x;
+  const float y = row[e + 1 < l ? e + 1 : l], z = row[e + 2 < l ? e + 2 : l], w = row[e + 3 < l ? e + 3 : l];
+  v.y = e + 1 < len ? y : v.x;
+  v.z = e + 2 < len ? z : v.x;
+  v.w = e + 3 < len ? w : v.x;
   return v;
+}
+
+// group i clamped into [0, ng): loads are issued unconditionally (no branch around a
+// load, so hipcc's s_waitcnt counting stays exact); callers predicate the stores
+template <bool VEC, bool NT>
+__device__ __forceinline__ f4 load_group_c(const float *row, int64_t i, int64_t ng, int64_t len) {
+  return load_group<VEC, NT>(row, i < ng ? i : ng - 1, len);
 }
 
 template <bool VEC, bool NT>
@@ -337,22 +383,16 @@ inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 inline bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
 inline bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
 
+// one-shot streaming grid: every lane owns kFlatU groups, no loop (a loop around
+// loads + stores makes hipcc wait for the stores at the loop header: on CDNA the
+// stores share vmcnt with the loads)
+inline int64_t oneshot_grid(int64_t groups) {
+  return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kFlatU));
+}
+
 inline int reduce_grid(int64_t groups, int per_thread) {
   int64_t b = cdiv(groups, (int64_t)kBlock * per_thread);
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxReduceGrid));
-}
-
-inline int flat_grid(int64_t groups) {
-  const int64_t b = cdiv(groups, (int64_t)kBlock);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(b, std::max(256, g_tune.flat_grid_cap)));
-}
-
-// blocks per row for the (row, chunk) kernels: one block per 1024 groups, at most
-// ~32 blocks per CU over the whole grid and at most 65535 (chunks are grid-strided)
-inline int64_t chunk_grid(int64_t rowlen, int64_t rows) {
-  int64_t c = cdiv(cdiv(rowlen, 4), (int64_t)kBlock * 4);
-  const int64_t cap = std::max<int64_t>(1, (256 * 32) / std::max<int64_t>(rows, 1));
-  return std::max<int64_t>(1, std::min<int64_t>(std::min(c, cap), 65535));
 }
 
 inline int launch_rc() {
