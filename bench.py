@@ -133,7 +133,7 @@ class C3Lsq:
         self.n = n
         lib = H.lib()
         st = H.stream_of(dev)
-        w = H.workspace(dev)
+        w = H.workspace(dev, n)
         self.ws = w
         self.slots = []
         for i in range(min(slots, 2)):   # 2 slots x 1.2 GB already defeat the MALL

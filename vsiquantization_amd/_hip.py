@@ -128,20 +128,31 @@ def stream_of(device) -> c_p:
 class _Workspace:
     """Per (device, stream) reduction workspace + self-resetting arrival counter."""
 
-    def __init__(self, device):
-        n = lib().vsiq_workspace_doubles(0)
-        self.ws = torch.empty(n, dtype=torch.float64, device=device)
+    def __init__(self, device, n):
+        self.device = device
         self.counter = torch.zeros(1, dtype=torch.int32, device=device)
-        self.ws_len = n
+        self.ws = None
+        self.ws_len = 0
+        self.reserve(n)
+
+    def reserve(self, n):
+        need = int(lib().vsiq_workspace_doubles(int(n)))
+        if need > self.ws_len:
+            self.ws = torch.empty(need, dtype=torch.float64, device=self.device)
+            self.ws_len = need
+        return self
 
 
 _WS = {}
 
 
-def workspace(device) -> _Workspace:
+def workspace(device, n: int = 0) -> _Workspace:
+    """Workspace for a reducing launch over n elements on the current stream of `device`.
+    (Growing it while a previous launch still reads the old buffer is safe: the caching
+    allocator only recycles the old block after work queued on this stream.)"""
     dev = torch.device(device)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     w = _WS.get(key)
     if w is None:
-        w = _WS[key] = _Workspace(dev)
-    return w
+        w = _WS[key] = _Workspace(dev, n)
+    return w.reserve(n)

@@ -27,7 +27,8 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
   const int64_t ng = cdiv(a.rowlen, 4);
   // workgroup size: enough lanes that a row fits in <= 5 groups per lane where possible
   int bs = g_tune.pc_block;
-  if (bs <= 0) bs = ng > 4 * 512 ? 1024 : (ng > 2 * 256 ? 512 : 256);
+  // (measured on MI355X at 1024 x 9216: 512 lanes x 5 groups beats 256 x 9 and 1024 x 3)
+  if (bs <= 0) bs = ng <= 5 * 256 ? 256 : (ng <= 5 * 512 ? 512 : 1024);
   // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
   int rpb = g_tune.pc_rows_per_block;
   if (rpb <= 0) rpb = 1;

@@ -132,7 +132,7 @@ def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
     grads = torch.empty(2, dtype=torch.float64, device=dev)
     sd, sh = scalar_source(scale, dev)
     zd, zh = scalar_source(zero_point, dev)
-    w = H.workspace(dev)
+    w = H.workspace(dev, g.numel())
     rc = H.lib().vsiq_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), H.ptr(sd), sh,
                                   H.ptr(zd), zh, int(bool(learn_zp)), int(qmin), int(qmax),
                                   float(gscale), H.ptr(grads), H.ptr(w.ws), _i64(w.ws_len),
@@ -183,7 +183,7 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     dev = x.device
     qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev) if want_qp else None
     st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev) if want_stats else None
-    w = H.workspace(dev)
+    w = H.workspace(dev, x.numel())
     rc = H.lib().vsiq_observe_f32(H.ptr(x), _i64(x.numel()), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
                                   int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps),
                                   H.ptr(w.ws), _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
