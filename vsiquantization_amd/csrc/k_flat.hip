@@ -138,8 +138,8 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
   obs_block_reduce(a);
   if (threadIdx.x == 0) {
     double *r = ws + (int64_t)blockIdx.x * kPartials;
-    r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan;
-    r[3] = a.sa; r[4] = a.s1; r[5] = a.s2;
+    partial_store(r + 0, a.mn); partial_store(r + 1, a.mx); partial_store(r + 2, (double)a.nan);
+    partial_store(r + 3, a.sa); partial_store(r + 4, a.s1); partial_store(r + 5, a.s2);
   }
   if (!arrive_last(counter)) return;
 
@@ -148,10 +148,10 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
   double nanc = 0.0;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
     const double *r = ws + (int64_t)b * kPartials;
-    a.mn = fminf(a.mn, (float)r[0]);
-    a.mx = fmaxf(a.mx, (float)r[1]);
-    nanc += r[2];
-    a.sa += r[3]; a.s1 += r[4]; a.s2 += r[5];
+    a.mn = fminf(a.mn, (float)partial_load(r + 0));
+    a.mx = fmaxf(a.mx, (float)partial_load(r + 1));
+    nanc += partial_load(r + 2);
+    a.sa += partial_load(r + 3); a.s1 += partial_load(r + 4); a.s2 += partial_load(r + 5);
   }
   {
     __shared__ double s_nanc[kWaves];
@@ -277,26 +277,35 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   LsqAcc c{0.0, 0.0};
   const int64_t ng = cdiv(n, 4);
   (void)prefetch;
-  // one-shot: kFlatU groups of x and g per lane, all loads issued before any math
-  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;
-  f4 xv[kFlatU], gv[kFlatU];
+  // kLsqGroups groups per lane, straight-line (fully unrolled): group k+2 is loaded
+  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kLsqGroups + threadIdx.x;
+  f4 xv[kLsqGroups], gv[kLsqGroups];
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
-    xv[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
-    gv[u] = load_group_c<VEC, NT>(g, base + u * kBlock, ng, n);
+  for (int k = 0; k < 2; ++k) {
+    xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
+    gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
   }
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) lsq_group<VEC, NT, ZPL>(gx, base + u * kBlock, ng, n, xv[u], gv[u], p, c);
+  for (int k = 0; k < kLsqGroups; ++k) {
+    if (k + 2 < kLsqGroups) {
+      xv[k + 2] = load_group_c<VEC, NT>(x, base + (k + 2) * kBlock, ng, n);
+      gv[k + 2] = load_group_c<VEC, NT>(g, base + (k + 2) * kBlock, ng, n);
+    }
+    lsq_group<VEC, NT, ZPL>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
+  }
   lsq_block_reduce(c);
   if (threadIdx.x == 0) {
     double *r = ws + (int64_t)blockIdx.x * kPartials;
-    r[0] = c.t; r[1] = c.z;
+    partial_store(r + 0, c.t);
+    partial_store(r + 1, c.z);
   }
   if (!arrive_last(counter)) return;
   c = LsqAcc{0.0, 0.0};
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
     const double *r = ws + (int64_t)b * kPartials;
-    c.t += r[0]; c.z += r[1];
+    c.t += partial_load(r + 0);
+    c.z += partial_load(r + 1);
   }
   lsq_block_reduce(c);
   if (threadIdx.x == 0) {
@@ -382,7 +391,7 @@ const char *vsiq_error_string(int code) {
 }
 
 int64_t vsiq_workspace_doubles(int64_t n) {
-  const int64_t g = std::max<int64_t>(kMaxReduceGrid, oneshot_grid(cdiv(std::max<int64_t>(n, 0), 4)));
+  const int64_t g = std::max<int64_t>(kMaxReduceGrid, lsq_grid(cdiv(std::max<int64_t>(n, 0), 4)));
   return g * kPartials;
 }
 
@@ -465,7 +474,7 @@ int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
                      void *stream) {
   if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax) return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
-  const int64_t grid = oneshot_grid(cdiv(n, 4));
+  const int64_t grid = lsq_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
   // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given

@@ -36,6 +36,7 @@ constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
 constexpr int kPartials = 8;           // doubles per partial record
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
+constexpr int kLsqGroups = 16;         // groups per lane in K4 (fewer workgroups -> fewer partials)
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -311,14 +312,25 @@ struct AddU {
   __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
 };
 
-// Last-workgroup-done hand-off.  Every block's thread 0 has stored its partial
-// record; returns true (block-uniform) in the block that arrives last, after an
-// agent-scope acquire so its plain loads see every other block's partials.
+// Cross-workgroup partials without fences (MI355X_MICROARCH.md "Valid forms",
+// row 1): thread 0 of each workgroup stores its partial record write-through
+// (sc1), drains it (s_waitcnt vmcnt(0)) and only then bumps the arrival counter;
+// the workgroup whose add returns gridDim.x-1 takes an agent acquire and reads
+// every record with sc1 loads.  No per-workgroup release fence: a release writes
+// back the XCD's whole L2 (buffer_wbl2), which behind streaming stores cost
+// microseconds per workgroup.
+__device__ __forceinline__ void partial_store(double *p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double partial_load(const double *p) {
+  return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Call after thread 0 has partial_store()d its record; returns true (block-uniform)
+// in the last workgroup to arrive.
 __device__ __forceinline__ bool arrive_last(uint32_t *counter) {
   __shared__ int s_last;
-  __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
@@ -388,6 +400,10 @@ inline bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
 // stores share vmcnt with the loads)
 inline int64_t oneshot_grid(int64_t groups) {
   return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kFlatU));
+}
+
+inline int64_t lsq_grid(int64_t groups) {
+  return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kLsqGroups));
 }
 
 inline int reduce_grid(int64_t groups, int per_thread) {
