@@ -93,6 +93,18 @@ int vsiq_selftest_div(const float *divisors, int count, unsigned long long *mism
                       void *stream);
 
 /*
+ * Self-test of the no-check fast paths, over all 2^32 fp32 inputs:
+ *   mode 0: the quantizer code clamp(rint(x/s + zp), qmin, qmax) (value, sign of
+ *           zero, STE mask bit) of the fast forward element vs the IEEE one, for
+ *           every x with |x| <= 2^62, per (scales[k], zero_points[k]);
+ *   mode 1: the STE backward quotient RN(RN(g*s)/s) (zero_points unused).
+ * counts[2k] += mismatches, counts[2k+1] += inputs checked (uint64, zeroed by the
+ * caller); a pair outside the fast domain checks nothing (counts[2k+1] == 0).
+ */
+int vsiq_selftest_fq(int mode, const float *scales, const float *zero_points, int count,
+                     float qmin, float qmax, unsigned long long *counts, void *stream);
+
+/*
  * Per-tensor fake-quant forward (K1).
  * Replaces quantizers/uniform.py:54-55 + :95 (discreate_tensor):
  *   y = (clamp(rint(x/s + zp), qmin, qmax) - zp) * s      (fp32)

@@ -317,6 +317,43 @@ def test_fast_division_exhaustive():
     assert npy(bad).tolist() == [0] * len(divs)
 
 
+def _selftest_fq(mode, scales, zps, lo, hi):
+    s = torch.tensor(np.asarray(scales, np.float32), device=DEV)
+    z = torch.tensor(np.asarray(zps, np.float32), device=DEV)
+    out = torch.zeros(2 * len(scales), dtype=torch.int64, device=DEV)
+    H.check(H.lib().vsiq_selftest_fq(mode, H.ptr(s), H.ptr(z), len(scales), float(lo), float(hi),
+                                     H.ptr(out), H.stream_of(s.device)), "vsiq_selftest_fq")
+    return npy(out).reshape(-1, 2)
+
+
+def test_fast_quantizer_exhaustive():
+    """The no-check forward element (fq_elem_fast) gives the reference's code c =
+    clamp(rint(x/s + zp)) -- value, sign of zero and STE mask bit -- for ALL 2^32 x
+    with |x| <= 2^62, for scales/zero points inside the fast domain; outside it the
+    kernels take the IEEE path (checked count 0 here)."""
+    ones = float(np.float32(np.nextafter(np.float32(2), np.float32(0))))
+    pairs = [(2.0 ** -20, 0.0), (2.0 ** 62, 0.0), (0.0123, 0.0), (1 / 127, 0.0), (ones, 0.0),
+             (0.05, 3.0), (0.02, -5.0), (0.1, 128.0), (3.7, 0.37), (0.3, 2.0 ** -12),
+             (1e-3, -2.5), (2.0 ** -19 * 1.7, 1.0), (1e5, 0.0), (0.031, 255.0), (1.0, 0.5),
+             (2.0 ** -21, 0.0), (0.1, 1e-5), (0.1, float("nan"))]      # last three: outside
+    for lo, hi in ((-128, 127), (0, 255), (-2, 1)):
+        res = _selftest_fq(0, [p[0] for p in pairs], [p[1] for p in pairs], lo, hi)
+        assert res[:, 0].tolist() == [0] * len(pairs), (lo, hi, res.tolist())
+        assert (res[:-3, 1] > 3_100_000_000).all() and (res[-3:, 1] == 0).all(), res.tolist()
+
+
+def test_fast_ste_division_exhaustive():
+    """ste_quot(g) = RN(RN(g*s)/s) for ALL 2^32 g inside its domain."""
+    rng = np.random.default_rng(5)
+    ones = float(np.float32(np.nextafter(np.float32(2), np.float32(0))))
+    scales = [2.0 ** -60, 2.0 ** 60, 0.1, 1 / 3, ones, 1.0, 0.0123, 1 / 127, 255.00001,
+              float(np.float32(np.nextafter(np.float32(1), np.float32(0)))), 2.0 ** -61] + \
+        list(rng.uniform(1e-4, 10.0, 6))
+    res = _selftest_fq(1, scales, [0.0] * len(scales), 0, 0)
+    assert res[:, 0].tolist() == [0] * len(scales), res.tolist()
+    assert (np.delete(res[:, 1], 10) > 1_700_000_000).all() and res[10, 1] == 0, res.tolist()
+
+
 def test_tail_groups_and_mask_bits_per_tensor():
     """n % 4 != 0 and n % 256 != 0: scalar groups, partial ballots."""
     for n in (5, 255, 257, 1001, 4099):

@@ -41,6 +41,7 @@ _SIGS = {
     "vsiq_mask_words": ([c_i64, c_i64], c_i64),
     "vsiq_set_tuning": ([c_int, c_int], c_int),
     "vsiq_selftest_div": ([c_p, c_int, c_p, c_p], c_int),
+    "vsiq_selftest_fq": ([c_int, c_p, c_p, c_int, ctypes.c_float, ctypes.c_float, c_p, c_p], c_int),
     "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
                         c_int),
     "vsiq_observe_f32": ([c_p, c_i64, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p], c_int),

@@ -20,29 +20,23 @@ __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, 
   f4 v[kFlatU];
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+  GroupOut go[kFlatU];
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    go[u] = fq_out_flat<VEC, CODES, MASK>(v[u], p, base + u * kBlock, n);
+    if (MASK) mask_put(mlo, mhi, u, go[u].b);
+  }
+  const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
     const int64_t i = base + u * kBlock;
-    if (i - threadIdx.x % kWave >= ng) break;   // whole wave past the end (uniform)
-    const bool in = i < ng;
-    Elem e0, e1, e2, e3;
-    fq_group(v[u], p, e0, e1, e2, e3);
-    if (in) {
-      f4 o;
-      o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
-      store_group<VEC, NT>(y, i, n, o);
-      if (CODES) {
-        const uint32_t c = e0.code | (e1.code << 8) | (e2.code << 16) | (e3.code << 24);
-        if (VEC) reinterpret_cast<uint32_t *>(codes)[i] = c;
-        else
-          for (int j = 0; j < valid_in_group(i, n); ++j) codes[4 * i + j] = (uint8_t)(c >> (8 * j));
-      }
-    }
-    if (MASK) {
-      const int nv = in ? valid_in_group(i, n) : 0;
-      store_mask_chunk(mask + 4 * (i / kWave), e0.m && nv > 0, e1.m && nv > 1, e2.m && nv > 2,
-                       e3.m && nv > 3);
-    }
+    if (i - lane >= ng) break;   // whole wave past the end (uniform)
+    fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[u]);
+  }
+  if (MASK && lane < 4 * kFlatU) {   // lane 4u+j: word j of slot u's chunk
+    const int64_t first = base - lane + (lane >> 2) * kBlock;
+    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
   }
 }
 
@@ -344,6 +338,53 @@ __global__ __launch_bounds__(kBlock) void k_selftest_div(const float *__restrict
 }
 
 
+// exhaustive check of the no-check fast paths, every 32-bit input pattern:
+//   mode 0: quantizer code c = clamp(rint(x/s + zp)) (value, sign, STE mask bit)
+//           of fq_elem_fast vs the IEEE element, for x with fq_x_ok(x), per
+//           (scales[k], zps[k]) inside fq_fast_qp;
+//   mode 1: STE quotient ste_quot(g) vs RN(RN(g*s)/s), for g with ste_ok(g).
+// counts[2k] = mismatches, counts[2k+1] = inputs checked (0 if the qparams are
+// outside the fast domain).
+__global__ __launch_bounds__(kBlock) void k_selftest_fq(int mode, const float *__restrict__ ss,
+                                                        const float *__restrict__ zs, int nk, float lo,
+                                                        float hi, unsigned long long *__restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (int k = 0; k < nk; ++k) {
+    QP p;
+    p.s = ss[k];
+    p.z = mode == 0 ? zs[k] : 0.f;
+    p.lo = lo;
+    p.hi = hi;
+    p.discrete = 1;
+    p.d = make_fastdiv(p.s);
+    p.fast = fq_fast_qp(p.s, p.z);
+    const SteDiv sd = make_stediv(p.s);
+    const bool dom = mode == 0 ? p.fast != 0 : sd.fast != 0;
+    uint32_t bad = 0, seen = 0;
+    if (dom) {
+      for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < (1ull << 32); i += stride) {
+        const float x = __uint_as_float((uint32_t)i);
+        if (mode == 0) {
+          if (!fq_x_ok(x)) continue;
+          const Elem f = fq_elem_fast(x, p), w = fq_elem<true>(x, p);
+          bad += (__float_as_uint(f.y) != __float_as_uint(w.y) || f.m != w.m) ? 1u : 0u;
+        } else {
+          if (!ste_ok(x)) continue;
+          const float f = ste_quot(x, sd), w = ste_ieee(x, true, sd);
+          bad += (__float_as_uint(f) != __float_as_uint(w) && !(f != f && w != w)) ? 1u : 0u;
+        }
+        ++seen;
+      }
+    }
+    bad = wave_reduce(bad, AddU());
+    seen = wave_reduce(seen, AddU());
+    if (threadIdx.x % kWave == 0) {
+      if (bad) atomicAdd(out + 2 * k, (unsigned long long)bad);
+      if (seen) atomicAdd(out + 2 * k + 1, (unsigned long long)seen);
+    }
+  }
+}
+
 template <bool VEC, bool NT>
 void launch_fq_fwd(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
                    const QPSrc &src, hipStream_t st) {
@@ -418,6 +459,17 @@ int vsiq_selftest_div(const float *divisors, int count, unsigned long long *mism
   if (count == 0) return 0;
   hipLaunchKernelGGL(k_selftest_div, dim3(256 * 16), dim3(kBlock), 0, (hipStream_t)stream,
                      divisors, count, mismatches);
+  return launch_rc();
+}
+
+int vsiq_selftest_fq(int mode, const float *scales, const float *zero_points, int count,
+                     float qmin, float qmax, unsigned long long *counts, void *stream) {
+  if (mode != 0 && mode != 1) return VSIQ_E_ARG;
+  if (count < 0 || (count > 0 && (!scales || !counts || (mode == 0 && !zero_points))))
+    return VSIQ_E_ARG;
+  if (count == 0) return 0;
+  hipLaunchKernelGGL(k_selftest_fq, dim3(256 * 16), dim3(kBlock), 0, (hipStream_t)stream, mode,
+                     scales, zero_points, count, qmin, qmax, counts);
   return launch_rc();
 }
 

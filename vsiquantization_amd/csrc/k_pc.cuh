@@ -92,6 +92,8 @@ __device__ __forceinline__ QP pc_row_qparams(float mn, float mx, uint32_t nan, R
   p.hi = a.hi;
   p.discrete = 0;
   p.d = make_fastdiv(p.s);
+  p.fast = (fq_fast_qp(p.s, p.z) && !nan &&
+            __builtin_fmaxf(__builtin_fabsf(mn), __builtin_fabsf(mx)) <= 0x1p62f) ? 1u : 0u;
   return p;
 }
 
@@ -129,32 +131,26 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
   const QP p = pc_row_qparams<STATS, BS>(mn, mx, nan, rs, rmn, rmx, row, par, a);
   if (!y) return;
   float *yr = y + row * a.rowlen;
-  uint64_t *mr = MASK ? mask + row * mask_words_per_row(a.rowlen) : nullptr;
+  uint8_t *cr = CODES ? codes + row * a.rowlen : nullptr;
+  GroupOut go[NV];
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    go[k] = fq_out_row<VEC, CODES, MASK>(v[k], p, threadIdx.x + k * BS, a.rowlen);
+    if (MASK) mask_put(mlo, mhi, k, go[k].b);
+  }
+  const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int64_t i = threadIdx.x + k * BS;
-    // whole waves past the row end skip; a partially valid wave still ballots
-    if (i - threadIdx.x % kWave >= ng) continue;
-    const bool in = i < ng;
-    Elem e0, e1, e2, e3;
-    fq_group(v[k], p, e0, e1, e2, e3);
-    if (in) {
-      f4 o;
-      o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
-      store_group<VEC, NT>(yr, i, a.rowlen, o);
-      if (CODES) {
-        const uint32_t c = e0.code | (e1.code << 8) | (e2.code << 16) | (e3.code << 24);
-        uint8_t *cr = codes + row * a.rowlen;
-        if (VEC) reinterpret_cast<uint32_t *>(cr)[i] = c;
-        else
-          for (int j = 0; j < valid_in_group(i, a.rowlen); ++j) cr[4 * i + j] = (uint8_t)(c >> (8 * j));
-      }
-    }
-    if (MASK) {
-      const int nv = in ? valid_in_group(i, a.rowlen) : 0;
-      store_mask_chunk(mr + 4 * (i / kWave), e0.m && nv > 0, e1.m && nv > 1, e2.m && nv > 2,
-                       e3.m && nv > 3);
-    }
+    if (i - lane >= ng) continue;   // whole wave past the row end (uniform)
+    fq_store_out<VEC, NT, CODES>(yr, cr, i, ng, a.rowlen, go[k]);
+  }
+  if (MASK && lane < 4 * NV) {   // lane 4k+j: word j of group slot k's chunk
+    const int64_t first = threadIdx.x - lane + (lane >> 2) * BS;
+    if (first < ng)
+      mask[row * mask_words_per_row(a.rowlen) + 4 * (first / kWave) + (lane & 3)] =
+          ((uint64_t)mhi << 32) | mlo;
   }
 }
 
@@ -177,11 +173,13 @@ __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ 
     rmn[r] = a.run_min[row];
     rmx[r] = a.run_max[row];
   }
-#pragma unroll
-  for (int r = 0; r < RPB; ++r) {
-    if (row0 + r > last) break;   // uniform
-    pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[r], rmn[r], rmx[r], row0 + r, r & 1, y,
-                                                        codes, mask, a);
+  // RPB is 1 or 2; written out because the unroller refuses the (large) loop body
+  static_assert(RPB == 1 || RPB == 2, "rows per block");
+  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a);
+  if constexpr (RPB == 2) {
+    if (row0 + 1 <= last)   // uniform
+      pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[RPB - 1], rmn[RPB - 1], rmx[RPB - 1],
+                                                          row0 + 1, 1, y, codes, mask, a);
   }
 }
 
@@ -215,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
     const int64_t i = base + threadIdx.x;
     const bool in = i < ng;
     Elem e0, e1, e2, e3;
-    fq_group(load_group_c<VEC, NT>(xr, i, ng, a.rowlen), p, e0, e1, e2, e3);
+    fq_group_row(load_group_c<VEC, NT>(xr, i, ng, a.rowlen), p, e0, e1, e2, e3);
     if (in) {
       f4 o;
       o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;

@@ -25,10 +25,11 @@ extern template bool launch_pc_bs<false, false, false, 1024>(const float *, floa
 template <bool VEC, bool NT, bool STATS>
 int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
   const int64_t ng = cdiv(a.rowlen, 4);
-  // workgroup size: enough lanes that a row fits in <= 5 groups per lane where possible
+  // workgroup size: the smallest that holds the row in <= 9 groups per lane
+  // (measured on MI355X at 1024 x 9216: 256 lanes x 9 groups 13.0 us, 512 x 5 15.9,
+  //  1024 x 3 17.4 -- more rows in flight per CU beats fewer groups per lane)
   int bs = g_tune.pc_block;
-  // (measured on MI355X at 1024 x 9216: 512 lanes x 5 groups beats 256 x 9 and 1024 x 3)
-  if (bs <= 0) bs = ng <= 5 * 256 ? 256 : (ng <= 5 * 512 ? 512 : 1024);
+  if (bs <= 0) bs = ng <= 9 * 256 ? 256 : (ng <= 9 * 512 ? 512 : 1024);
   // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
   int rpb = g_tune.pc_rows_per_block;
   if (rpb <= 0) rpb = 1;
@@ -73,30 +74,26 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
   f4 v[kFlatU];
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(xr, base + u * kBlock, ng, a.rowlen);
+  GroupOut go[kFlatU];
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    go[u] = fq_out_flat<VEC, CODES, MASK>(v[u], p, base + u * kBlock, a.rowlen);
+    if (MASK) mask_put(mlo, mhi, u, go[u].b);
+  }
+  uint8_t *cr = CODES ? codes + row * a.rowlen : nullptr;
+  const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
     const int64_t i = base + u * kBlock;
-    if (i - threadIdx.x % kWave >= ng) break;
-    const bool in = i < ng;
-    Elem e0, e1, e2, e3;
-    fq_group(v[u], p, e0, e1, e2, e3);
-    if (in) {
-      f4 o;
-      o.x = e0.y; o.y = e1.y; o.z = e2.y; o.w = e3.y;
-      store_group<VEC, NT>(yr, i, a.rowlen, o);
-      if (CODES) {
-        const uint32_t c = e0.code | (e1.code << 8) | (e2.code << 16) | (e3.code << 24);
-        uint8_t *cr = codes + row * a.rowlen;
-        if (VEC) reinterpret_cast<uint32_t *>(cr)[i] = c;
-        else
-          for (int j = 0; j < valid_in_group(i, a.rowlen); ++j) cr[4 * i + j] = (uint8_t)(c >> (8 * j));
-      }
-    }
-    if (MASK) {
-      const int nv = in ? valid_in_group(i, a.rowlen) : 0;
-      store_mask_chunk(mask + row * mask_words_per_row(a.rowlen) + 4 * (i / kWave), e0.m && nv > 0,
-                       e1.m && nv > 1, e2.m && nv > 2, e3.m && nv > 3);
-    }
+    if (i - lane >= ng) break;
+    fq_store_out<VEC, NT, CODES>(yr, cr, i, ng, a.rowlen, go[u]);
+  }
+  if (MASK && lane < 4 * kFlatU) {
+    const int64_t first = base - lane + (lane >> 2) * kBlock;
+    if (first < ng)
+      mask[row * mask_words_per_row(a.rowlen) + 4 * (first / kWave) + (lane & 3)] =
+          ((uint64_t)mhi << 32) | mlo;
   }
 }
 

@@ -5,13 +5,11 @@ namespace vsiq {
 
 // ----------------------------------------------------------------------------
 // STE backward with the saved 1-bit mask: gx = (m ? g*s : 0) / s, grid (rows, chunks)
+// (division: ste_quot in vsiq_common.cuh)
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ float ste_gm(float g, uint32_t m, const FastDiv &d) {
-  const float gq = g * d.b;          // MulBackward0
-  return m ? gq : 0.0f;              // ClampBackward1
-}
-
-// one-shot: workgroup b covers chunk b % chunks of row b / chunks (kFlatU groups per lane)
+// one-shot: workgroup b covers chunk b % chunks of row b / chunks (kFlatU groups per
+// lane).  A wave's 64 groups are one 256-element mask chunk: its four mask words
+// are wave-uniform, read with scalar loads and used directly as lane masks.
 template <bool VEC, bool NT>
 __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     const uint64_t *__restrict__ mask,
@@ -20,35 +18,50 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     double shost) {
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
-  const FastDiv s = make_fastdiv((float)(sdev ? sdev[row] : shost));
+  const SteDiv d = make_stediv((float)(sdev ? sdev[row] : shost));
   const int64_t ng = cdiv(rowlen, 4);
+  const int64_t nchunk = cdiv(ng, kWave);
   const float *gr = g + row * rowlen;
   float *xr = gx + row * rowlen;
   const uint64_t *mr = mask + row * mask_words_per_row(rowlen);
-  const int lane = threadIdx.x % kWave;
   const int64_t base = chunk * kBlock * kFlatU + threadIdx.x;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   f4 v[kFlatU];
-  uint32_t m[kFlatU];
+  uint64_t w[kFlatU][4];
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
     const int64_t i = base + u * kBlock;
-    const int64_t ic = i < ng ? i : ng - 1;
-    v[u] = load_group<VEC, NT>(gr, ic, rowlen);
-    m[u] = load_mask_nibble(mr + 4 * (ic / kWave), (int)(ic % kWave));
+    v[u] = load_group<VEC, NT>(gr, i < ng ? i : ng - 1, rowlen);
+    int64_t c = chunk * (kBlock / kWave) * kFlatU + u * (kBlock / kWave) + wave0;
+    c = c < nchunk ? c : nchunk - 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[u][j] = mr[4 * c + j];
   }
+  // all groups computed before the first store: a (predicated, hence branched-around)
+  // store ahead of a load's use would make hipcc wait for the store as well
+  f4 o[kFlatU];
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
-    const int64_t i = base + u * kBlock;
-    const float a0 = ste_gm(v[u].x, m[u] & 1u, s), a1 = ste_gm(v[u].y, m[u] & 2u, s);
-    const float a2 = ste_gm(v[u].z, m[u] & 4u, s), a3 = ste_gm(v[u].w, m[u] & 8u, s);
-    f4 o;   // DivBackward0: gm / s
-    o.x = fdiv_fast(a0, s); o.y = fdiv_fast(a1, s); o.z = fdiv_fast(a2, s); o.w = fdiv_fast(a3, s);
-    if (!(fdiv_ok(a0, s) & fdiv_ok(a1, s) & fdiv_ok(a2, s) & fdiv_ok(a3, s))) {
-      o.x = a0 / s.b; o.y = a1 / s.b; o.z = a2 / s.b; o.w = a3 / s.b;   // rare: IEEE
+    const bool m0 = __builtin_amdgcn_inverse_ballot_w64(w[u][0]);
+    const bool m1 = __builtin_amdgcn_inverse_ballot_w64(w[u][1]);
+    const bool m2 = __builtin_amdgcn_inverse_ballot_w64(w[u][2]);
+    const bool m3 = __builtin_amdgcn_inverse_ballot_w64(w[u][3]);
+    o[u].x = m0 ? ste_quot(v[u].x, d) : 0.0f;
+    o[u].y = m1 ? ste_quot(v[u].y, d) : 0.0f;
+    o[u].z = m2 ? ste_quot(v[u].z, d) : 0.0f;
+    o[u].w = m3 ? ste_quot(v[u].w, d) : 0.0f;
+    if (!(d.fast & ste_ok(v[u].x) & ste_ok(v[u].y) & ste_ok(v[u].z) & ste_ok(v[u].w))) {
+      o[u].x = ste_ieee(v[u].x, m0, d);   // rare
+      o[u].y = ste_ieee(v[u].y, m1, d);
+      o[u].z = ste_ieee(v[u].z, m2, d);
+      o[u].w = ste_ieee(v[u].w, m3, d);
     }
-    if (i < ng) store_group<VEC, NT>(xr, i, rowlen, o);
   }
-  (void)lane;
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int64_t i = base + u * kBlock;
+    if (i < ng) store_group<VEC, NT>(xr, i, rowlen, o[u]);
+  }
 }
 
 

@@ -119,6 +119,7 @@ struct QP {
   float s, z, lo, hi;
   int discrete;
   FastDiv d;
+  uint32_t fast;   // quantizer fast path allowed (fq_fast_qp; K3 also: row finite, no NaN)
 };
 
 template <bool IEEE>
@@ -171,6 +172,123 @@ __device__ __forceinline__ void fq_group(f4 v, const QP &p, Elem &e0, Elem &e1, 
   }
 }
 
+// ----------------------------------------------------------------------------
+// Quantizer fast path: no per-element division check.
+//
+// The forward output depends on x/s only through c = clamp(rint(x/s + zp)).
+// With s in [2^-20, 2^62] (positive), zp finite and either integer-valued or
+// |zp| >= 2^-12, and |x| <= 2^62:
+//   * |x| >= 2^-63: the two Markstein steps give RN(x/s) exactly (fdiv proof);
+//   * |x| <  2^-63: the true quotient is below 2^-43 and the computed one below
+//     2^-38, both under half an ulp of any |zp| >= 2^-12, so RN(q + zp) = zp for
+//     both; for zp = 0, rint(q) = +-0 and copysign(q, x) makes the zero's sign
+//     that of x/s (s > 0), as IEEE; for integer zp != 0 both give zp.
+// So c (value AND sign) is the reference's for every such x; NaN/inf/huge x
+// and out-of-range scales take the IEEE path.  vsiq_selftest_fq() checks this
+// for all 2^32 inputs on the GPU.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fq_fast_qp(float s, float z) {
+  const uint32_t us = __float_as_uint(s);   // sign bit set -> huge -> rejected
+  const bool s_ok = (us - 0x35800000u) <= (0x5e800000u - 0x35800000u);   // [2^-20, 2^62]
+  const float az = __builtin_fabsf(z);
+  const bool z_ok = az <= 0x1p62f && (z == __builtin_rintf(z) || az >= 0x1p-12f);
+  return (s_ok && z_ok) ? 1u : 0u;
+}
+
+__device__ __forceinline__ float fq_quot(float x, const FastDiv &d) {
+  const float q0 = x * d.r;
+  const float e0 = __builtin_fmaf(-q0, d.b, x);
+  const float q1 = __builtin_fmaf(e0, d.r, q0);
+  const float e1 = __builtin_fmaf(-q1, d.b, x);
+  const float q2 = __builtin_fmaf(e1, d.r, q1);
+  return __builtin_copysignf(q2, x);
+}
+
+__device__ __forceinline__ uint32_t fq_x_ok(float x) { return __builtin_fabsf(x) <= 0x1p62f ? 1u : 0u; }   // NaN -> 0
+
+// x not NaN / inf here, so r is finite and the clamp needs no NaN care:
+// c = r <= hi ? r : hi, then r >= lo ? c : lo  (== torch.clamp incl. -0.0)
+__device__ __forceinline__ Elem fq_elem_fast(float x, const QP &p) {
+  const float r = __builtin_rintf(fq_quot(x, p.d) + p.z);
+  const bool le = r <= p.hi, ge = r >= p.lo;
+  const float c = ge ? (le ? r : p.hi) : p.lo;
+  Elem e;
+  e.y = p.discrete ? c : (c - p.z) * p.s;
+  e.code = (uint32_t)((int)c) & 0xffu;
+  e.m = le && ge;
+  return e;
+}
+
+// group of a row whose fast flag (p.fast) is uniform over the workgroup
+__device__ __forceinline__ void fq_group_row(f4 v, const QP &p, Elem &e0, Elem &e1, Elem &e2,
+                                             Elem &e3) {
+  if (p.fast) {
+    e0 = fq_elem_fast(v.x, p);
+    e1 = fq_elem_fast(v.y, p);
+    e2 = fq_elem_fast(v.z, p);
+    e3 = fq_elem_fast(v.w, p);
+  } else {
+    fq_group(v, p, e0, e1, e2, e3);
+  }
+}
+
+// group of a flat tensor: one range compare per element, IEEE for the rare group
+// holding a NaN / inf / |x| > 2^62 (or for out-of-range qparams)
+__device__ __forceinline__ void fq_group_flat(f4 v, const QP &p, Elem &e0, Elem &e1, Elem &e2,
+                                              Elem &e3) {
+  e0 = fq_elem_fast(v.x, p);
+  e1 = fq_elem_fast(v.y, p);
+  e2 = fq_elem_fast(v.z, p);
+  e3 = fq_elem_fast(v.w, p);
+  const uint32_t ok = p.fast & fq_x_ok(v.x) & fq_x_ok(v.y) & fq_x_ok(v.z) & fq_x_ok(v.w);
+  if (!ok) {
+    e0 = fq_elem<true>(v.x, p);
+    e1 = fq_elem<true>(v.y, p);
+    e2 = fq_elem<true>(v.z, p);
+    e3 = fq_elem<true>(v.w, p);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// STE backward division gx = (m ? RN(g*s) : 0) / s
+// p = RN(g*s) is within half an ulp of g*s, so g is a faithful
+// quotient of p/s and ONE Markstein step from it is RN(p/s):
+//   q = RN(g + RN(p - g*s) * r),   r = RN(1/s),
+// the residual p - g*s being exact (it is the product's rounding error).  Valid
+// for s in [2^-60, 2^60] and |g| in [2^-40, 2^64) (p and the quotient normal, no
+// overflow) or g == +-0 (copysign(q, p): -0/s = -0).  Other groups (NaN, inf,
+// tiny g, extreme scales) take the IEEE division.  vsiq_selftest_fq(mode 1)
+// checks it for all 2^32 g on the GPU.
+// ----------------------------------------------------------------------------
+struct SteDiv {
+  float s, r;
+  uint32_t fast;
+};
+
+__device__ __forceinline__ SteDiv make_stediv(float s) {
+  SteDiv d;
+  d.s = s;
+  d.r = 1.0f / s;
+  d.fast = (__float_as_uint(s) - 0x21800000u) <= (0x5d800000u - 0x21800000u) ? 1u : 0u;
+  return d;
+}
+
+__device__ __forceinline__ float ste_quot(float g, const SteDiv &d) {
+  const float p = g * d.s;                       // MulBackward0
+  const float e = __builtin_fmaf(-g, d.s, p);    // exact residual
+  return __builtin_copysignf(__builtin_fmaf(e, d.r, g), p);
+}
+
+// branch-free (bitwise-combinable) validity of ste_quot for one element
+__device__ __forceinline__ uint32_t ste_ok(float g) {
+  const float a = __builtin_fabsf(g);
+  return ((uint32_t)(a >= 0x1p-40f) & (uint32_t)(a < 0x1p64f)) | (uint32_t)(g == 0.0f);
+}
+
+__device__ __forceinline__ float ste_ieee(float g, bool m, const SteDiv &d) {
+  return (m ? g * d.s : 0.0f) / d.s;             // ClampBackward1, DivBackward0 (IEEE)
+}
+
 // where qparams come from (one struct, passed by value -> kernarg / SGPRs)
 struct QPSrc {
   const double *qp;     // observer record [scale, zp, ...] or null
@@ -203,6 +321,7 @@ __device__ __forceinline__ QP load_qp(const QPSrc &a) {
   p.hi = a.hi;
   p.discrete = a.discrete;
   p.d = make_fastdiv(p.s);
+  p.fast = fq_fast_qp(p.s, p.z);
   return p;
 }
 
@@ -284,6 +403,114 @@ __device__ __forceinline__ uint32_t load_mask_nibble(const uint64_t *words, int 
   const uint64_t w0 = words[0], w1 = words[1], w2 = words[2], w3 = words[3];
   return (uint32_t)((w0 >> lane) & 1u) | ((uint32_t)((w1 >> lane) & 1u) << 1) |
          ((uint32_t)((w2 >> lane) & 1u) << 2) | ((uint32_t)((w3 >> lane) & 1u) << 3);
+}
+
+// One fake-quantized group i (elements 4i..4i+3 of a row of `len`) ready for its
+// stores: y, the 4 code bytes, and the 4 ballot words of the wave's mask chunk
+// (wave-uniform, SGPRs).  Each path packs its own result, so the fast/IEEE merge
+// is a merge of SGPR words rather than of per-lane booleans.
+struct GroupOut {
+  f4 o;
+  uint32_t c;
+  uint64_t b[4];
+};
+
+template <bool VEC, bool CODES, bool MASK>
+__device__ __forceinline__ GroupOut fq_pack(const Elem (&e)[4], int64_t i, int64_t len) {
+  GroupOut g;
+  g.o.x = e[0].y; g.o.y = e[1].y; g.o.z = e[2].y; g.o.w = e[3].y;
+  g.c = CODES ? (e[0].code | (e[1].code << 8) | (e[2].code << 16) | (e[3].code << 24)) : 0u;
+  if (MASK) {
+    if (VEC) {   // len % 4 == 0: a group is wholly valid or wholly past the end
+      const bool in = 4 * i < len;
+      g.b[0] = __ballot(e[0].m && in); g.b[1] = __ballot(e[1].m && in);
+      g.b[2] = __ballot(e[2].m && in); g.b[3] = __ballot(e[3].m && in);
+    } else {
+      const int nv = valid_in_group(i, len);   // 0 past the end
+      g.b[0] = __ballot(e[0].m && nv > 0); g.b[1] = __ballot(e[1].m && nv > 1);
+      g.b[2] = __ballot(e[2].m && nv > 2); g.b[3] = __ballot(e[3].m && nv > 3);
+    }
+  } else {
+    g.b[0] = g.b[1] = g.b[2] = g.b[3] = 0;
+  }
+  return g;
+}
+
+// Fast path of a group (see fq_elem_fast).  The clamp compares are taken as wave
+// lane masks (v_cmp -> SGPR pair): they drive the selects directly and their AND
+// IS the STE mask ballot, so no per-lane boolean is ever materialized.
+constexpr int kCmpOGE = 3, kCmpOLE = 5;   // llvm FCmp predicates
+
+template <bool VEC, bool CODES, bool MASK>
+__device__ __forceinline__ GroupOut fq_out_fast(f4 v, const QP &p, int64_t i, int64_t len) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  float yv[4];
+  GroupOut g;
+  g.c = 0;
+  const int nv = VEC ? 4 : valid_in_group(i, len);
+  const uint64_t in_all = (MASK && VEC) ? __ballot(4 * i < len) : 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float r = __builtin_rintf(fq_quot(x[j], p.d) + p.z);
+    const uint64_t le = __builtin_amdgcn_fcmpf(r, p.hi, kCmpOLE);
+    const uint64_t ge = __builtin_amdgcn_fcmpf(r, p.lo, kCmpOGE);
+    float c = __builtin_amdgcn_inverse_ballot_w64(le) ? r : p.hi;
+    c = __builtin_amdgcn_inverse_ballot_w64(ge) ? c : p.lo;
+    yv[j] = p.discrete ? c : (c - p.z) * p.s;
+    if (CODES) g.c |= ((uint32_t)((int)c) & 0xffu) << (8 * j);
+    if (MASK) g.b[j] = le & ge & (VEC ? in_all : __ballot(nv > j));
+    else g.b[j] = 0;
+  }
+  g.o.x = yv[0]; g.o.y = yv[1]; g.o.z = yv[2]; g.o.w = yv[3];
+  return g;
+}
+
+template <bool VEC, bool CODES, bool MASK>
+__device__ __forceinline__ GroupOut fq_out_slow(f4 v, const QP &p, int64_t i, int64_t len) {
+  Elem e[4];
+  fq_group(v, p, e[0], e[1], e[2], e[3]);
+  return fq_pack<VEC, CODES, MASK>(e, i, len);
+}
+
+// group of a row whose p.fast is uniform over the workgroup
+template <bool VEC, bool CODES, bool MASK>
+__device__ __forceinline__ GroupOut fq_out_row(f4 v, const QP &p, int64_t i, int64_t len) {
+  if (p.fast) return fq_out_fast<VEC, CODES, MASK>(v, p, i, len);
+  return fq_out_slow<VEC, CODES, MASK>(v, p, i, len);
+}
+
+// group of a flat tensor: one range compare per element; a wave holding any NaN /
+// inf / |x| > 2^62 (or out-of-range qparams) takes the checked path as a whole
+template <bool VEC, bool CODES, bool MASK>
+__device__ __forceinline__ GroupOut fq_out_flat(f4 v, const QP &p, int64_t i, int64_t len) {
+  const uint32_t ok = p.fast & fq_x_ok(v.x) & fq_x_ok(v.y) & fq_x_ok(v.z) & fq_x_ok(v.w);
+  if (__ballot(!ok) == 0) return fq_out_fast<VEC, CODES, MASK>(v, p, i, len);
+  return fq_out_slow<VEC, CODES, MASK>(v, p, i, len);
+}
+
+// Mask words of several groups gathered into lanes: lane 4*slot + j receives word
+// j of slot `slot` (v_writelane, no select chains); one store per lane later.
+__device__ __forceinline__ void mask_put(uint32_t &lo, uint32_t &hi, int slot, const uint64_t (&b)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t l = 4 * slot + j, wl = (uint32_t)b[j], wh = (uint32_t)(b[j] >> 32);
+    // lane select in M0 (two SGPR operands would break gfx9's constant-bus limit)
+    asm("v_writelane_b32 %0, %1, m0" : "+v"(lo) : "s"(wl), "{m0}"(l));
+    asm("v_writelane_b32 %0, %1, m0" : "+v"(hi) : "s"(wh), "{m0}"(l));
+  }
+}
+
+template <bool VEC, bool NT, bool CODES>
+__device__ __forceinline__ void fq_store_out(float *yr, uint8_t *cr, int64_t i, int64_t ng, int64_t len,
+                                             const GroupOut &g) {
+  if (i < ng) {
+    store_group<VEC, NT>(yr, i, len, g.o);
+    if (CODES) {
+      if (VEC) reinterpret_cast<uint32_t *>(cr)[i] = g.c;
+      else
+        for (int j = 0; j < valid_in_group(i, len); ++j) cr[4 * i + j] = (uint8_t)(g.c >> (8 * j));
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------
