@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 1
+#define VSIQ_ABI_VERSION 2
 
 #define VSIQ_E_ARG (-1)      /* invalid argument (null pointer, bad size, qmin>qmax) */
 #define VSIQ_E_ALIGN (-2)    /* misaligned pointer where alignment is required */
@@ -201,6 +201,36 @@ int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
                      double zp_host, int zp_learn, int qmin, int qmax, double gscale,
                      double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
                      void *stream);
+
+/*
+ * Fused activation + activation fake-quant (K5).  Replaces, in the fused layers,
+ * F.relu / F.silu after the conv (modules/fused.py:124-134, :198-206) followed by
+ * quantize_out (quantizers/fake_quantize.py:49-50): the conv output c is read
+ * once and act(c) is never materialized.  act: VSIQ_ACT_NONE / _RELU / _SILU.
+ *   relu(c) = c < 0 ? 0 : c        bwd: c <= 0 ? 0 : g          (bit-exact)
+ *   silu(c) = c / (1 + exp(-c))    bwd: g*sig*(1 + c*(1 - sig))  (GPU expf: within
+ *                                  a few ulp of torch's CPU Sleef exp)
+ * Each entry point is its plain counterpart applied to act(c); the backward ones
+ * take c again and return the gradient with respect to c.
+ */
+#define VSIQ_ACT_NONE 0
+#define VSIQ_ACT_RELU 1
+#define VSIQ_ACT_SILU 2
+int vsiq_act_fq_fwd_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                        const double *qp_dev, const double *scale_dev, double scale_host,
+                        const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
+                        int qmax, void *stream);
+int vsiq_act_observe_f32(const float *c, int64_t n, int act, double *stats_out, float *run_minmax,
+                         double *qp_out, int symmetric, double qden, double eps, double *ws,
+                         int64_t ws_len, uint32_t *counter, void *stream);
+int vsiq_act_ste_bwd_f32(const float *g, const uint64_t *mask, const float *c, float *gc, int64_t n,
+                         int act, const double *scale_dev, int64_t rowlen, double scale_host,
+                         void *stream);
+int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, int act,
+                         const double *scale_dev, double scale_host, const double *zp_dev,
+                         double zp_host, int zp_learn, int qmin, int qmax, double gscale,
+                         double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+                         void *stream);
 
 #ifdef __cplusplus
 }

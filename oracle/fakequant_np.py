@@ -154,6 +154,43 @@ def lsq_forward_backward(x, g, scale, zero_point, qmin, qmax, gscale, learn_zp=F
     return y, gx, grad_s, grad_zp
 
 
+# --------------------------------------------------------------------------- fused activation (K5)
+def act_forward(c, act):
+    """The fused layers' activation before quantize_out (modules/fused.py:133):
+    F.relu (torch CPU: c < 0 -> +0, -0.0 and NaN pass through) or F.silu
+    (torch CPU silu_kernel: c / (1 + exp(-c)), fp32; numpy's exp is within an ulp
+    of torch's Sleef exp, so SiLU parity is toleranced, see tests)."""
+    c = np.asarray(c, dtype=F32)
+    if act is None or act == "none":
+        return c
+    if act == "relu":
+        return np.where(c < 0, F32(0.0), c).astype(F32)
+    if act == "silu":
+        with np.errstate(all="ignore"):
+            return (c / (F32(1.0) + np.exp(-c).astype(F32))).astype(F32)
+    raise ValueError(act)
+
+
+def act_backward(g, c, act):
+    """Autograd of act_forward: relu threshold_backward(g, relu(c), 0) = c <= 0 ? 0 : g
+    (NaN passes g); silu_backward (g * sig) * fma(c, 1 - sig, 1): torch's vectorized
+    CPU kernel contracts the inner multiply-add into an FMA (matches its outputs far
+    better than the unfused order; exp itself still differs by an ulp)."""
+    g = np.asarray(g, dtype=F32)
+    c = np.asarray(c, dtype=F32)
+    if act is None or act == "none":
+        return g
+    if act == "relu":
+        return np.where(c <= 0, F32(0.0), g).astype(F32)
+    if act == "silu":
+        with np.errstate(all="ignore"):
+            sig = (F32(1.0) / (F32(1.0) + np.exp(-c).astype(F32))).astype(F32)
+            one_m = (F32(1.0) - sig).astype(F32)
+            inner = (c.astype(np.float64) * one_m.astype(np.float64) + 1.0).astype(F32)   # fma
+            return ((g * sig).astype(F32) * inner).astype(F32)
+    raise ValueError(act)
+
+
 # --------------------------------------------------------------------------- per-channel
 def per_channel_observe_fq(w, symmetric: bool, bits: int, obs_bits: int = 8, eps: float = 1e-8,
                            run_min=None, run_max=None):

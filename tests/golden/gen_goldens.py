@@ -14,6 +14,7 @@ Reference call sites exercised (file:line under /root/reference):
   * quantizers/uniform.py:242-271      ScaleGradient / RoundStraightThrough (autograd)
   * quantizers/quantization_manager.py:55-114  collect / quantize / learn-init sequence
   * modules/fused.py:32-134 + modules/fuse.py:45-149  (toy fused model, host structure)
+  * modules/fused.py:133 + quantizers/fake_quantize.py:49-50  (F.relu / F.silu, then quantize_out)
 
 Per-channel has no reference class: it is defined as the
 reference classes applied independently to each out-channel slice W[c].
@@ -287,6 +288,53 @@ for bits, sym in ((4, True), (2, True), (8, False)):
     except Exception as e:
         rec.update(learn_raises=type(e).__name__)
     cases.append(rec)
+
+# ---------------------------------------------------------------------------
+# 6. Fused activation + activation fake-quant (K5): the fused layers run
+#    F.relu / F.silu on the conv output (modules/fused.py:133) and then
+#    quantize_out (quantizers/fake_quantize.py:49-50).  Gradients are w.r.t. the
+#    pre-activation c (autograd through the activation).
+# ---------------------------------------------------------------------------
+import torch.nn.functional as F  # noqa: E402
+
+act_idx = 0
+for act in ("relu", "silu"):
+    fn = F.relu if act == "relu" else F.silu
+    for mode, sym, bits in (("observe", True, 8), ("observe", False, 8), ("observe", False, 4),
+                            ("fixed", False, 8), ("fixed", True, 4),
+                            ("learn", True, 8), ("learn", True, 4)):
+        g = torch.Generator().manual_seed(500 + act_idx)
+        c = torch.randn(4, 8, 6, 6, generator=g) * 1.5
+        if mode == "fixed":   # specials: signed zeros, NaN, infinities, exact ties
+            flat = c.view(-1)
+            flat[:8] = torch.tensor([-0.0, 0.0, float("nan"), float("inf"), float("-inf"),
+                                     -1e-40, 1e-40, 0.5])
+        gg = torch.randn(c.shape, generator=torch.Generator().manual_seed(600 + act_idx))
+        q = UniformQuantizer(bits, sym)
+        cr = c.clone().requires_grad_(True)
+        a = fn(cr)
+        rec = dict(kind="act_fq", key=f"act{act_idx}", act=act, mode=mode, sym=sym, bits=bits)
+        if mode == "observe":
+            obs = MinMaxObserver(sym)          # num_bits 8 through the manager
+            s_, z_ = obs.forward(a.detach())
+            y = q.quantize(a, s_, z_, False)
+            rec.update(scale=float(s_), zp=int(z_), min_val=float(obs.min_val), max_val=float(obs.max_val))
+        elif mode == "fixed":
+            s_, z_ = (0.05, 0) if sym else (0.03, 7)
+            y = q.quantize(a, s_, z_, False)
+            rec.update(scale=s_, zp=z_)
+        else:
+            scale = torch.nn.Parameter(torch.tensor(np.float64(0.04 if bits == 8 else 0.35)))
+            y = q.quantize(a, scale, 0, True)
+            rec.update(scale=float(scale.detach()), zp=0)
+        y.backward(gg)
+        key = rec["key"]
+        rec.update(x=put(key + "_c", c), g=put(key + "_g", gg), y=put(key + "_y", y),
+                   grad_x=put(key + "_gc", cr.grad))
+        if mode == "learn":
+            rec.update(scale_grad=float(scale.grad))
+        cases.append(rec)
+        act_idx += 1
 
 np.savez_compressed(os.path.join(OUT, "fakequant_goldens.npz"), **arrays)
 with open(os.path.join(OUT, "cases.json"), "w") as f:

@@ -116,3 +116,30 @@ def test_manager_sequence(case):
     G.assert_bitwise_f32(y4, G.arr(case["y4"]), "y4")
     G.assert_bitwise_f32(gx4, G.arr(case["gx4"]), "gx4")
     assert gsc == pytest.approx(case["scale_grad"], rel=1e-4)
+
+
+@pytest.mark.parametrize("case", G.cases("act_fq"), ids=lambda c: c["key"])
+def test_act_fq(case):
+    """Fused activation + activation fake quant (K5): ReLU bit-exact, SiLU toleranced."""
+    c = G.arr(case["x"])
+    g = G.arr(case["g"])
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    a = O.act_forward(c, case["act"])
+    if case["mode"] == "observe":
+        s, z = O.minmax_qparams(*O.observe_minmax(a), case["sym"], 8)
+        assert (s, z) == (case["scale"], case["zp"])
+    else:
+        s, z = case["scale"], case["zp"]
+    if case["mode"] == "learn":
+        y, gx, gs, _ = O.lsq_forward_backward(a, g, s, 0, qmin, qmax, O.grad_scale(qmax, c.size))
+        assert abs(gs - case["scale_grad"]) <= 1e-4 * max(1e-3, abs(case["scale_grad"]))
+    else:
+        y, _, m = O.fq_forward(a, s, z, qmin, qmax)
+        gx = O.fq_backward_fixed(g, m, s)
+    gc = O.act_backward(gx, c, case["act"])
+    if case["act"] == "relu":
+        G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+        G.assert_bitwise_f32(gc, G.arr(case["grad_x"]), "grad_c")
+    else:
+        G.assert_fq_close(y, G.arr(case["y"]), s, "y")
+        G.assert_close_f32(gc, G.arr(case["grad_x"]), "grad_c")

@@ -31,11 +31,12 @@ def t(fn, reps=64):
 
 cfgs = [("copy nt u1 g1024", lambda i: scl.exp_copy(P(gs[i % SL].data_ptr()), P(ys[i % SL].data_ptr()), ctypes.c_int64(N // 4), 1024, 1, 1, st)),
         ("product ste", lambda i: H.lib().vsiq_ste_bwd_f32(P(gs[i % SL].data_ptr()), P(ms[i % SL].data_ptr()), P(ys[i % SL].data_ptr()), ctypes.c_int64(N), None, ctypes.c_int64(0), ctypes.c_double(0.05), st))]
-for mm, name in ((0, "mask"), (1, "nomask"), (2, "scale")):
-    for su in (1, 2, 4, 8):
-        cfgs.append((f"ste {name} su{su}", (lambda su, mm: lambda i: lib.exp_ste(
-            P(gs[i % SL].data_ptr()), P(ms[i % SL].data_ptr()), P(ys[i % SL].data_ptr()),
-            ctypes.c_int64(N), ctypes.c_float(0.05), su, mm, st))(su, mm)))
+for mm, name in ((0, "mask"), (4, "halves")):
+    for su in ((2, 9) if mm == 0 else (1, 2, 3, 4, 8)):
+        for lds in (0,):
+            cfgs.append((f"ste {name} su{su} lds{lds // 1024}k", (lambda su, mm, lds: lambda i: lib.exp_ste(
+                P(gs[i % SL].data_ptr()), P(ms[i % SL].data_ptr()), P(ys[i % SL].data_ptr()),
+                ctypes.c_int64(N), ctypes.c_float(0.05), su, mm, st, lds))(su, mm, lds)))
 res = {}
 for rnd in range(3):
     for name, fn in cfgs:

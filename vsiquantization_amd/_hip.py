@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # record layouts (include/vsiq.h)
 ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)
@@ -33,6 +33,18 @@ ST_LEN = 10
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK = 1, 2, 5
+ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
+
+
+def act_code(act) -> int:
+    """None / "relu" / "silu" (or the VSIQ_ACT_* integer) -> VSIQ_ACT_* code."""
+    if isinstance(act, int) and act in (ACT_NONE, ACT_RELU, ACT_SILU):
+        return act
+    try:
+        return ACT_CODES[act]
+    except KeyError:
+        raise ValueError(f"unsupported fused activation {act!r} (None, 'relu' or 'silu')") from None
 
 _SIGS = {
     "vsiq_abi_version": ([], c_int),
@@ -52,6 +64,13 @@ _SIGS = {
     "vsiq_ste_bwd_f32": ([c_p, c_p, c_p, c_i64, c_p, c_i64, c_d, c_p], c_int),
     "vsiq_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d, c_p, c_p,
                           c_i64, c_p, c_p], c_int),
+    "vsiq_act_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_d, c_p, c_d, c_int, c_int,
+                             c_int, c_int, c_p], c_int),
+    "vsiq_act_observe_f32": ([c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p],
+                             c_int),
+    "vsiq_act_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_i64, c_d, c_p], c_int),
+    "vsiq_act_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d,
+                              c_p, c_p, c_i64, c_p, c_p], c_int),
 }
 EXPORTED = tuple(_SIGS)
 

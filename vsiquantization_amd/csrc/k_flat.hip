@@ -1,44 +1,11 @@
-// k_flat.hip — per-tensor kernels: K1 fake-quant forward, K2 observer, K4 LSQ
-// backward, the division self-test, and the library-level C ABI entry points.
+// k_flat.hip — K2 per-tensor observer (optionally over a fused ReLU/SiLU), the
+// division / fast-path self-tests, and the library-level C ABI entry points
+// (K1 lives in k_fq.hip, K4 in k_lsq.hip, the STE backward in k_ste.hip).
 #include "vsiq_common.cuh"
 
 namespace vsiq {
 
 Tuning g_tune;
-
-// ----------------------------------------------------------------------------
-// K1: per-tensor fake-quant forward (flat, grid-stride over 4-element groups)
-// ----------------------------------------------------------------------------
-template <bool VEC, bool NT, bool CODES, bool MASK>
-__global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
-                                                   uint8_t *__restrict__ codes,
-                                                   uint64_t *__restrict__ mask, int64_t n,
-                                                   QPSrc src) {
-  const QP p = load_qp(src);
-  const int64_t ng = cdiv(n, 4);
-  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;   // lanes chunk-aligned
-  f4 v[kFlatU];
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
-  GroupOut go[kFlatU];
-  uint32_t mlo = 0, mhi = 0;
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
-    go[u] = fq_out_flat<VEC, CODES, MASK>(v[u], p, base + u * kBlock, n);
-    if (MASK) mask_put(mlo, mhi, u, go[u].b);
-  }
-  const int lane = threadIdx.x % kWave;
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
-    const int64_t i = base + u * kBlock;
-    if (i - lane >= ng) break;   // whole wave past the end (uniform)
-    fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[u]);
-  }
-  if (MASK && lane < 4 * kFlatU) {   // lane 4u+j: word j of slot u's chunk
-    const int64_t first = base - lane + (lane >> 2) * kBlock;
-    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
-  }
-}
 
 // ----------------------------------------------------------------------------
 // K2: per-tensor observer (min, max, NaN count, sum|x|, sum x, sum x^2)
@@ -104,7 +71,7 @@ __device__ __forceinline__ void obs_block_reduce(ObsAcc &a) {
   __syncthreads();
 }
 
-template <bool VEC, bool NT>
+template <bool VEC, bool NT, int ACT>
 __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x, int64_t n,
                                                     double *__restrict__ stats_out,
                                                     float *__restrict__ run_minmax,
@@ -127,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
       v[u] = load_group_c<VEC, NT>(x, base + u * stride, ng, n);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (base + u * stride < ng) obs_add4(a, v[u], valid_in_group(base + u * stride, n));
+      if (base + u * stride < ng) obs_add4(a, act_fwd4<ACT>(v[u]), valid_in_group(base + u * stride, n));
   }
   obs_block_reduce(a);
   if (threadIdx.x == 0) {
@@ -190,131 +157,6 @@ __global__ void k_observe_finalize(const double *__restrict__ stats, float *__re
                   run_minmax, qp_out, sym, qden, eps);
 }
 
-
-// ----------------------------------------------------------------------------
-// K4: learnable (LSQ) backward, grad_x + f64 scale / zp gradient sums
-// ----------------------------------------------------------------------------
-struct LsqAcc {
-  double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
-};
-
-// one element of the learnable backward; returns grad_x, adds the f64 gradient terms
-template <bool ZPL, bool IEEE>
-__device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
-  const float u = fdiv_t<IEEE>(x, p.d);
-  const float r = __builtin_rintf(u + p.z);
-  const float q = fq_clamp(r, p.lo, p.hi);
-  const bool m = (r >= p.lo && r <= p.hi);
-  const float gq = g * p.s;                 // MulBackward0 (self)
-  const float gm = m ? gq : 0.0f;           // ClampBackward1
-  const float t1 = g * (q - p.z);           // MulBackward0 (other)
-  const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
-  const float t2 = (-gm) * xs;              // DivBackward0 (other)
-  if (valid) {
-    acc.t += (double)t1 + (double)t2;
-    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
-  }
-  return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
-}
-
-// all three divisions of an element inside the fast-division range?
-__device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
-  const float u = fdiv_fast(x, p.d);
-  const float r = __builtin_rintf(u + p.z);
-  const bool m = (r >= p.lo && r <= p.hi);
-  const float gm = m ? g * p.s : 0.0f;
-  return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
-}
-
-__device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
-  __shared__ double s[2][kWaves];
-  c.t = wave_reduce(c.t, AddD());
-  c.z = wave_reduce(c.z, AddD());
-  const int w = threadIdx.x / kWave;
-  if (threadIdx.x % kWave == 0) { s[0][w] = c.t; s[1][w] = c.z; }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int i = 1; i < kWaves; ++i) { c.t += s[0][i]; c.z += s[1][i]; }
-  __syncthreads();
-}
-
-template <bool VEC, bool NT, bool ZPL>
-__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xv, f4 gv,
-                                          const QP &p, LsqAcc &c) {
-  const int nv = i < ng ? valid_in_group(i, n) : 0;
-  const uint32_t ok = lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
-                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p);
-  f4 o;
-  if (ok) {
-    o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
-    o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);
-    o.z = lsq_elem<ZPL, false>(xv.z, gv.z, p, c, nv > 2);
-    o.w = lsq_elem<ZPL, false>(xv.w, gv.w, p, c, nv > 3);
-  } else {   // rare (divergent): an element outside the fast-division range
-    o.x = lsq_elem<ZPL, true>(xv.x, gv.x, p, c, nv > 0);
-    o.y = lsq_elem<ZPL, true>(xv.y, gv.y, p, c, nv > 1);
-    o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
-    o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
-  }
-  if (nv > 0) store_group<VEC, NT>(gx, i, n, o);
-}
-
-template <bool VEC, bool NT, bool ZPL>
-__global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
-                                                    const float *__restrict__ x,
-                                                    float *__restrict__ gx, int64_t n,
-                                                    QPSrc src, double gscale, int prefetch,
-                                                    double *__restrict__ grad_out,
-                                                    double *__restrict__ ws,
-                                                    uint32_t *__restrict__ counter) {
-  const QP p = load_qp(src);
-  LsqAcc c{0.0, 0.0};
-  const int64_t ng = cdiv(n, 4);
-  (void)prefetch;
-  // kLsqGroups groups per lane, straight-line (fully unrolled): group k+2 is loaded
-  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
-  const int64_t base = (int64_t)blockIdx.x * kBlock * kLsqGroups + threadIdx.x;
-  f4 xv[kLsqGroups], gv[kLsqGroups];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
-    gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
-  }
-#pragma unroll
-  for (int k = 0; k < kLsqGroups; ++k) {
-    if (k + 2 < kLsqGroups) {
-      xv[k + 2] = load_group_c<VEC, NT>(x, base + (k + 2) * kBlock, ng, n);
-      gv[k + 2] = load_group_c<VEC, NT>(g, base + (k + 2) * kBlock, ng, n);
-    }
-    lsq_group<VEC, NT, ZPL>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
-  }
-  lsq_block_reduce(c);
-  if (threadIdx.x == 0) {
-    double *r = ws + (int64_t)blockIdx.x * kPartials;
-    partial_store(r + 0, c.t);
-    partial_store(r + 1, c.z);
-  }
-  if (!arrive_last(counter)) return;
-  c = LsqAcc{0.0, 0.0};
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const double *r = ws + (int64_t)b * kPartials;
-    c.t += partial_load(r + 0);
-    c.z += partial_load(r + 1);
-  }
-  lsq_block_reduce(c);
-  if (threadIdx.x == 0) {
-    grad_out[0] = c.t * gscale;
-    double gz = 0.0;
-    if (ZPL) {
-      // ClampBackward of zero_point_rounding (uniform.py:101): in-range test on round(zp)
-      const double zr = __builtin_rint(src.zdev ? *src.zdev : src.zhost);   // NaN -> not in range
-      const bool zin = zr >= (double)p.lo && zr <= (double)p.hi;
-      gz = zin ? c.z * gscale : 0.0;
-    }
-    grad_out[1] = gz;
-    *counter = 0u;
-  }
-}
 
 // ----------------------------------------------------------------------------
 // exhaustive check of fdiv against the IEEE division: every 32-bit pattern a,
@@ -385,32 +227,32 @@ __global__ __launch_bounds__(kBlock) void k_selftest_fq(int mode, const float *_
   }
 }
 
-template <bool VEC, bool NT>
-void launch_fq_fwd(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
-                   const QPSrc &src, hipStream_t st) {
-  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4))), block(kBlock);
-  if (codes && mask)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, codes, mask, n, src);
-  else if (codes)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, codes, mask, n, src);
-  else if (mask)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, codes, mask, n, src);
+template <int ACT>
+void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_out, float *run_minmax,
+                    double *qp_out, int sym, double qden, double eps, double *ws, uint32_t *counter,
+                    int grid, hipStream_t st) {
+  const dim3 g(grid), b(kBlock);
+  if (vec && nt)
+    hipLaunchKernelGGL((k_observe<true, true, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out, sym,
+                       qden, eps, ws, counter);
+  else if (vec)
+    hipLaunchKernelGGL((k_observe<true, false, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out, sym,
+                       qden, eps, ws, counter);
   else
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, codes, mask, n, src);
+    hipLaunchKernelGGL((k_observe<false, false, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
+                       sym, qden, eps, ws, counter);
 }
 
-
-template <bool VEC, bool NT>
-void launch_lsq(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
-                double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
-                hipStream_t st) {
-  const int pf = 0;
-  if (zpl)
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, n, src,
-                       gscale, pf, grad_out, ws, counter);
-  else
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, n, src,
-                       gscale, pf, grad_out, ws, counter);
+int observe(const float *x, int64_t n, int act, double *stats_out, float *run_minmax, double *qp_out,
+            int symmetric, double qden, double eps, double *ws, int64_t ws_len, uint32_t *counter,
+            void *stream) {
+  if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
+  const bool vec = aligned16(x) && n % 4 == 0;
+  const int grid = reduce_grid(cdiv(n, 4), 4);
+  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
+           symmetric, qden, eps, ws, counter, grid, (hipStream_t)stream);
+  return launch_rc();
 }
 
 }  // namespace vsiq
@@ -473,42 +315,19 @@ int vsiq_selftest_fq(int mode, const float *scales, const float *zero_points, in
   return launch_rc();
 }
 
-int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t n,
-                    const double *qp_dev, const double *scale_dev, double scale_host,
-                    const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
-                    int qmax, void *stream) {
-  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y))) return VSIQ_E_ARG;
-  if (n == 0) return 0;
-  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
-  hipStream_t st = (hipStream_t)stream;
-  QPSrc src{qp_dev, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax,
-            qp_dev ? 0 : zp_round, discrete ? 1 : 0};
-  const bool vec = (n % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
-  const bool nt = g_tune.nontemporal != 0;
-  uint8_t *c = (uint8_t *)codes;
-  VSIQ_B2(launch_fq_fwd, vec, nt, x, y, c, mask, n, src, st);
-  return launch_rc();
-}
-
 int vsiq_observe_f32(const float *x, int64_t n, double *stats_out, float *run_minmax,
                      double *qp_out, int symmetric, double qden, double eps, double *ws,
                      int64_t ws_len, uint32_t *counter, void *stream) {
-  if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
-  const bool vec = aligned16(x) && n % 4 == 0;
-  const int grid = reduce_grid(cdiv(n, 4), 4);
-  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 g(grid), b(kBlock);
-  if (vec && g_tune.nontemporal)
-    hipLaunchKernelGGL((k_observe<true, true>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
-                       symmetric, qden, eps, ws, counter);
-  else if (vec)
-    hipLaunchKernelGGL((k_observe<true, false>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
-                       symmetric, qden, eps, ws, counter);
-  else
-    hipLaunchKernelGGL((k_observe<false, false>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
-                       symmetric, qden, eps, ws, counter);
-  return launch_rc();
+  return observe(x, n, kActNone, stats_out, run_minmax, qp_out, symmetric, qden, eps, ws, ws_len,
+                 counter, stream);
+}
+
+int vsiq_act_observe_f32(const float *c, int64_t n, int act, double *stats_out, float *run_minmax,
+                         double *qp_out, int symmetric, double qden, double eps, double *ws,
+                         int64_t ws_len, uint32_t *counter, void *stream) {
+  if (act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  return observe(c, n, act, stats_out, run_minmax, qp_out, symmetric, qden, eps, ws, ws_len, counter,
+                 stream);
 }
 
 int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out, int symmetric,
@@ -516,24 +335,6 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
   if (!stats) return VSIQ_E_ARG;
   hipLaunchKernelGGL(k_observe_finalize, dim3(1), dim3(kWave), 0, (hipStream_t)stream, stats,
                      run_minmax, qp_out, symmetric, qden, eps);
-  return launch_rc();
-}
-
-int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
-                     const double *scale_dev, double scale_host, const double *zp_dev,
-                     double zp_host, int zp_learn, int qmin, int qmax, double gscale,
-                     double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
-                     void *stream) {
-  if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax) return VSIQ_E_ARG;
-  const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
-  const int64_t grid = lsq_grid(cdiv(n, 4));
-  if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
-  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
-  // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
-  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
-  const bool nt = g_tune.nontemporal != 0;
-  VSIQ_B2(launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
-          (hipStream_t)stream);
   return launch_rc();
 }
 

@@ -1,0 +1,103 @@
+// k_fq.hip — K1 per-tensor fake-quant forward (optionally behind a fused ReLU/SiLU,
+// K5), and its C ABI entry points.
+#include "vsiq_common.cuh"
+
+namespace vsiq {
+
+// ----------------------------------------------------------------------------
+// K1: y = fq(act(x)), one-shot (kFlatU groups per lane, no loop: exact vmcnt)
+// ----------------------------------------------------------------------------
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+__global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
+                                                   uint8_t *__restrict__ codes,
+                                                   uint64_t *__restrict__ mask, int64_t n,
+                                                   QPSrc src) {
+  const QP p = load_qp(src);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;   // lanes chunk-aligned
+  f4 v[kFlatU];
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+  GroupOut go[kFlatU];
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4<ACT>(v[u]), p, base + u * kBlock, n);
+    if (MASK) mask_put(mlo, mhi, u, go[u].b);
+  }
+  const int lane = threadIdx.x % kWave;
+#pragma unroll
+  for (int u = 0; u < kFlatU; ++u) {
+    const int64_t i = base + u * kBlock;
+    if (i - lane >= ng) break;   // whole wave past the end (uniform)
+    fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[u]);
+  }
+  if (MASK && lane < 4 * kFlatU) {   // lane 4u+j: word j of slot u's chunk
+    const int64_t first = base - lane + (lane >> 2) * kBlock;
+    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
+  }
+}
+
+template <int ACT, bool VEC, bool NT>
+void launch_fq_act(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
+                   const QPSrc &src, hipStream_t st) {
+  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4))), block(kBlock);
+  if (codes && mask)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, true, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else if (codes)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, false, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else if (mask)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, true, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
+  else
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, false, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
+}
+
+template <int ACT>
+void launch_fq(bool vec, bool nt, const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
+               const QPSrc &src, hipStream_t st) {
+  if (vec && nt) launch_fq_act<ACT, true, true>(x, y, codes, mask, n, src, st);
+  else if (vec) launch_fq_act<ACT, true, false>(x, y, codes, mask, n, src, st);
+  else if (nt) launch_fq_act<ACT, false, true>(x, y, codes, mask, n, src, st);
+  else launch_fq_act<ACT, false, false>(x, y, codes, mask, n, src, st);
+}
+
+int fq_fwd(const float *x, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+           const double *qp_dev, const double *scale_dev, double scale_host, const double *zp_dev,
+           double zp_host, int zp_round, int discrete, int qmin, int qmax, void *stream) {
+  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y)) || act < kActNone || act > kActSilu)
+    return VSIQ_E_ARG;
+  if (n == 0) return 0;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  QPSrc src{qp_dev, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax,
+            qp_dev ? 0 : zp_round, discrete ? 1 : 0};
+  const bool vec = (n % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
+  const bool nt = g_tune.nontemporal != 0;
+  uint8_t *c = (uint8_t *)codes;
+  VSIQ_ACT(act, launch_fq, vec, nt, x, y, c, mask, n, src, st);
+  return launch_rc();
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int vsiq_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t n,
+                    const double *qp_dev, const double *scale_dev, double scale_host,
+                    const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
+                    int qmax, void *stream) {
+  return fq_fwd(x, y, codes, mask, n, kActNone, qp_dev, scale_dev, scale_host, zp_dev, zp_host,
+                zp_round, discrete, qmin, qmax, stream);
+}
+
+int vsiq_act_fq_fwd_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                        const double *qp_dev, const double *scale_dev, double scale_host,
+                        const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
+                        int qmax, void *stream) {
+  return fq_fwd(c, y, codes, mask, n, act, qp_dev, scale_dev, scale_host, zp_dev, zp_host,
+                zp_round, discrete, qmin, qmax, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,202 @@
+// k_lsq.hip — K4 learnable (LSQ) backward: grad_x + f64 scale / zero-point gradient
+// sums (optionally through a fused ReLU/SiLU, K5), and its C ABI entry points.
+#include "vsiq_common.cuh"
+
+namespace vsiq {
+
+// ----------------------------------------------------------------------------
+// K4: learnable (LSQ) backward, grad_x + f64 scale / zp gradient sums
+// ----------------------------------------------------------------------------
+struct LsqAcc {
+  double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
+};
+
+// one element of the learnable backward; returns grad_x, adds the f64 gradient terms
+template <bool ZPL, bool IEEE>
+__device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
+  const float u = fdiv_t<IEEE>(x, p.d);
+  const float r = __builtin_rintf(u + p.z);
+  const float q = fq_clamp(r, p.lo, p.hi);
+  const bool m = (r >= p.lo && r <= p.hi);
+  const float gq = g * p.s;                 // MulBackward0 (self)
+  const float gm = m ? gq : 0.0f;           // ClampBackward1
+  const float t1 = g * (q - p.z);           // MulBackward0 (other)
+  const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
+  const float t2 = (-gm) * xs;              // DivBackward0 (other)
+  if (valid) {
+    acc.t += (double)t1 + (double)t2;
+    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
+  }
+  return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
+}
+
+// all three divisions of an element inside the fast-division range?
+__device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
+  const float u = fdiv_fast(x, p.d);
+  const float r = __builtin_rintf(u + p.z);
+  const bool m = (r >= p.lo && r <= p.hi);
+  const float gm = m ? g * p.s : 0.0f;
+  return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
+}
+
+__device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
+  __shared__ double s[2][kWaves];
+  c.t = wave_reduce(c.t, AddD());
+  c.z = wave_reduce(c.z, AddD());
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) { s[0][w] = c.t; s[1][w] = c.z; }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int i = 1; i < kWaves; ++i) { c.t += s[0][i]; c.z += s[1][i]; }
+  __syncthreads();
+}
+
+// xc: the loaded input -- the quantizer input itself, or (ACT) the pre-activation c
+// whose act(c) the forward quantized; grad_x then goes through the act's backward
+template <bool VEC, bool NT, bool ZPL, int ACT>
+__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv,
+                                          const QP &p, LsqAcc &c) {
+  const f4 xv = act_fwd4<ACT>(xc);
+  const int nv = i < ng ? valid_in_group(i, n) : 0;
+  const uint32_t ok = lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
+                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p);
+  f4 o;
+  if (ok) {
+    o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
+    o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);
+    o.z = lsq_elem<ZPL, false>(xv.z, gv.z, p, c, nv > 2);
+    o.w = lsq_elem<ZPL, false>(xv.w, gv.w, p, c, nv > 3);
+  } else {   // rare (divergent): an element outside the fast-division range
+    o.x = lsq_elem<ZPL, true>(xv.x, gv.x, p, c, nv > 0);
+    o.y = lsq_elem<ZPL, true>(xv.y, gv.y, p, c, nv > 1);
+    o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
+    o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
+  }
+  if (nv > 0) store_group<VEC, NT>(gx, i, n, act_bwd4<ACT>(o, xc));
+}
+
+template <bool VEC, bool NT, bool ZPL, int ACT>
+__global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
+                                                    const float *__restrict__ x,
+                                                    float *__restrict__ gx, int64_t n,
+                                                    QPSrc src, double gscale, int prefetch,
+                                                    double *__restrict__ grad_out,
+                                                    double *__restrict__ ws,
+                                                    uint32_t *__restrict__ counter) {
+  const QP p = load_qp(src);
+  LsqAcc c{0.0, 0.0};
+  const int64_t ng = cdiv(n, 4);
+  (void)prefetch;
+  // kLsqGroups groups per lane, straight-line (fully unrolled): group k+2 is loaded
+  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kLsqGroups + threadIdx.x;
+  f4 xv[kLsqGroups], gv[kLsqGroups];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
+    gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
+  }
+#pragma unroll
+  for (int k = 0; k < kLsqGroups; ++k) {
+    if (k + 2 < kLsqGroups) {
+      xv[k + 2] = load_group_c<VEC, NT>(x, base + (k + 2) * kBlock, ng, n);
+      gv[k + 2] = load_group_c<VEC, NT>(g, base + (k + 2) * kBlock, ng, n);
+    }
+    lsq_group<VEC, NT, ZPL, ACT>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
+  }
+  lsq_block_reduce(c);
+  if (threadIdx.x == 0) {
+    double *r = ws + (int64_t)blockIdx.x * kPartials;
+    partial_store(r + 0, c.t);
+    partial_store(r + 1, c.z);
+  }
+  if (!arrive_last(counter)) return;
+  c = LsqAcc{0.0, 0.0};
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
+    const double *r = ws + (int64_t)b * kPartials;
+    c.t += partial_load(r + 0);
+    c.z += partial_load(r + 1);
+  }
+  lsq_block_reduce(c);
+  if (threadIdx.x == 0) {
+    grad_out[0] = c.t * gscale;
+    double gz = 0.0;
+    if (ZPL) {
+      // ClampBackward of zero_point_rounding (uniform.py:101): in-range test on round(zp)
+      const double zr = __builtin_rint(src.zdev ? *src.zdev : src.zhost);   // NaN -> not in range
+      const bool zin = zr >= (double)p.lo && zr <= (double)p.hi;
+      gz = zin ? c.z * gscale : 0.0;
+    }
+    grad_out[1] = gz;
+    *counter = 0u;
+  }
+}
+
+
+template <int ACT, bool VEC, bool NT>
+void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
+                    double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
+                    hipStream_t st) {
+  const int pf = 0;
+  if (zpl)
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
+                       gx, n, src, gscale, pf, grad_out, ws, counter);
+  else
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
+                       gx, n, src, gscale, pf, grad_out, ws, counter);
+}
+
+template <int ACT>
+void launch_lsq(bool vec, bool nt, const float *g, const float *x, float *gx, int64_t n,
+                const QPSrc &src, int zpl, double gscale, double *grad_out, double *ws,
+                uint32_t *counter, int64_t grid, hipStream_t st) {
+  if (vec && nt) launch_lsq_act<ACT, true, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+  else if (vec) launch_lsq_act<ACT, true, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+  else if (nt) launch_lsq_act<ACT, false, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+  else launch_lsq_act<ACT, false, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+}
+
+int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const double *scale_dev,
+            double scale_host, const double *zp_dev, double zp_host, int zp_learn, int qmin, int qmax,
+            double gscale, double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+            void *stream) {
+  if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax || act < kActNone ||
+      act > kActSilu)
+    return VSIQ_E_ARG;
+  const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
+  const int64_t grid = lsq_grid(cdiv(n, 4));
+  if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
+  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
+  const bool nt = g_tune.nontemporal != 0;
+  VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
+           (hipStream_t)stream);
+  return launch_rc();
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
+                     const double *scale_dev, double scale_host, const double *zp_dev,
+                     double zp_host, int zp_learn, int qmin, int qmax, double gscale,
+                     double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+                     void *stream) {
+  return lsq_bwd(g, x, gx, n, kActNone, scale_dev, scale_host, zp_dev, zp_host, zp_learn, qmin, qmax,
+                 gscale, grad_out, ws, ws_len, counter, stream);
+}
+
+int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, int act,
+                         const double *scale_dev, double scale_host, const double *zp_dev,
+                         double zp_host, int zp_learn, int qmin, int qmax, double gscale,
+                         double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
+                         void *stream) {
+  return lsq_bwd(g, c, gc, n, act, scale_dev, scale_host, zp_dev, zp_host, zp_learn, qmin, qmax,
+                 gscale, grad_out, ws, ws_len, counter, stream);
+}
+
+}  // extern "C"

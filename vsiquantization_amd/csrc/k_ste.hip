@@ -10,9 +10,12 @@ namespace vsiq {
 // one-shot: workgroup b covers chunk b % chunks of row b / chunks (kFlatU groups per
 // lane).  A wave's 64 groups are one 256-element mask chunk: its four mask words
 // are wave-uniform, read with scalar loads and used directly as lane masks.
-template <bool VEC, bool NT>
+// ACT (K5): `pre` holds the pre-activation c of a fused ReLU/SiLU; the result is
+// the activation's backward applied to the quantizer's grad_x.
+template <bool VEC, bool NT, int ACT>
 __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     const uint64_t *__restrict__ mask,
+                                                    const float *__restrict__ pre,
                                                     float *__restrict__ gx, int64_t rowlen,
                                                     uint32_t chunks, const double *__restrict__ sdev,
                                                     double shost) {
@@ -26,12 +29,13 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
   const uint64_t *mr = mask + row * mask_words_per_row(rowlen);
   const int64_t base = chunk * kBlock * kFlatU + threadIdx.x;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  f4 v[kFlatU];
+  f4 v[kFlatU], cv[kFlatU];
   uint64_t w[kFlatU][4];
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
     const int64_t i = base + u * kBlock;
     v[u] = load_group<VEC, NT>(gr, i < ng ? i : ng - 1, rowlen);
+    if (ACT) cv[u] = load_group<VEC, NT>(pre + row * rowlen, i < ng ? i : ng - 1, rowlen);
     int64_t c = chunk * (kBlock / kWave) * kFlatU + u * (kBlock / kWave) + wave0;
     c = c < nchunk ? c : nchunk - 1;
 #pragma unroll
@@ -56,6 +60,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
       o[u].z = ste_ieee(v[u].z, m2, d);
       o[u].w = ste_ieee(v[u].w, m3, d);
     }
+    if (ACT) o[u] = act_bwd4<ACT>(o[u], cv[u]);
   }
 #pragma unroll
   for (int u = 0; u < kFlatU; ++u) {
@@ -65,12 +70,38 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
 }
 
 
-template <bool VEC, bool NT>
-void launch_ste(const float *g, const uint64_t *m, float *gx, int64_t rows, int64_t rowlen,
-                const double *sdev, double shost, hipStream_t st) {
+template <int ACT, bool VEC, bool NT>
+void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *gx, int64_t rows,
+                    int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
   const int64_t chunks = oneshot_grid(cdiv(rowlen, 4));
-  hipLaunchKernelGGL((k_ste_bwd<VEC, NT>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0, st, g, m,
-                     gx, rowlen, (uint32_t)chunks, sdev, shost);
+  hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0, st, g,
+                     m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost);
+}
+
+template <int ACT>
+void launch_ste(bool vec, bool nt, const float *g, const uint64_t *m, const float *pre, float *gx,
+                int64_t rows, int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
+  if (vec && nt) launch_ste_act<ACT, true, true>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
+  else if (vec) launch_ste_act<ACT, true, false>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
+  else if (nt) launch_ste_act<ACT, false, true>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
+  else launch_ste_act<ACT, false, false>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
+}
+
+int ste_bwd(const float *g, const uint64_t *mask, const float *pre, float *gx, int64_t n, int act,
+            const double *scale_dev, int64_t rowlen, double scale_host, void *stream) {
+  if (n < 0 || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  if (n == 0) return 0;
+  if (!g || !mask || !gx || (act != kActNone && !pre)) return VSIQ_E_ARG;
+  if (!aligned8(mask)) return VSIQ_E_ALIGN;
+  if (!scale_dev || rowlen <= 0) rowlen = n;
+  if (n % rowlen != 0) return VSIQ_E_ARG;
+  const int64_t rows = n / rowlen;
+  if (rows * oneshot_grid(cdiv(rowlen, 4)) > 0x7fffffffLL) return VSIQ_E_ARG;
+  const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(gx) && (!pre || aligned16(pre));
+  const bool nt = g_tune.nontemporal != 0;
+  VSIQ_ACT(act, launch_ste, vec, nt, g, mask, pre, gx, rows, rowlen, scale_dev, scale_host,
+           (hipStream_t)stream);
+  return launch_rc();
 }
 
 }  // namespace vsiq
@@ -81,18 +112,13 @@ extern "C" {
 
 int vsiq_ste_bwd_f32(const float *g, const uint64_t *mask, float *gx, int64_t n,
                      const double *scale_dev, int64_t rowlen, double scale_host, void *stream) {
-  if (n < 0) return VSIQ_E_ARG;
-  if (n == 0) return 0;
-  if (!g || !mask || !gx) return VSIQ_E_ARG;
-  if (!aligned8(mask)) return VSIQ_E_ALIGN;
-  if (!scale_dev || rowlen <= 0) rowlen = n;
-  if (n % rowlen != 0) return VSIQ_E_ARG;
-  const int64_t rows = n / rowlen;
-  if (rows * oneshot_grid(cdiv(rowlen, 4)) > 0x7fffffffLL) return VSIQ_E_ARG;
-  const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(gx);
-  const bool nt = g_tune.nontemporal != 0;
-  VSIQ_B2(launch_ste, vec, nt, g, mask, gx, rows, rowlen, scale_dev, scale_host, (hipStream_t)stream);
-  return launch_rc();
+  return ste_bwd(g, mask, nullptr, gx, n, kActNone, scale_dev, rowlen, scale_host, stream);
+}
+
+int vsiq_act_ste_bwd_f32(const float *g, const uint64_t *mask, const float *c, float *gc, int64_t n,
+                         int act, const double *scale_dev, int64_t rowlen, double scale_host,
+                         void *stream) {
+  return ste_bwd(g, mask, c, gc, n, act, scale_dev, rowlen, scale_host, stream);
 }
 
 }  // extern "C"

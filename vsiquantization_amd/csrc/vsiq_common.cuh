@@ -289,6 +289,59 @@ __device__ __forceinline__ float ste_ieee(float g, bool m, const SteDiv &d) {
   return (m ? g * d.s : 0.0f) / d.s;             // ClampBackward1, DivBackward0 (IEEE)
 }
 
+// ----------------------------------------------------------------------------
+// Activation fused in front of the activation quantizer (K5): ConvBnReLU's
+// F.relu / F.silu (fused.py:124-134) followed by quantize_out (fake_quantize.py:49-50).
+// The forward reads the conv output c once; the backward re-derives act(c) and
+// applies the activation's backward to the quantizer's grad_x.
+//   relu:  c < 0 ? 0 : c          (torch CPU: relu(-0.0) = -0.0, relu(NaN) = NaN)
+//          bwd: threshold_backward(g, relu(c), 0) = c <= 0 ? 0 : g  (NaN passes g)
+//   silu:  c / (1 + exp(-c))      (torch CPU silu_kernel)
+//          bwd: (g * sig) * fma(c, 1 - sig, 1),  sig = 1 / (1 + exp(-c))  (torch's
+//          vectorized CPU kernel contracts the inner multiply-add); exp differs from
+//          torch's Sleef exp by about an ulp, so SiLU is within a few ulp, not bitwise
+// ----------------------------------------------------------------------------
+enum { kActNone = 0, kActRelu = 1, kActSilu = 2 };
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float c) {
+  if (ACT == kActRelu) return c < 0.0f ? 0.0f : c;
+  if (ACT == kActSilu) return c / (1.0f + __builtin_expf(-c));
+  return c;
+}
+
+template <int ACT>
+__device__ __forceinline__ f4 act_fwd4(f4 v) {
+  if (ACT == kActNone) return v;
+  f4 o;
+  o.x = act_fwd<ACT>(v.x); o.y = act_fwd<ACT>(v.y); o.z = act_fwd<ACT>(v.z); o.w = act_fwd<ACT>(v.w);
+  return o;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_bwd(float g, float c) {
+  if (ACT == kActRelu) return c <= 0.0f ? 0.0f : g;
+  if (ACT == kActSilu) {
+    const float sig = 1.0f / (1.0f + __builtin_expf(-c));
+    return (g * sig) * __builtin_fmaf(c, 1.0f - sig, 1.0f);
+  }
+  return g;
+}
+
+template <int ACT>
+__device__ __forceinline__ f4 act_bwd4(f4 g, f4 c) {
+  if (ACT == kActNone) return g;
+  f4 o;
+  o.x = act_bwd<ACT>(g.x, c.x); o.y = act_bwd<ACT>(g.y, c.y);
+  o.z = act_bwd<ACT>(g.z, c.z); o.w = act_bwd<ACT>(g.w, c.w);
+  return o;
+}
+
+// runtime act -> template dispatch
+#define VSIQ_ACT(ACTV, F, ...)                                   \
+  ((ACTV) == kActRelu ? F<kActRelu>(__VA_ARGS__)                 \
+                      : (ACTV) == kActSilu ? F<kActSilu>(__VA_ARGS__) : F<kActNone>(__VA_ARGS__))
+
 // where qparams come from (one struct, passed by value -> kernarg / SGPRs)
 struct QPSrc {
   const double *qp;     // observer record [scale, zp, ...] or null

@@ -9,6 +9,11 @@ eager torch ops in the reference:
   per_channel_observe_fq   per-channel MinMax + UniformQuantizer (K3)
   FakeQuantFixedFn         autograd of uniform.py:55,95 with fixed qparams (STE)
   FakeQuantLearnFn         autograd of uniform.py:47-56 (LSQ: ScaleGradient, STE) (K4)
+
+Every op takes an optional ``act`` ("relu" / "silu", K5): the op is then applied
+to act(x) without materializing it -- the fused layers' F.relu / F.silu before
+quantize_out (modules/fused.py:124-134, quantizers/fake_quantize.py:49-50) -- and
+the backward ops return the gradient with respect to the pre-activation x.
 """
 from __future__ import annotations
 
@@ -58,7 +63,7 @@ def _i64(n):
 # --------------------------------------------------------------------------- forward (K1)
 def fake_quant(x: torch.Tensor, scale, zero_point, qmin: int, qmax: int, *, zp_round: bool = False,
                qp: torch.Tensor | None = None, want_mask: bool = False, want_codes: bool = False,
-               discrete: bool = False):
+               discrete: bool = False, act=None):
     """y = (clamp(rint(x/s + zp), qmin, qmax) - zp) * s  (uniform.py:55,95), fp32, bit-exact.
 
     qp: optional observer record (f64[QP_LEN] on x.device) used instead of scale/zero_point.
@@ -76,16 +81,24 @@ def fake_quant(x: torch.Tensor, scale, zero_point, qmin: int, qmax: int, *, zp_r
     else:
         sd, sh = scalar_source(scale, dev)
         zd, zh = scalar_source(zero_point, dev)
-    rc = H.lib().vsiq_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(x.numel()),
-                                 H.ptr(qp), H.ptr(sd), sh, H.ptr(zd), zh, int(bool(zp_round)),
-                                 int(bool(discrete)), int(qmin), int(qmax), H.stream_of(dev))
-    H.check(rc, "vsiq_fq_fwd_f32")
+    rc = H.lib().vsiq_act_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(x.numel()),
+                                     H.act_code(act), H.ptr(qp), H.ptr(sd), sh, H.ptr(zd), zh,
+                                     int(bool(zp_round)), int(bool(discrete)), int(qmin), int(qmax),
+                                     H.stream_of(dev))
+    H.check(rc, "vsiq_act_fq_fwd_f32")
     return y, mask, codes
 
 
-def ste_backward(g: torch.Tensor, mask: torch.Tensor, scale, rowlen: int = 0) -> torch.Tensor:
-    """gx = (mask ? g*s : 0) / s  — autograd of uniform.py:55,95 with a fixed scale."""
+def ste_backward(g: torch.Tensor, mask: torch.Tensor, scale, rowlen: int = 0, *, pre=None,
+                 act=None) -> torch.Tensor:
+    """gx = (mask ? g*s : 0) / s  — autograd of uniform.py:55,95 with a fixed scale;
+    with ``act``, the activation's backward at the pre-activation ``pre`` follows."""
     g = H.require_device_f32(g, "grad_output")
+    a = H.act_code(act)
+    if a != H.ACT_NONE:
+        pre = H.require_device_f32(pre, "pre-activation")
+        if pre.shape != g.shape:
+            raise ValueError(f"pre-activation shape {tuple(pre.shape)} != grad shape {tuple(g.shape)}")
     dev = g.device
     gx = torch.empty_like(g)
     if isinstance(scale, torch.Tensor) and scale.device.type == "cuda" and scale.numel() > 1:
@@ -93,9 +106,9 @@ def ste_backward(g: torch.Tensor, mask: torch.Tensor, scale, rowlen: int = 0) ->
     else:
         sd, sh = scalar_source(scale, dev)
         rowlen = 0
-    rc = H.lib().vsiq_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(gx), _i64(g.numel()), H.ptr(sd),
-                                  _i64(rowlen), sh, H.stream_of(dev))
-    H.check(rc, "vsiq_ste_bwd_f32")
+    rc = H.lib().vsiq_act_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(pre if a else None), H.ptr(gx),
+                                      _i64(g.numel()), a, H.ptr(sd), _i64(rowlen), sh, H.stream_of(dev))
+    H.check(rc, "vsiq_act_ste_bwd_f32")
     return gx
 
 
@@ -103,9 +116,13 @@ class FakeQuantFixedFn(torch.autograd.Function):
     """Fixed-qparam fake quant with the reference's STE gradient (x only)."""
 
     @staticmethod
-    def forward(ctx, x, scale, zero_point, qmin, qmax, qp):
-        y, mask, _ = fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, want_mask=True)
-        ctx.save_for_backward(mask)
+    def forward(ctx, x, scale, zero_point, qmin, qmax, qp, act=None):
+        y, mask, _ = fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, want_mask=True, act=act)
+        ctx.act = act
+        if H.act_code(act) != H.ACT_NONE:
+            ctx.save_for_backward(mask, x)
+        else:
+            ctx.save_for_backward(mask)
         if qp is not None:
             ctx.scale = qp[H.QP_SCALE:H.QP_SCALE + 1]
         else:
@@ -114,18 +131,22 @@ class FakeQuantFixedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        (mask,) = ctx.saved_tensors
-        return ste_backward(gy.contiguous(), mask, ctx.scale), None, None, None, None, None
+        saved = ctx.saved_tensors
+        pre = saved[1] if len(saved) > 1 else None
+        gx = ste_backward(gy.contiguous(), saved[0], ctx.scale, pre=pre, act=ctx.act)
+        return gx, None, None, None, None, None, None
 
 
-def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None):
+def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None, act=None):
     if x.requires_grad and torch.is_grad_enabled():
-        return FakeQuantFixedFn.apply(x, scale, zero_point, qmin, qmax, qp)
-    return fake_quant(x, scale, zero_point, qmin, qmax, qp=qp)[0]
+        return FakeQuantFixedFn.apply(x, scale, zero_point, qmin, qmax, qp, act)
+    return fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, act=act)[0]
 
 
 # --------------------------------------------------------------------------- learnable (K4)
-def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
+    """K4: (grad_x, f64[2] {grad_scale, grad_zp}); with ``act``, x is the pre-activation
+    and grad_x goes through the activation's backward."""
     g = H.require_device_f32(g, "grad_output")
     dev = g.device
     gx = torch.empty_like(g)
@@ -133,11 +154,11 @@ def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
     sd, sh = scalar_source(scale, dev)
     zd, zh = scalar_source(zero_point, dev)
     w = H.workspace(dev, g.numel())
-    rc = H.lib().vsiq_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), H.ptr(sd), sh,
-                                  H.ptr(zd), zh, int(bool(learn_zp)), int(qmin), int(qmax),
-                                  float(gscale), H.ptr(grads), H.ptr(w.ws), _i64(w.ws_len),
-                                  H.ptr(w.counter), H.stream_of(dev))
-    H.check(rc, "vsiq_lsq_bwd_f32")
+    rc = H.lib().vsiq_act_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), H.act_code(act),
+                                      H.ptr(sd), sh, H.ptr(zd), zh, int(bool(learn_zp)), int(qmin),
+                                      int(qmax), float(gscale), H.ptr(grads), H.ptr(w.ws),
+                                      _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
+    H.check(rc, "vsiq_act_lsq_bwd_f32")
     return gx, grads
 
 
@@ -148,32 +169,32 @@ class FakeQuantLearnFn(torch.autograd.Function):
     form (ScaleGradient x gscale on scale and zp, ClampBackward1 mask, STE)."""
 
     @staticmethod
-    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
         x = H.require_device_f32(x)
-        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp)
+        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, act=act)
         ctx.save_for_backward(x)
         ctx.scale, ctx.zp = scale, zero_point
-        ctx.args = (qmin, qmax, gscale, learn_zp)
+        ctx.args = (qmin, qmax, gscale, learn_zp, act)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
-        qmin, qmax, gscale, learn_zp = ctx.args
+        qmin, qmax, gscale, learn_zp, act = ctx.args
         s, z = ctx.scale, ctx.zp
-        gx, grads = lsq_backward(gy.contiguous(), x, s, z, qmin, qmax, gscale, learn_zp)
+        gx, grads = lsq_backward(gy.contiguous(), x, s, z, qmin, qmax, gscale, learn_zp, act=act)
         gs = gz = None
         if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
             gs = grads[0].to(device=s.device, dtype=s.dtype).reshape(s.shape)
         if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
             gz = grads[1].to(device=z.device, dtype=z.dtype).reshape(z.shape)
-        return gx, gs, gz, None, None, None, None
+        return gx, gs, gz, None, None, None, None, None
 
 
 # --------------------------------------------------------------------------- observer (K2)
 def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: float = 1e-8,
                    run_minmax: torch.Tensor | None = None, want_qp: bool = True,
-                   want_stats: bool = True):
+                   want_stats: bool = True, act=None):
     """One pass over x: min/max/NaN/sums -> running state update -> f64 qparams (no sync).
 
     Returns (qp f64[QP_LEN] | None, stats f64[ST_LEN] | None)."""
@@ -184,10 +205,11 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev) if want_qp else None
     st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev) if want_stats else None
     w = H.workspace(dev, x.numel())
-    rc = H.lib().vsiq_observe_f32(H.ptr(x), _i64(x.numel()), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
-                                  int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps),
-                                  H.ptr(w.ws), _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
-    H.check(rc, "vsiq_observe_f32")
+    rc = H.lib().vsiq_act_observe_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), H.ptr(st),
+                                      H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
+                                      qden(symmetric, num_bits, eps), float(eps), H.ptr(w.ws),
+                                      _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
+    H.check(rc, "vsiq_act_observe_f32")
     return qp, st
 
 

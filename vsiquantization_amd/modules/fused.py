@@ -40,21 +40,44 @@ def _activation(x, is_relu):
     return F.relu(x) if is_relu else F.silu(x)
 
 
-class _ConvCore(FakeQuantize):
-    """conv2d (+ unfolded BN) (+ ReLU/SiLU) core shared by the Conv* layers."""
+class _FusedActCore(FakeQuantize):
+    """Shared forward of the fused layers.
+
+    ``run_forward_core`` keeps the reference's conv/linear -> (BN) -> ReLU/SiLU.
+    When the output is quantized, ``forward`` instead hands the pre-activation to
+    the activation quantizer with ``act=`` (K5): ReLU/SiLU, the activation
+    observer and the fake quant then run on the conv output in one pass, and the
+    backward returns the gradient with respect to the pre-activation directly."""
 
     has_act = True
 
-    def _conv(self, x, weights, bias):
-        c = self.conv_fuse
-        return F.conv2d(x, weights, bias, stride=c.stride, padding=c.padding, dilation=c.dilation,
-                        groups=c.groups)
+    def _pre_act(self, x, weights, bias):
+        raise NotImplementedError
 
     def run_forward_core(self, x, weights, bias):
-        x = self._conv(x, weights, bias)
+        x = self._pre_act(x, weights, bias)
+        return _activation(x, self.is_relu) if self.has_act else x
+
+    def forward(self, x):
+        if not (self.has_act and self.quantize_out):
+            return super().forward(x)
+        if self.quantize_inp:
+            x = self.quantize_activation(x)
+        w, b = self.get_weight_bias()
+        c = self._pre_act(x, self.quantize_weights(w), b)
+        return self.activation_quantizer.quantize(c, act="relu" if self.is_relu else "silu")
+
+
+class _ConvCore(_FusedActCore):
+    """conv2d (+ unfolded BN) (+ ReLU/SiLU) core shared by the Conv* layers."""
+
+    def _pre_act(self, x, weights, bias):
+        c = self.conv_fuse
+        x = F.conv2d(x, weights, bias, stride=c.stride, padding=c.padding, dilation=c.dilation,
+                     groups=c.groups)
         if not getattr(self, "is_fuse_bn", True):
             x = self.bn(x)
-        return _activation(x, self.is_relu) if self.has_act else x
+        return x
 
 
 class ConvBnReLU(_ConvCore):
@@ -114,17 +137,15 @@ class Conv(_ConvCore):
             self.conv_fuse.bias.data.copy_(cv.bias.data)
 
 
-class _LinearCore(FakeQuantize):
-    has_act = True
-
+class _LinearCore(_FusedActCore):
     def get_weight_bias(self):
         return self.linear_fuse.weight, self.linear_fuse.bias
 
-    def run_forward_core(self, x, weights, bias):
+    def _pre_act(self, x, weights, bias):
         x = F.linear(x, weights, bias)
         if not getattr(self, "is_fuse_bn", True):
             x = self.bn(x)
-        return _activation(x, self.is_relu) if self.has_act else x
+        return x
 
     def _copy_linear(self, linear):
         self.linear_fuse = nn.Linear(linear.in_features, linear.out_features,

@@ -87,11 +87,12 @@ class MinMaxObserver(BaseObserver):
         self._dirty = False
 
     # ------------------------------------------------------------------ protocol
-    def observe_device(self, x, want_stats=True, want_qp=True):
-        """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device."""
+    def observe_device(self, x, want_stats=True, want_qp=True, act=None):
+        """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device.
+        ``act``: observe act(x) (fused ReLU/SiLU, K5) without materializing it."""
         state = self.device_state(H.require_device_f32(x).device)
         qp, st = observe_tensor(x, symmetric=self.symmetric, num_bits=self.num_bits, eps=self.eps,
-                                run_minmax=state, want_qp=want_qp, want_stats=want_stats)
+                                run_minmax=state, want_qp=want_qp, want_stats=want_stats, act=act)
         self._dirty = True
         return qp, st
 

@@ -9,10 +9,14 @@ per-tensor UniformQuantizer behaviour.  A learnable per-channel scale is the
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 
 from ..fakequant import PerChannelFQFn, per_channel_fake_quant
 from ..utils.registry import register_class
 from .uniform import UniformQuantizer
+
+
+_ACTS = {"relu": F.relu, "silu": F.silu}
 
 
 def _per_channel(v) -> bool:
@@ -23,9 +27,11 @@ def _per_channel(v) -> bool:
 class PerChannelUniformQuantizer(UniformQuantizer):
     axis = 0
 
-    def quantize(self, x, scale, zero_point, is_learning_scale):
+    def quantize(self, x, scale, zero_point, is_learning_scale, act=None):
         if not (_per_channel(scale) or _per_channel(zero_point)):
-            return super().quantize(x, scale, zero_point, is_learning_scale)
+            return super().quantize(x, scale, zero_point, is_learning_scale, act=act)
+        if act is not None:   # per-channel activations: activation first (torch), then K3-fixed
+            x = _ACTS[act](x)
         if is_learning_scale:
             raise NotImplementedError("learnable per-channel scale: planned (SURVEY §8f row 2)")
         C = x.shape[0]

@@ -22,6 +22,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import _hip as H
 from ..fakequant import observe_finalize, observe_tensor, stats_from_row_sums
@@ -31,6 +32,7 @@ from ..utils.registry import CLASS_REGISTRY
 from .per_channel import PerChannelUniformQuantizer
 
 _STAT_NAMES = ("mean_abs_x", "mean_x", "std")
+_ACTS = {"relu": F.relu, "silu": F.silu}
 
 
 class _StatList:
@@ -96,19 +98,22 @@ class QuantizationManager(nn.Module):
         return (isinstance(x, torch.Tensor) and x.device.type == "cuda"
                 and isinstance(self.observer, (MinMaxObserver, PerChannelMinMaxObserver)))
 
-    def collect_qparameter(self, x):
-        """Observe ``x`` and refresh scale/zero_point when calibrating (qm.py:55-71)."""
+    def collect_qparameter(self, x, act=None):
+        """Observe ``x`` (or act(x), K5) and refresh scale/zero_point when calibrating
+        (qm.py:55-71)."""
         if self.is_learning_scale or not self.is_observer_qparam:
             return
+        if act is not None and not self._act_fusable(x):
+            x, act = _ACTS[act](x), None
         if self._device_observer(x):
             if isinstance(self.observer, PerChannelMinMaxObserver):
                 rs = self.observer.observe(x, want_row_stats=True)
                 self._record_stats(stats_from_row_sums(rs, x.numel()))
                 self.scale, self.zero_point = self.observer.get_scale_zero_point()
             elif self.dist_group is not None:
-                self._collect_distributed(x)
+                self._collect_distributed(x, act)
             else:
-                qp, st = self.observer.observe_device(x)
+                qp, st = self.observer.observe_device(x, act=act)
                 self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
                 self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
             return
@@ -121,11 +126,11 @@ class QuantizationManager(nn.Module):
         self.scale, self.zero_point = self.observer.forward(x)
 
     # ------------------------------------------------------------------ multi-GPU observer
-    def _collect_distributed(self, x):
+    def _collect_distributed(self, x, act=None):
         from ..distributed import allreduce_stats
         obs = self.observer
         _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
-                               run_minmax=None, want_qp=False, want_stats=True)
+                               run_minmax=None, want_qp=False, want_stats=True, act=act)
         if self.dist_defer:
             if self.is_quantize:
                 raise RuntimeError("deferred observer sync (dist_defer) needs is_quantize=False "
@@ -154,9 +159,27 @@ class QuantizationManager(nn.Module):
         self._calib_init = None
         self.scale, self.zero_point = self.observer.get_scale_zero_point()
 
-    def quantize(self, x):
-        """collect_qparameter, then fake-quantize when enabled (qm.py:73-90)."""
-        if (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
+    def _act_fusable(self, x) -> bool:
+        """Can act(x) be fused into this manager's kernels (K5)?  Needs a CUDA tensor,
+        this package's per-tensor quantizer and (when observing) per-tensor observer."""
+        from .uniform import UniformQuantizer
+        if not (isinstance(x, torch.Tensor) and x.device.type == "cuda"):
+            return False
+        if not isinstance(self.quantizer, UniformQuantizer) or isinstance(self.quantizer,
+                                                                          PerChannelUniformQuantizer):
+            return False
+        observing = not self.is_learning_scale and self.is_observer_qparam
+        return not observing or (isinstance(self.observer, MinMaxObserver)
+                                 and not isinstance(self.observer, PerChannelMinMaxObserver))
+
+    def quantize(self, x, act=None):
+        """collect_qparameter, then fake-quantize when enabled (qm.py:73-90).
+
+        ``act`` ("relu" / "silu"): the layer's activation, applied to ``x`` first; with
+        this package's kernels it is fused into the observer and the fake quant (K5)."""
+        if act is not None and not (self.is_quantize and self._act_fusable(x)):
+            x, act = _ACTS[act](x), None
+        if act is None and (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
                 and isinstance(self.observer, PerChannelMinMaxObserver)
                 and isinstance(self.quantizer, PerChannelUniformQuantizer) and self._device_observer(x)):
             # fused per-channel observe + quantize: one read, one write of x
@@ -164,9 +187,12 @@ class QuantizationManager(nn.Module):
             self._record_stats(stats_from_row_sums(rs, x.numel()))
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
             return y
-        self.collect_qparameter(x)
+        self.collect_qparameter(x, act)
         if self.is_quantize:
-            return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale)
+            if act is None:
+                return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale)
+            return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale,
+                                           act=act)
         return x
 
     # ------------------------------------------------------------------ learnable qparams

@@ -70,10 +70,13 @@ class UniformQuantizer(BaseQuantizer):
         self.calib_grad_scale = 1
 
     # ------------------------------------------------------------------ protocol
-    def quantize(self, x, scale, zero_point, is_learning_scale):
-        """Fake-quantize ``x`` (uniform.py:34-56): ``(clamp(round(x/s+zp)) - zp) * s``."""
+    def quantize(self, x, scale, zero_point, is_learning_scale, act=None):
+        """Fake-quantize ``x`` (uniform.py:34-56): ``(clamp(round(x/s+zp)) - zp) * s``.
+
+        ``act`` ("relu" / "silu", an MI355X extension of the protocol): quantize
+        act(x) in the same pass (K5); gradients are with respect to ``x``."""
         if not is_learning_scale:
-            return fake_quant_fixed(x, scale, zero_point, self.qmin, self.qmax)
+            return fake_quant_fixed(x, scale, zero_point, self.qmin, self.qmax, act=act)
         gscale = _reduce_gscale(self.calculate_grad_scale(x) * self.calib_grad_scale)
         learn_zp = not self.symmetric
         if learn_zp and not isinstance(zero_point, torch.Tensor):
@@ -82,7 +85,7 @@ class UniformQuantizer(BaseQuantizer):
         if not learn_zp and isinstance(zero_point, torch.Tensor) and zero_point.requires_grad:
             raise NotImplementedError("a gradient-requiring zero point with a symmetric learnable "
                                       "quantizer is not supported")
-        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp)
+        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp, act)
 
     def _int_zero_point_learnable(self, zero_point):
         # Reference behaviour (uniform.py:50-52 -> :100 -> :267): torch.round(<int>) raises.
