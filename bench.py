@@ -39,7 +39,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=["c2", "c3"], default="c2")
+    p.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -162,6 +163,121 @@ class C3Lsq:
         return True
 
 
+def yolov8n_backbone(img=320, width=(3, 16, 32, 64, 128, 256), depth=(1, 2, 2)):
+    """The 27 Conv(+BN+ReLU) layers of the reference's DarkNet backbone (nets/yolov8.py:75-117,
+    yolo_v8_n widths/depths :224-227) in forward order: (cin, cout, k, stride, hout)."""
+    layers, h = [], img
+
+    def conv(cin, cout, k, s):
+        nonlocal h
+        h = (h + 2 * ((k - 1) // 2) - k) // s + 1
+        layers.append((cin, cout, k, s, h))
+
+    def csp(cin, cout, n):
+        conv(cin, cout, 1, 1)
+        for _ in range(n):
+            conv(cout // 2, cout // 2, 3, 1)
+            conv(cout // 2, cout // 2, 3, 1)
+        conv((2 + n) * cout // 2, cout, 1, 1)
+
+    conv(width[0], width[1], 3, 2)
+    conv(width[1], width[2], 3, 2); csp(width[2], width[2], depth[0])
+    conv(width[2], width[3], 3, 2); csp(width[3], width[3], depth[1])
+    conv(width[3], width[4], 3, 2); csp(width[4], width[4], depth[2])
+    conv(width[4], width[5], 3, 2); csp(width[5], width[5], depth[0])
+    conv(width[5], width[5] // 2, 1, 1); conv(width[5] * 2, width[5], 1, 1)   # SPP
+    return layers
+
+
+class C4Backbone:
+    """C4: the YOLOv8n backbone's 27 ConvBnReLU quantizers at 320x320, batch 256, in the
+    learning phase: per layer the learnable weight fake quant (K1 fwd, K4 bwd) and the fused
+    ReLU + learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd).  The conv itself
+    is MIOpen and out of scope: synthetic conv outputs of the right shapes stand in for it."""
+
+    name = "C4 YOLOv8n backbone ConvBnReLU fake-quant (weights + fused ReLU/act), learnable"
+
+    def __init__(self, dev, slots, seed_base, batch=256, bits_w=2, bits_a=4):
+        from vsiquantization_amd import _hip as H
+        self.H = H
+        lib = H.lib()
+        st = H.stream_of(dev)
+        self.layers = yolov8n_backbone()
+        self.shape = (batch, 3, 320, 320)
+        qw = (-(2 ** (bits_w - 1)), 2 ** (bits_w - 1) - 1)
+        qa = (-(2 ** (bits_a - 1)), 2 ** (bits_a - 1) - 1)
+        self.bits = (bits_w, bits_a)
+        gen = torch.Generator(device=dev).manual_seed(seed_base)
+        self.fwd, self.bwd, self.keep = [], [], []
+        n_act = n_w = 0
+        for cin, cout, k, s_, h in self.layers:
+            w = torch.randn(cout, cin, k, k, device=dev, generator=gen) * (2.0 / (cin * k * k)) ** 0.5
+            c = torch.randn(batch, cout, h, h, device=dev, generator=gen)
+            g = torch.randn(batch, cout, h, h, device=dev, generator=gen)
+            gw = torch.randn_like(w)
+            t = dict(w=w, c=c, g=g, gw=gw, wq=torch.empty_like(w), y=torch.empty_like(c),
+                     gc=torch.empty_like(c), gwx=torch.empty_like(w),
+                     sw=torch.tensor(float(w.abs().mean()) * 2 / (qw[1] ** 0.5), dtype=torch.float64, device=dev),
+                     sa=torch.tensor(2 * 0.8 / (qa[1] ** 0.5), dtype=torch.float64, device=dev),
+                     grads_w=torch.empty(2, dtype=torch.float64, device=dev),
+                     grads_a=torch.empty(2, dtype=torch.float64, device=dev))
+            t["ws_w"] = torch.empty(lib.vsiq_workspace_doubles(w.numel()), dtype=torch.float64, device=dev)
+            t["ws_a"] = torch.empty(lib.vsiq_workspace_doubles(c.numel()), dtype=torch.float64, device=dev)
+            t["cnt_w"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            t["cnt_a"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            P = {kk: H.ptr(v) for kk, v in t.items()}
+            nw, na = w.numel(), c.numel()
+            gsw, gsa = (qw[1] * nw) ** -0.5, (qa[1] * na) ** -0.5
+            self.fwd.append((lib.vsiq_fq_fwd_f32, (P["w"], P["wq"], None, None, H.c_i64(nw), None, P["sw"],
+                                                   0.0, None, 0.0, 0, 0, qw[0], qw[1], st)))
+            self.fwd.append((lib.vsiq_act_fq_fwd_f32, (P["c"], P["y"], None, None, H.c_i64(na), H.ACT_RELU,
+                                                       None, P["sa"], 0.0, None, 0.0, 0, 0, qa[0], qa[1], st)))
+            self.bwd.append((lib.vsiq_act_lsq_bwd_f32, (P["g"], P["c"], P["gc"], H.c_i64(na), H.ACT_RELU,
+                                                        P["sa"], 0.0, None, 0.0, 0, qa[0], qa[1], gsa,
+                                                        P["grads_a"], P["ws_a"], H.c_i64(t["ws_a"].numel()),
+                                                        P["cnt_a"], st)))
+            self.bwd.append((lib.vsiq_lsq_bwd_f32, (P["gw"], P["w"], P["gwx"], H.c_i64(nw), P["sw"], 0.0,
+                                                    None, 0.0, 0, qw[0], qw[1], gsw, P["grads_w"], P["ws_w"],
+                                                    H.c_i64(t["ws_w"].numel()), P["cnt_w"], st)))
+            self.keep.append(t)
+            n_act += na
+            n_w += nw
+        self.n = n_act + n_w
+        self.n_act, self.n_w = n_act, n_w
+        self.slots = [None]
+        # algorithmic bytes per step: fwd 8 B/elem (weights and activations; the fused ReLU 0),
+        # bwd 12 B/elem (read g, read x or c, write grad)
+        self.kernels = {"fwd_all_layers": 8 * self.n, "bwd_all_layers": 12 * self.n}
+
+    def launch(self, i):
+        rc = 0
+        for f, a in self.fwd:
+            rc |= f(*a)
+        for f, a in self.bwd:
+            rc |= f(*a)
+        return rc
+
+    def launch_group(self, i0, cnt, ev):
+        rc = 0
+        ev[0].record()
+        for _ in range(cnt):
+            for f, a in self.fwd:
+                rc |= f(*a)
+        ev[1].record()
+        for _ in range(cnt):
+            for f, a in self.bwd:
+                rc |= f(*a)
+        ev[2].record()
+        return rc
+
+    def check(self):
+        """grad scale of the first activation quantizer is finite and the fused ReLU zeroed
+        the gradient wherever the conv output is negative."""
+        t = self.keep[0]
+        neg = t["c"] < 0
+        return bool(torch.isfinite(t["grads_a"]).all()) and bool((t["gc"][neg] == 0).all())
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(workload, seconds):
     """The reference's eager-torch op sequence (oracle/eager_torch.py) on the host cores."""
@@ -176,6 +292,21 @@ def cpu_baseline(workload, seconds):
         fn = lambda: E.per_channel_step(w, g, symmetric=False, bits=8)  # noqa: E731
         n = w.numel()
         sample = f"{rows} of 1024 out-channels of the 1024x1024x3x3 weight (9216 elem/row), fwd+bwd"
+    elif workload == "c4":
+        imgs = 4   # bounded sample: 4 of the 256 images, all 27 layers + their weights
+        tens = []
+        for cin, cout, k, _, h in yolov8n_backbone():
+            tens.append((torch.randn(cout, cin, k, k, generator=gen) * (2.0 / (cin * k * k)) ** 0.5,
+                         torch.randn(cout, cin, k, k, generator=gen),
+                         torch.randn(imgs, cout, h, h, generator=gen),
+                         torch.randn(imgs, cout, h, h, generator=gen)))
+
+        def fn():
+            for w, gw, c, g in tens:
+                E.lsq_step(w, gw, scale=0.05, bits=2)
+                E.lsq_step(c, g, scale=0.5, bits=4, act="relu")
+        n = sum(t[0].numel() + t[2].numel() for t in tens)
+        sample = f"{imgs} of 256 images through all 27 backbone layers (+ weights), fwd+bwd"
     else:
         x = torch.randn(64, 3, 224, 224, generator=gen)
         g = torch.randn(64, 3, 224, 224, generator=gen)
@@ -219,13 +350,16 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
 
-    W = (C2PerChannel if a.workload == "c2" else C3Lsq)(dev, a.slots, 1000 * rank)
+    if a.workload == "c4":
+        W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch)
+    else:
+        W = (C2PerChannel if a.workload == "c2" else C3Lsq)(dev, a.slots, 1000 * rank)
     for i in range(a.warmup):
         assert W.launch(i) == 0
     torch.cuda.synchronize()
     ok = W.check()
 
-    ns = len(W.slots)
+    ns = len(W.slots) if a.workload != "c4" else 4   # C4: events around 4 steps' phases
     groups = [(g0, min(ns, a.steps - g0)) for g0 in range(0, a.steps, ns)]
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in groups]
     if world > 1:
@@ -256,9 +390,12 @@ def main():
                       "frac": W.kernels[k] / dur[k] / 1e9 / HBM_PEAK_GBS} for k in names}
 
     total_elems = W.n * a.steps * world
+    metrics = {"c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
+               "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
+               "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
+                     "HBM GB/s vs roofline"}
     out = {
-        "metric": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline"
-        if a.workload == "c2" else "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
+        "metric": metrics[a.workload],
         "value": total_elems / dt / 1e6,
         "unit": "Melem/s",
         "n_gpus": world,
@@ -278,6 +415,12 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         "kernels": per_kernel,
     }
+    if a.workload == "c4":
+        out["config"].update(layers=len(W.layers), bits_w=W.bits[0], bits_a=W.bits[1],
+                             act_elements_per_step=W.n_act, weight_elements_per_step=W.n_w,
+                             parallelism=f"dp x{world} (batch {a.batch} per GPU; quantizer path has no "
+                                         "collective, scale grads ride DDP's all-reduce)",
+                             note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:

@@ -51,12 +51,18 @@ def per_channel_step(w, g, symmetric=False, bits=8):
     return w.grad
 
 
-def lsq_step(x, g, scale=0.03, bits=8):
-    """Learnable symmetric fake-quant fwd + bwd (uniform.py:47-56 with ScaleGradient)."""
+def lsq_step(x, g, scale=0.03, bits=8, act=None):
+    """Learnable symmetric fake-quant fwd + bwd (uniform.py:47-56 with ScaleGradient);
+    act="relu"/"silu": the fused layers' activation first (modules/fused.py:133)."""
     qmin, qmax = qrange(bits, True)
     s = torch.nn.Parameter(torch.tensor(scale, dtype=torch.float64))
     gscale = (qmax * x.numel()) ** -0.5
-    x = x.detach().requires_grad_(True)
+    x0 = x.detach().requires_grad_(True)
+    x = x0
+    if act == "relu":
+        x = torch.nn.functional.relu(x0)
+    elif act == "silu":
+        x = torch.nn.functional.silu(x0)
 
     class _ScaleGrad(torch.autograd.Function):
         @staticmethod
@@ -69,4 +75,4 @@ def lsq_step(x, g, scale=0.03, bits=8):
 
     y = fake_quant(x, _ScaleGrad.apply(s), 0, qmin, qmax)
     y.backward(g)
-    return x.grad, s.grad
+    return x0.grad, s.grad
