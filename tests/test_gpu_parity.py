@@ -293,6 +293,18 @@ def test_lsq_c3_full_size(sym):
         assert float(zp.grad) == pytest.approx(gzo, rel=1e-9)
 
 
+@pytest.mark.parametrize("n", [1, 4099, 295_000, 3_276_800, 13_107_200])
+def test_lsq_groups_per_lane_sizes(n):
+    """K4 picks 2 / 4 / 16 groups per lane by tensor size (grid >= 2048 workgroups):
+    every variant bitwise on grad_x, f64 scale gradient vs the closed form."""
+    x = _rand(n, n % 97, 0.5)
+    g = _rand(n, n % 89 + 1)
+    gx, grads = FQ.lsq_backward(cu(g), cu(x), 0.01, 0, -8, 7, 0.37, False)
+    _, gxo, gso, _ = O.lsq_forward_backward(x, g, 0.01, 0, -8, 7, 0.37)
+    G.assert_bitwise_f32(npy(gx), gxo, "grad_x")
+    assert float(grads[0]) == pytest.approx(gso, rel=1e-9, abs=1e-12)
+
+
 def test_reductions_deterministic():
     x = cu(_rand(3_000_001, 5))
     g = cu(_rand(3_000_001, 6))

@@ -75,7 +75,7 @@ __device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int6
   if (nv > 0) store_group<VEC, NT>(gx, i, n, act_bwd4<ACT>(o, xc));
 }
 
-template <bool VEC, bool NT, bool ZPL, int ACT>
+template <bool VEC, bool NT, bool ZPL, int ACT, int G>
 __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ x,
                                                     float *__restrict__ gx, int64_t n,
@@ -87,18 +87,18 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   LsqAcc c{0.0, 0.0};
   const int64_t ng = cdiv(n, 4);
   (void)prefetch;
-  // kLsqGroups groups per lane, straight-line (fully unrolled): group k+2 is loaded
-  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
-  const int64_t base = (int64_t)blockIdx.x * kBlock * kLsqGroups + threadIdx.x;
-  f4 xv[kLsqGroups], gv[kLsqGroups];
+  // G groups per lane, straight-line (fully unrolled): group k+2 is loaded while
+  // group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
+  const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
+  f4 xv[G], gv[G];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
     gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
   }
 #pragma unroll
-  for (int k = 0; k < kLsqGroups; ++k) {
-    if (k + 2 < kLsqGroups) {
+  for (int k = 0; k < G; ++k) {
+    if (k + 2 < G) {
       xv[k + 2] = load_group_c<VEC, NT>(x, base + (k + 2) * kBlock, ng, n);
       gv[k + 2] = load_group_c<VEC, NT>(g, base + (k + 2) * kBlock, ng, n);
     }
@@ -133,17 +133,30 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
 }
 
 
+template <int ACT, bool VEC, bool NT, int G>
+void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
+                  double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
+                  hipStream_t st) {
+  const int pf = 0;
+  if (zpl)
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
+                       gx, n, src, gscale, pf, grad_out, ws, counter);
+  else
+    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
+                       gx, n, src, gscale, pf, grad_out, ws, counter);
+}
+
 template <int ACT, bool VEC, bool NT>
 void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
                     double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                     hipStream_t st) {
-  const int pf = 0;
-  if (zpl)
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
-                       gx, n, src, gscale, pf, grad_out, ws, counter);
+  const int per_lane = lsq_groups_per_lane(cdiv(n, 4));
+  if (per_lane == kLsqGroups)
+    launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+  else if (per_lane == 4)
+    launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
   else
-    hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
-                       gx, n, src, gscale, pf, grad_out, ws, counter);
+    launch_lsq_g<ACT, VEC, NT, 2>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
 }
 
 template <int ACT>

@@ -36,7 +36,8 @@ constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
 constexpr int kPartials = 8;           // doubles per partial record
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
-constexpr int kLsqGroups = 16;         // groups per lane in K4 (fewer workgroups -> fewer partials)
+constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workgroups -> fewer partials)
+constexpr int kLsqMinGrid = 64;        // K4: shrink groups per lane only below this grid
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -682,8 +683,23 @@ inline int64_t oneshot_grid(int64_t groups) {
   return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kFlatU));
 }
 
-inline int64_t lsq_grid(int64_t groups) {
-  return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kLsqGroups));
+// K4 groups per lane for a tensor of `groups` 4-element groups.  16 amortizes each
+// workgroup's reduction epilogue (block reduce, partial record, arrival atomic) and
+// keeps a lane's loads streaming: on MI355X it beats 2 or 4 groups per lane even at
+// 3.3M elements with only 200 workgroups (23.6 us vs 27.7 us).  Only tensors too
+// small for 64 workgroups (weights, < ~1M elements) drop to 4 or 2 groups per lane,
+// where the serial 16-deep chain dominated (17 us -> 6 us for a 295K-element weight).
+inline int lsq_groups_per_lane(int64_t groups) {
+  for (int g : {kLsqGroups, 4})
+    if (cdiv(groups, (int64_t)kBlock * g) >= kLsqMinGrid) return g;
+  return 2;
+}
+
+inline int64_t lsq_grid(int64_t groups, int per_lane) {
+  return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * per_lane));
+}
+
+inline int64_t lsq_grid(int64_t groups) { return lsq_grid(groups, lsq_groups_per_lane(groups));
 }
 
 inline int reduce_grid(int64_t groups, int per_thread) {
