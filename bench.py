@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
     p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -278,6 +278,68 @@ class C4Backbone:
         return bool(torch.isfinite(t["grads_a"]).all()) and bool((t["gc"][neg] == 0).all())
 
 
+class C5Calibration:
+    """C5: calibration of the YOLOv8n backbone's 27 activation quantizers (MinMaxObserver,
+    a4 sym) on batches of 128 images per GPU (1024 over 8 GPUs), observer-only pass over
+    the fused ReLU (K2-relu, 4 B/elem read), deferred multi-GPU sync: every rank records
+    per-call statistics on the device and ONE sync_calibration (two RCCL all-reduces for
+    all layers and calls) at the end of the timed region replays the running min/max --
+    bit-identical to one GPU (tests/test_dist_gloo.py).  Synthetic conv outputs stand in
+    for the conv (MIOpen, out of scope); images would be uint8/255 (yolov8_qat.py:42-52)."""
+
+    name = "C5 YOLOv8n backbone calibration: fused-ReLU MinMax observers, deferred RCCL sync"
+
+    def __init__(self, dev, slots, seed_base, batch=128, bits_a=4):
+        import torch.nn as nn
+        from vsiquantization_amd.quantizers.quantization_manager import QuantizationManager
+        self.layers = yolov8n_backbone()
+        self.shape = (batch, 3, 320, 320)
+        gen = torch.Generator(device=dev).manual_seed(seed_base)
+        self.acts = [torch.randn(batch, co, h, h, device=dev, generator=gen) for _, co, _, _, h in self.layers]
+        self.model = nn.ModuleList(
+            QuantizationManager("UniformQuantizer", "MinMaxObserver", bits_a, True, is_learning_scale=False)
+            for _ in self.layers)
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        for qm in self.model:
+            qm.is_observer_qparam, qm.is_quantize = True, False
+            if world > 1:
+                qm.dist_group, qm.dist_defer = dist.group.WORLD, True
+        self.world = world
+        self.n = sum(a.numel() for a in self.acts)
+        self.slots = [None]
+        self.kernels = {"observe_all_layers": 4 * self.n, "sync": 0}
+
+    def launch(self, i):
+        for qm, c in zip(self.model, self.acts):
+            qm.collect_qparameter(c, act="relu")
+        return 0
+
+    def launch_group(self, i0, cnt, ev):
+        from vsiquantization_amd.distributed import sync_calibration
+        ev[0].record()
+        for _ in range(cnt):
+            self.launch(0)
+        ev[1].record()
+        if self.world > 1:
+            sync_calibration(self.model)
+        ev[2].record()
+        return 0
+
+    def check(self):
+        """min/max identical on every rank after the deferred sync (and finite qparams)."""
+        from vsiquantization_amd.distributed import sync_calibration
+        if self.world > 1:
+            sync_calibration(self.model)
+        mm = torch.tensor([[qm.observer.min_val, qm.observer.max_val] for qm in self.model],
+                          dtype=torch.float64, device=self.acts[0].device)
+        if self.world > 1:
+            hi, lo = mm.clone(), mm.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            return bool(torch.equal(hi, lo))
+        return bool(torch.isfinite(mm).all())
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(workload, seconds):
     """The reference's eager-torch op sequence (oracle/eager_torch.py) on the host cores."""
@@ -292,6 +354,18 @@ def cpu_baseline(workload, seconds):
         fn = lambda: E.per_channel_step(w, g, symmetric=False, bits=8)  # noqa: E731
         n = w.numel()
         sample = f"{rows} of 1024 out-channels of the 1024x1024x3x3 weight (9216 elem/row), fwd+bwd"
+    elif workload == "c5":
+        imgs = 4   # bounded sample: 4 of the 128 images per GPU, all 27 layers
+
+        acts = [torch.randn(imgs, co, h, h, generator=gen) for _, co, _, _, h in yolov8n_backbone()]
+
+        def fn():   # reference calibration per layer: relu, observer (2 .item()), 3 stats
+            for c in acts:
+                a = torch.relu(c)
+                E.observe(a)
+                a.abs().mean().item(), a.mean().item(), a.std().item()
+        n = sum(t.numel() for t in acts)
+        sample = f"{imgs} of 128 images per GPU through all 27 backbone observers (relu + MinMax + stats)"
     elif workload == "c4":
         imgs = 4   # bounded sample: 4 of the 256 images, all 27 layers + their weights
         tens = []
@@ -352,6 +426,8 @@ def main():
 
     if a.workload == "c4":
         W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch)
+    elif a.workload == "c5":
+        W = C5Calibration(dev, a.slots, 1000 * rank, batch=128)
     else:
         W = (C2PerChannel if a.workload == "c2" else C3Lsq)(dev, a.slots, 1000 * rank)
     for i in range(a.warmup):
@@ -359,7 +435,8 @@ def main():
     torch.cuda.synchronize()
     ok = W.check()
 
-    ns = len(W.slots) if a.workload != "c4" else 4   # C4: events around 4 steps' phases
+    ns = len(W.slots) if a.workload not in ("c4", "c5") else (4 if a.workload == "c4" else 16)
+    # C4: events around 4 steps' phases; C5: 16 calibration batches, then the deferred sync
     groups = [(g0, min(ns, a.steps - g0)) for g0 in range(0, a.steps, ns)]
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in groups]
     if world > 1:
@@ -386,14 +463,17 @@ def main():
     achieved = W.kernels[dom] / dur[dom] / 1e9
     traffic = load_pmc_traffic(a.workload, dom)
     per_kernel = {k: {"avg_us": dur[k] * 1e6, "alg_bytes": W.kernels[k],
-                      "GBps": W.kernels[k] / dur[k] / 1e9,
-                      "frac": W.kernels[k] / dur[k] / 1e9 / HBM_PEAK_GBS} for k in names}
+                      "GBps": W.kernels[k] / dur[k] / 1e9 if dur[k] > 0 else 0.0,
+                      "frac": W.kernels[k] / dur[k] / 1e9 / HBM_PEAK_GBS if dur[k] > 0 else 0.0}
+                  for k in names}
 
     total_elems = W.n * a.steps * world
     metrics = {"c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
                "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
                "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
-                     "HBM GB/s vs roofline"}
+                     "HBM GB/s vs roofline",
+               "c5": "Melements/s calibration observer pass (fused ReLU, 27 layers, deferred RCCL "
+                     "sync) + achieved HBM GB/s vs roofline"}
     out = {
         "metric": metrics[a.workload],
         "value": total_elems / dt / 1e6,
@@ -420,6 +500,12 @@ def main():
                              act_elements_per_step=W.n_act, weight_elements_per_step=W.n_w,
                              parallelism=f"dp x{world} (batch {a.batch} per GPU; quantizer path has no "
                                          "collective, scale grads ride DDP's all-reduce)",
+                             note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
+    if a.workload == "c5":
+        out["config"].update(layers=len(W.layers), images_per_gpu_per_batch=128,
+                             batches=a.steps, act_elements_per_batch=W.n,
+                             parallelism=f"dp x{world} (128 images per GPU per batch; deferred "
+                                         "observer sync: 2 all-reduces per calibration run)",
                              note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)

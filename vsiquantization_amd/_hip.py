@@ -80,7 +80,8 @@ class VsiqError(RuntimeError):
 
 
 def library_path() -> str:
-    return _build.OUT
+    # VSIQ_LIBRARY: experiments only (tools/exp), e.g. a variant build of the same ABI
+    return os.environ.get("VSIQ_LIBRARY") or _build.OUT
 
 
 def lib():

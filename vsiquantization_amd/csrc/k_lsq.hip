@@ -87,20 +87,20 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   LsqAcc c{0.0, 0.0};
   const int64_t ng = cdiv(n, 4);
   (void)prefetch;
-  // G groups per lane, straight-line (fully unrolled): group k+2 is loaded while
-  // group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
+  // G groups per lane, straight-line (fully unrolled): group k+kLsqPrefetch is loaded
+  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
   const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
   f4 xv[G], gv[G];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kLsqPrefetch && k < G; ++k) {
     xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
     gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
   }
 #pragma unroll
   for (int k = 0; k < G; ++k) {
-    if (k + 2 < G) {
-      xv[k + 2] = load_group_c<VEC, NT>(x, base + (k + 2) * kBlock, ng, n);
-      gv[k + 2] = load_group_c<VEC, NT>(g, base + (k + 2) * kBlock, ng, n);
+    if (k + kLsqPrefetch < G) {
+      xv[k + kLsqPrefetch] = load_group_c<VEC, NT>(x, base + (k + kLsqPrefetch) * kBlock, ng, n);
+      gv[k + kLsqPrefetch] = load_group_c<VEC, NT>(g, base + (k + kLsqPrefetch) * kBlock, ng, n);
     }
     lsq_group<VEC, NT, ZPL, ACT>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
   }

@@ -37,6 +37,10 @@ constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
 constexpr int kPartials = 8;           // doubles per partial record
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
 constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workgroups -> fewer partials)
+#ifndef VSIQ_LSQ_PREFETCH
+#define VSIQ_LSQ_PREFETCH 2
+#endif
+constexpr int kLsqPrefetch = VSIQ_LSQ_PREFETCH;   // K4 groups in flight ahead of the one computing
 constexpr int kLsqMinGrid = 64;        // K4: shrink groups per lane only below this grid
 
 typedef float f4 __attribute__((ext_vector_type(4)));
