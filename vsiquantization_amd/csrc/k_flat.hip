@@ -71,7 +71,9 @@ __device__ __forceinline__ void obs_block_reduce(ObsAcc &a) {
   __syncthreads();
 }
 
-template <bool VEC, bool NT, int ACT>
+// One-shot: G groups per lane (grid = ng / (256 G)), all G loads issued up front
+// (no loop: the loads of a wave stay in flight together and s_waitcnt is exact).
+template <bool VEC, bool NT, int ACT, int G>
 __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x, int64_t n,
                                                     double *__restrict__ stats_out,
                                                     float *__restrict__ run_minmax,
@@ -82,19 +84,14 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
   ObsAcc a;
   obs_init(a);
   const int64_t ng = cdiv(n, 4);
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  constexpr int U = 4;
-  const int64_t iters = block_iters(ng, (int64_t)blockIdx.x * kBlock, stride * U);
-  for (int64_t it = 0; it < iters; ++it) {
-    const int64_t base = t0 + it * stride * U;
-    f4 v[U];
+  const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
+  f4 v[G];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = load_group_c<VEC, NT>(x, base + u * stride, ng, n);
+  for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (base + u * stride < ng) obs_add4(a, act_fwd4<ACT>(v[u]), valid_in_group(base + u * stride, n));
+  for (int k = 0; k < G; ++k) {
+    const int64_t i = base + k * kBlock;
+    if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
   }
   obs_block_reduce(a);
   if (threadIdx.x == 0) {
@@ -107,13 +104,12 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
   // ---- epilogue in the last block: fixed-order combine of the partials ----
   obs_init(a);
   double nanc = 0.0;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const double *r = ws + (int64_t)b * kPartials;
-    a.mn = fminf(a.mn, (float)partial_load(r + 0));
-    a.mx = fmaxf(a.mx, (float)partial_load(r + 1));
-    nanc += partial_load(r + 2);
-    a.sa += partial_load(r + 3); a.s1 += partial_load(r + 4); a.s2 += partial_load(r + 5);
-  }
+  fold_partials<6>(ws, (int)gridDim.x, [&](const double (&r)[6]) {
+    a.mn = fminf(a.mn, (float)r[0]);
+    a.mx = fmaxf(a.mx, (float)r[1]);
+    nanc += r[2];
+    a.sa += r[3]; a.s1 += r[4]; a.s2 += r[5];
+  });
   {
     __shared__ double s_nanc[kWaves];
     nanc = wave_reduce(nanc, AddD());
@@ -227,20 +223,34 @@ __global__ __launch_bounds__(kBlock) void k_selftest_fq(int mode, const float *_
   }
 }
 
+template <int ACT, bool VEC, bool NT, int G>
+void launch_observe_g(const float *x, int64_t n, double *stats_out, float *run_minmax, double *qp_out,
+                      int sym, double qden, double eps, double *ws, uint32_t *counter, int64_t grid,
+                      hipStream_t st) {
+  hipLaunchKernelGGL((k_observe<VEC, NT, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n,
+                     stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+}
+
 template <int ACT>
 void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_out, float *run_minmax,
                     double *qp_out, int sym, double qden, double eps, double *ws, uint32_t *counter,
-                    int grid, hipStream_t st) {
-  const dim3 g(grid), b(kBlock);
-  if (vec && nt)
-    hipLaunchKernelGGL((k_observe<true, true, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out, sym,
-                       qden, eps, ws, counter);
-  else if (vec)
-    hipLaunchKernelGGL((k_observe<true, false, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out, sym,
-                       qden, eps, ws, counter);
-  else
-    hipLaunchKernelGGL((k_observe<false, false, ACT>), g, b, 0, st, x, n, stats_out, run_minmax, qp_out,
-                       sym, qden, eps, ws, counter);
+                    hipStream_t st) {
+  // same groups-per-lane rule and grid as K4 (lsq_grid), so vsiq_workspace_doubles covers both
+  const int64_t ng = cdiv(n, 4);
+  const int per_lane = lsq_groups_per_lane(ng);
+  const int64_t grid = lsq_grid(ng, per_lane);
+#define VSIQ_OBS(V, N)                                                                              \
+  (per_lane == kLsqGroups                                                                           \
+       ? launch_observe_g<ACT, V, N, kLsqGroups>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, \
+                                                 ws, counter, grid, st)                             \
+   : per_lane == 4 ? launch_observe_g<ACT, V, N, 4>(x, n, stats_out, run_minmax, qp_out, sym, qden,  \
+                                                    eps, ws, counter, grid, st)                     \
+                   : launch_observe_g<ACT, V, N, 2>(x, n, stats_out, run_minmax, qp_out, sym, qden,  \
+                                                    eps, ws, counter, grid, st))
+  if (vec && nt) VSIQ_OBS(true, true);
+  else if (vec) VSIQ_OBS(true, false);
+  else VSIQ_OBS(false, false);
+#undef VSIQ_OBS
 }
 
 int observe(const float *x, int64_t n, int act, double *stats_out, float *run_minmax, double *qp_out,
@@ -248,10 +258,11 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
             void *stream) {
   if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
   const bool vec = aligned16(x) && n % 4 == 0;
-  const int grid = reduce_grid(cdiv(n, 4), 4);
-  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  const int64_t grid = lsq_grid(cdiv(n, 4));
+  if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (ws_len < grid * kPartials) return VSIQ_E_WS;
   VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
-           symmetric, qden, eps, ws, counter, grid, (hipStream_t)stream);
+           symmetric, qden, eps, ws, counter, (hipStream_t)stream);
   return launch_rc();
 }
 

@@ -112,11 +112,10 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   }
   if (!arrive_last(counter)) return;
   c = LsqAcc{0.0, 0.0};
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-    const double *r = ws + (int64_t)b * kPartials;
-    c.t += partial_load(r + 0);
-    c.z += partial_load(r + 1);
-  }
+  fold_partials<2>(ws, (int)gridDim.x, [&](const double (&r)[2]) {
+    c.t += r[0];
+    c.z += r[1];
+  });
   lsq_block_reduce(c);
   if (threadIdx.x == 0) {
     grad_out[0] = c.t * gscale;

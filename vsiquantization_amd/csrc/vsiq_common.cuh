@@ -33,7 +33,7 @@ namespace vsiq {
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kWaves = kBlock / kWave;
-constexpr int kMaxReduceGrid = 2048;   // partial slots per reducing launch
+constexpr int kMaxReduceGrid = 2048;   // minimum partial-record slots of a workspace
 constexpr int kPartials = 8;           // doubles per partial record
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
 constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workgroups -> fewer partials)
@@ -630,6 +630,26 @@ __device__ __forceinline__ bool arrive_last(uint32_t *counter) {
   return s_last != 0;
 }
 
+// Last-workgroup combine of the per-workgroup partial records: thread t folds
+// records t, t+B, t+2B, ... in that fixed order (deterministic), but the loads of 4
+// consecutive records are issued together -- a serial load->add chain over thousands
+// of records was a multi-microsecond tail on large grids.
+template <int K, typename F>
+__device__ __forceinline__ void fold_partials(const double *ws, int nrec, F &&f) {
+  for (int b0 = threadIdx.x; b0 < nrec; b0 += 4 * kBlock) {
+    double r[4][K];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = b0 + u * kBlock < nrec ? b0 + u * kBlock : nrec - 1;
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[u][k] = partial_load(ws + (int64_t)b * kPartials + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (b0 + u * kBlock < nrec) f(r[u]);
+  }
+}
+
 // f64 qparams from the running min/max (observers/minmax.py:49-74).
 // min_val <= 0 <= max_val always holds (state starts at 0/0, minmax.py:28-29).
 __device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, double qden,
@@ -706,10 +726,6 @@ inline int64_t lsq_grid(int64_t groups, int per_lane) {
 inline int64_t lsq_grid(int64_t groups) { return lsq_grid(groups, lsq_groups_per_lane(groups));
 }
 
-inline int reduce_grid(int64_t groups, int per_thread) {
-  int64_t b = cdiv(groups, (int64_t)kBlock * per_thread);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxReduceGrid));
-}
 
 inline int launch_rc() {
   const hipError_t e = hipGetLastError();
