@@ -280,64 +280,83 @@ class C4Backbone:
 
 class C5Calibration:
     """C5: calibration of the YOLOv8n backbone's 27 activation quantizers (MinMaxObserver,
-    a4 sym) on batches of 128 images per GPU (1024 over 8 GPUs), observer-only pass over
-    the fused ReLU (K2-relu, 4 B/elem read), deferred multi-GPU sync: every rank records
-    per-call statistics on the device and ONE sync_calibration (two RCCL all-reduces for
-    all layers and calls) at the end of the timed region replays the running min/max --
-    bit-identical to one GPU (tests/test_dist_gloo.py).  Synthetic conv outputs stand in
-    for the conv (MIOpen, out of scope); images would be uint8/255 (yolov8_qat.py:42-52)."""
+    sym) on batches of 128 images per GPU (1024 over 8 GPUs): per batch and layer one
+    observer pass over the fused ReLU of the conv output (K2-relu, 4 B/elem read), each
+    writing its per-call statistics record on the device (deferred mode, no sync); after
+    the last batch ONE deferred sync -- two RCCL all-reduces over all records of all
+    layers -- and the exact replay of every layer's running min/max (the path of
+    QuantizationManager.dist_defer + distributed.sync_calibration, here driven through the
+    C ABI so the Python manager's per-call host cost is not what is measured).  min/max are
+    bit-identical to a 1-GPU run (tests/test_dist_gloo.py).  Synthetic conv outputs stand
+    in for the conv (MIOpen, out of scope)."""
 
     name = "C5 YOLOv8n backbone calibration: fused-ReLU MinMax observers, deferred RCCL sync"
 
-    def __init__(self, dev, slots, seed_base, batch=128, bits_a=4):
-        import torch.nn as nn
-        from vsiquantization_amd.quantizers.quantization_manager import QuantizationManager
+    def __init__(self, dev, slots, seed_base, batch=128, steps=16):
+        from vsiquantization_amd import _hip as H
+        from vsiquantization_amd.fakequant import qden
+        self.H = H
+        lib = H.lib()
+        self.st = H.stream_of(dev)
         self.layers = yolov8n_backbone()
         self.shape = (batch, 3, 320, 320)
         gen = torch.Generator(device=dev).manual_seed(seed_base)
         self.acts = [torch.randn(batch, co, h, h, device=dev, generator=gen) for _, co, _, _, h in self.layers]
-        self.model = nn.ModuleList(
-            QuantizationManager("UniformQuantizer", "MinMaxObserver", bits_a, True, is_learning_scale=False)
-            for _ in self.layers)
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        for qm in self.model:
-            qm.is_observer_qparam, qm.is_quantize = True, False
-            if world > 1:
-                qm.dist_group, qm.dist_defer = dist.group.WORLD, True
-        self.world = world
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.steps = steps
+        L = len(self.layers)
+        self.rec = torch.zeros(steps, L, H.ST_LEN, dtype=torch.float64, device=dev)
+        self.ws = H.workspace(dev, max(a.numel() for a in self.acts))
+        self.qd = qden(True, 8, 1e-8)
+        self.f = lib.vsiq_act_observe_f32
+        self.ptrs = [H.ptr(a) for a in self.acts]
         self.n = sum(a.numel() for a in self.acts)
         self.slots = [None]
         self.kernels = {"observe_all_layers": 4 * self.n, "sync": 0}
+        self.minmax = None
+
+    def _observe(self, step):
+        H = self.H
+        rc = 0
+        base = self.rec[step % self.steps]
+        for j, (p, a) in enumerate(zip(self.ptrs, self.acts)):
+            rc |= self.f(p, H.c_i64(a.numel()), H.ACT_RELU, H.ptr(base[j]), None, None, 1, self.qd, 1e-8,
+                         H.ptr(self.ws.ws), H.c_i64(self.ws.ws_len), H.ptr(self.ws.counter), self.st)
+        return rc
 
     def launch(self, i):
-        for qm, c in zip(self.model, self.acts):
-            qm.collect_qparameter(c, act="relu")
-        return 0
+        return self._observe(i)
+
+    def _sync(self, k):
+        """The deferred sync over the first k batches: all-reduce + running-state replay."""
+        from vsiquantization_amd.distributed import allreduce_stats, replay_minmax_tensor
+        recs = self.rec[:k].transpose(0, 1).contiguous()          # [layers, calls, ST_LEN]
+        if self.world > 1:
+            allreduce_stats(recs)
+        self.minmax = replay_minmax_tensor(0.0, 0.0, recs)         # stays on the device
 
     def launch_group(self, i0, cnt, ev):
-        from vsiquantization_amd.distributed import sync_calibration
+        rc = 0
         ev[0].record()
-        for _ in range(cnt):
-            self.launch(0)
+        for j in range(cnt):
+            rc |= self._observe(i0 + j)
         ev[1].record()
-        if self.world > 1:
-            sync_calibration(self.model)
+        self._sync(min(self.steps, i0 + cnt))
         ev[2].record()
-        return 0
+        return rc
 
     def check(self):
-        """min/max identical on every rank after the deferred sync (and finite qparams)."""
-        from vsiquantization_amd.distributed import sync_calibration
-        if self.world > 1:
-            sync_calibration(self.model)
-        mm = torch.tensor([[qm.observer.min_val, qm.observer.max_val] for qm in self.model],
-                          dtype=torch.float64, device=self.acts[0].device)
+        """Running min/max after the sync identical on every rank; equal to a direct
+        reduction of the (synthetic) relu(conv output) on one GPU."""
+        self._sync(1)
+        mm = torch.stack(self.minmax, dim=-1)
         if self.world > 1:
             hi, lo = mm.clone(), mm.clone()
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
             return bool(torch.equal(hi, lo))
-        return bool(torch.isfinite(mm).all())
+        ref = [(min(0.0, float(torch.relu(a).min())), max(0.0, float(torch.relu(a).max()))) for a in self.acts]
+        return [tuple(r) for r in mm.tolist()] == ref
 
 
 # --------------------------------------------------------------------------- CPU baseline
@@ -427,7 +446,7 @@ def main():
     if a.workload == "c4":
         W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch)
     elif a.workload == "c5":
-        W = C5Calibration(dev, a.slots, 1000 * rank, batch=128)
+        W = C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=max(a.steps, a.warmup))
     else:
         W = (C2PerChannel if a.workload == "c2" else C3Lsq)(dev, a.slots, 1000 * rank)
     for i in range(a.warmup):

@@ -71,3 +71,26 @@ def test_sharded_observer_matches_single_rank(world):
     assert O.minmax_qparams(rmn, rmx, False) == O.minmax_qparams(mn, mx, False)
     # the NaN call contributes nothing, its fp32 means are NaN like torch's
     assert np.isnan(ret[0][2, H.ST_MEANABS])
+
+
+def test_replay_minmax_tensor_equals_sequential_fold():
+    """The vectorized replay (bench C5 / large calibrations) equals the reference fold."""
+    import numpy as np
+    import torch
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd.distributed import replay_minmax, replay_minmax_tensor
+    rng = np.random.default_rng(0)
+    recs = torch.zeros(5, 7, H.ST_LEN, dtype=torch.float64)
+    recs[..., H.ST_MIN] = torch.from_numpy(rng.normal(size=(5, 7)))
+    recs[..., H.ST_MAX] = torch.from_numpy(rng.normal(size=(5, 7)) + 1)
+    recs[1, 3, H.ST_NAN] = 2                       # a NaN call is skipped
+    recs[2, :, H.ST_MIN] = 0.5                     # never below the initial 0
+    recs[3, :, H.ST_MIN] = -0.0                    # -0.0 does not replace 0 (strict <)
+    init = [(0, 0), (-3.0, 0.5), (0, 0), (0, 0), (1.0, 1.0)]
+    mn, mx = replay_minmax_tensor([a for a, _ in init], [b for _, b in init], recs)
+    for i, (a, b) in enumerate(init):
+        calls = recs[i][:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist()
+        want = replay_minmax(a, b, calls)
+        got = (float(mn[i]), float(mx[i]))
+        assert got == tuple(float(w) for w in want)
+        assert np.signbit(got[0]) == np.signbit(float(want[0]))

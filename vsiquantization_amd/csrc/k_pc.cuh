@@ -31,10 +31,10 @@ __device__ __forceinline__ void rowsums_add4(RowSums &r, f4 v, int nv) {
   const float pa = (__builtin_fabsf(v.x) + __builtin_fabsf(vy)) +
                    (__builtin_fabsf(vz) + __builtin_fabsf(vw));
   const float p1 = (v.x + vy) + (vz + vw);
-  const double dx = v.x, dy = vy, dz = vz, dw = vw;
+  const float p2 = (v.x * v.x + vy * vy) + (vz * vz + vw * vw);   // fp32 over 4, f64 across groups
   r.sa += (double)pa;
   r.s1 += (double)p1;
-  r.s2 += __builtin_fma(dx, dx, __builtin_fma(dy, dy, __builtin_fma(dz, dz, dw * dw)));
+  r.s2 += (double)p2;
 }
 
 // Row reduction -> running state -> f64 qparams, returned to every lane.

@@ -574,26 +574,71 @@ __device__ __forceinline__ void fq_store_out(float *yr, uint8_t *cr, int64_t i, 
 // ----------------------------------------------------------------------------
 // wave / block reductions (wave64)
 // ----------------------------------------------------------------------------
+// Wave64 all-reduce on DPP (no LDS traffic): quad swaps, row rotations by 4 and 8
+// (every lane then holds its 16-lane row's result), row_bcast:15 / row_bcast:31 to
+// fold the four rows into lane 63, read back into an SGPR.  Fixed order, hence
+// deterministic.  Requires the whole wave active (all call sites are uniform).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+
+template <int CTRL, int ROW_MASK = 0xF, typename T>
+__device__ __forceinline__ T dpp(T v, T old) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit lanes");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, dpp32<CTRL, ROW_MASK>(__builtin_bit_cast(uint32_t, v),
+                                                      __builtin_bit_cast(uint32_t, old)));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v), o = __builtin_bit_cast(uint64_t, old);
+    const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)u, (uint32_t)o);
+    const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(u >> 32), (uint32_t)(o >> 32));
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T readlane63(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
+    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+  }
+}
+
 template <typename T, typename Op>
 __device__ __forceinline__ T wave_reduce(T v, Op op) {
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) v = op(v, __shfl_xor(v, off, kWave));
-  return v;
+  const T id = Op::identity();
+  v = op(v, dpp<0xB1>(v, id));         // quad_perm [1,0,3,2]
+  v = op(v, dpp<0x4E>(v, id));         // quad_perm [2,3,0,1]
+  v = op(v, dpp<0x124>(v, id));        // row_ror:4
+  v = op(v, dpp<0x128>(v, id));        // row_ror:8  -> every lane: its row's result
+  v = op(v, dpp<0x142, 0xA>(v, id));   // row_bcast:15 into rows 1, 3
+  v = op(v, dpp<0x143, 0xC>(v, id));   // row_bcast:31 into rows 2, 3 -> lane 63: the wave's
+  return readlane63(v);
 }
 
 struct MinOp {
+  static __device__ float identity() { return __builtin_inff(); }
   __device__ float operator()(float a, float b) const { return fminf(a, b); }
 };
 struct MaxOp {
+  static __device__ float identity() { return -__builtin_inff(); }
   __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
 };
 struct AddD {
+  static __device__ double identity() { return 0.0; }
   __device__ double operator()(double a, double b) const { return a + b; }
 };
 struct OrU {
+  static __device__ uint32_t identity() { return 0u; }
   __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; }
 };
 struct AddU {
+  static __device__ uint32_t identity() { return 0u; }
   __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
 };
 

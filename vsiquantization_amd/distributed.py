@@ -69,6 +69,23 @@ def replay_minmax(min_val, max_val, records):
     return min_val, max_val
 
 
+def replay_minmax_tensor(init_min, init_max, recs: torch.Tensor):
+    """Vectorized replay_minmax over a batch of layers: recs [layers, calls, ST_LEN] (any
+    device), init_min/init_max [layers] -> (min [layers], max [layers]) f64 tensors.
+
+    Equal to the sequential fold: under strict comparisons the running minimum ends as
+    the smallest call minimum when that is strictly below the initial value (equal
+    values are the same bits except +-0, which a strict compare never swaps), else the
+    initial value; NaN calls are skipped."""
+    nan_call = recs[..., H.ST_NAN] > 0
+    inf = torch.tensor(float("inf"), dtype=recs.dtype, device=recs.device)
+    mins = torch.where(nan_call, inf, recs[..., H.ST_MIN]).amin(dim=-1)
+    maxs = torch.where(nan_call, -inf, recs[..., H.ST_MAX]).amax(dim=-1)
+    init_min = torch.as_tensor(init_min, dtype=recs.dtype, device=recs.device)
+    init_max = torch.as_tensor(init_max, dtype=recs.dtype, device=recs.device)
+    return torch.where(mins < init_min, mins, init_min), torch.where(maxs > init_max, maxs, init_max)
+
+
 def _deferred_managers(model):
     from .quantizers.quantization_manager import QuantizationManager
     for m in model.modules():
@@ -81,6 +98,8 @@ def sync_calibration(model, group=None):
     mgrs = list(_deferred_managers(model))
     if not mgrs:
         return 0
+    for m in mgrs:
+        m._join()   # records may still be in flight on an observer side stream
     recs = [torch.stack(m._pending_records) for m in mgrs]
     counts = [r.shape[0] for r in recs]
     host = allreduce_stats(torch.cat(recs), group=group).cpu()

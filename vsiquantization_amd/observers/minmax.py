@@ -40,9 +40,18 @@ class MinMaxObserver(BaseObserver):
         self._state = None          # device fp32[2]: running (min_val, max_val)
         self._host = [0, 0]         # host mirror, valid when not self._dirty
         self._dirty = False
+        self._obs_stream = None     # side stream with pending updates (async calibration)
 
     # ------------------------------------------------------------------ state
+    def _join(self):
+        """Make the current stream wait for updates queued on a side stream."""
+        if self._obs_stream is not None:
+            if self._state is not None:
+                torch.cuda.current_stream(self._state.device).wait_stream(self._obs_stream)
+            self._obs_stream = None
+
     def _sync(self):
+        self._join()
         if self._dirty:
             mn, mx = self._state.tolist()
             self._host = [_host_number(mn), _host_number(mx)]
@@ -67,7 +76,7 @@ class MinMaxObserver(BaseObserver):
         self._set(1, v)
 
     def _set(self, i, v):
-        self._sync()
+        self._sync()   # joins a pending side stream first
         self._host[i] = v
         if self._state is not None:
             self._state[i] = 0.0 if v is None else float(v)
@@ -90,7 +99,10 @@ class MinMaxObserver(BaseObserver):
     def observe_device(self, x, want_stats=True, want_qp=True, act=None):
         """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device.
         ``act``: observe act(x) (fused ReLU/SiLU, K5) without materializing it."""
-        state = self.device_state(H.require_device_f32(x).device)
+        dev = H.require_device_f32(x).device
+        if self._obs_stream is not None and self._obs_stream != torch.cuda.current_stream(dev):
+            self._join()
+        state = self.device_state(dev)
         qp, st = observe_tensor(x, symmetric=self.symmetric, num_bits=self.num_bits, eps=self.eps,
                                 run_minmax=state, want_qp=want_qp, want_stats=want_stats, act=act)
         self._dirty = True

@@ -19,6 +19,8 @@ MI355X differences (behaviour-preserving):
 """
 from __future__ import annotations
 
+import itertools
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -33,6 +35,22 @@ from .per_channel import PerChannelUniformQuantizer
 
 _STAT_NAMES = ("mean_abs_x", "mean_x", "std")
 _ACTS = {"relu": F.relu, "silu": F.silu}
+
+# Calibration-time observer streams: an observe-only call (is_quantize False) has no
+# consumer until calibration ends, so its K2 pass is queued on a side stream and the
+# model's next layers do not wait for it (its reduction tail overlaps their work).
+# Managers are spread round-robin over a small per-device pool; each manager always
+# uses the same stream, so its own running state stays stream-ordered.
+_OBS_POOL = 4
+_OBS_STREAMS = {}
+_MGR_IDS = itertools.count()
+
+
+def _observer_stream(device, idx):
+    pool = _OBS_STREAMS.get(device)
+    if pool is None:
+        pool = _OBS_STREAMS[device] = [torch.cuda.Stream(device=device) for _ in range(_OBS_POOL)]
+    return pool[idx % len(pool)]
 
 
 class _StatList:
@@ -76,12 +94,31 @@ class QuantizationManager(nn.Module):
         self.dist_defer = False
         self._pending_records = []   # deferred: local per-call stats records f64[ST_LEN]
         self._calib_init = None
+        # observe-only calls queued on a side stream (see _observer_stream).  Off by
+        # default (then scale / zero_point are plain stream-ordered device tensors);
+        # calibrate_qat_model turns it on for the calibration run and joins at the end.
+        self.async_observer = False
+        self._obs_id = next(_MGR_IDS)
+        self._side = None            # side stream with this manager's pending records
         self.mean_abs_x = []
         self.mean_x = []
         self.std = []
 
+    # ------------------------------------------------------------------ side stream
+    def _join(self):
+        """Make the current stream wait for this manager's observer work on its side stream
+        (before any consumer of the scale / zero point / stats records / observer state)."""
+        side = self.__dict__.get("_side")
+        if side is not None:
+            self.__dict__["_side"] = None
+            torch.cuda.current_stream(side.device).wait_stream(side)
+            obs = self.__dict__.get("observer")
+            if isinstance(obs, MinMaxObserver):
+                obs._join()
+
     # ------------------------------------------------------------------ stats records
     def _materialize_stats(self):
+        self._join()
         pend = self.__dict__.get("_dev_stats")
         if pend:
             rows = torch.stack(pend).cpu().tolist()
@@ -105,18 +142,34 @@ class QuantizationManager(nn.Module):
             return
         if act is not None and not self._act_fusable(x):
             x, act = _ACTS[act](x), None
-        if self._device_observer(x):
-            if isinstance(self.observer, PerChannelMinMaxObserver):
-                rs = self.observer.observe(x, want_row_stats=True)
-                self._record_stats(stats_from_row_sums(rs, x.numel()))
-                self.scale, self.zero_point = self.observer.get_scale_zero_point()
-            elif self.dist_group is not None:
-                self._collect_distributed(x, act)
-            else:
-                qp, st = self.observer.observe_device(x, act=act)
-                self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
-                self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+        if (self.async_observer and not self.is_quantize and self._device_observer(x)
+                and not isinstance(self.observer, PerChannelMinMaxObserver)):
+            # observe-only: queue on this manager's side stream, do not wait for it
+            main = torch.cuda.current_stream(x.device)
+            side = _observer_stream(x.device, self._obs_id)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._observe_device(x, act)
+            x.record_stream(side)
+            self._side = side
+            self.observer._obs_stream = side
             return
+        self._join()
+        self._observe_device(x, act) if self._device_observer(x) else self._observe_host(x)
+
+    def _observe_device(self, x, act):
+        if isinstance(self.observer, PerChannelMinMaxObserver):
+            rs = self.observer.observe(x, want_row_stats=True)
+            self._record_stats(stats_from_row_sums(rs, x.numel()))
+            self.scale, self.zero_point = self.observer.get_scale_zero_point()
+        elif self.dist_group is not None:
+            self._collect_distributed(x, act)
+        else:
+            qp, st = self.observer.observe_device(x, act=act)
+            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+            self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+
+    def _observe_host(self, x):
         # third-party observer: the reference's host path
         xd = x.detach()
         self._materialize_stats()
@@ -177,6 +230,8 @@ class QuantizationManager(nn.Module):
 
         ``act`` ("relu" / "silu"): the layer's activation, applied to ``x`` first; with
         this package's kernels it is fused into the observer and the fake quant (K5)."""
+        if self.is_quantize or self.is_learning_scale:
+            self._join()
         if act is not None and not (self.is_quantize and self._act_fusable(x)):
             x, act = _ACTS[act](x), None
         if act is None and (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
@@ -198,6 +253,7 @@ class QuantizationManager(nn.Module):
     # ------------------------------------------------------------------ learnable qparams
     def make_learn_qparameter(self):
         """scale -> nn.Parameter (qm.py:92-103); float64 when it came from the learn init."""
+        self._join()
         s = self.scale
         s = s.detach().clone() if isinstance(s, torch.Tensor) else torch.tensor(s)
         self.scale = nn.Parameter(s, requires_grad=True)
