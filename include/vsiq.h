@@ -232,6 +232,31 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
                          double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
                          void *stream);
 
+/*
+ * Per-channel fake quant on a [rows, rowlen] view where row r uses the qparams of
+ * channel r % channels (axis 0 of [C, ...]: rows = channels = C; axis 1 of
+ * [N, C, ...]: rows = N*C, channels = C).  scale/zp f64 [channels] (zp nullable: 0).
+ */
+int vsiq_pcm_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
+                        int64_t rowlen, int64_t channels, const double *scale, const double *zp,
+                        int zp_round, int qmin, int qmax, void *stream);
+
+/*
+ * Per-channel learnable (LSQ) backward (K6): LSQFakeQuantize's per-channel path
+ * (quantizers/lsq_module.py:134-166: ScaleGradient on scale_param and the rounded
+ * zero_point_param_float, per-channel fake quant) and a learnable
+ * PerChannelUniformQuantizer.  Same element math as vsiq_lsq_bwd_f32, gradients
+ * summed per channel (f64 sums of the fp32 terms, fixed order):
+ *   grad_scale_out[c] = gscale * sum_{rows of c} [ g*(q-zp) - (mask?g*s:0)*((x/s)/s) ]
+ *   grad_zp_out[c]    = gscale * sum [ (mask?g*s:0) - g*s ] * (rint(zp[c]) in [qmin, qmax])
+ * grad_zp_out nullable.  ws: vsiq_pcm_workspace_doubles(rows, rowlen) doubles.
+ */
+int64_t vsiq_pcm_workspace_doubles(int64_t rows, int64_t rowlen);
+int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                         int64_t channels, const double *scale, const double *zp, int zp_learn,
+                         int qmin, int qmax, double gscale, double *grad_scale_out,
+                         double *grad_zp_out, double *ws, int64_t ws_len, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -154,6 +154,40 @@ def lsq_forward_backward(x, g, scale, zero_point, qmin, qmax, gscale, learn_zp=F
     return y, gx, grad_s, grad_zp
 
 
+# --------------------------------------------------------------------------- per-channel LSQ (K6)
+def pc_lsq_forward_backward(x, g, scales, zps, qmin, qmax, gscale, axis=1, learn_zp=True):
+    """LSQFakeQuantize's learnable per-channel path (quantizers/lsq_module.py:134-166,
+    314-343): every channel slice along ``axis`` is lsq_forward_backward with its own
+    fp32 scale / rounded zero point; gradients per channel (f64 sums of fp32 terms).
+    Returns y, grad_x, grad_scale [C], grad_zp [C]."""
+    x = np.asarray(x, dtype=F32)
+    g = np.asarray(g, dtype=F32)
+    C = x.shape[axis]
+    y = np.empty_like(x)
+    gx = np.empty_like(x)
+    gs = np.zeros(C)
+    gz = np.zeros(C)
+    for c in range(C):
+        idx = [slice(None)] * x.ndim
+        idx[axis] = c
+        idx = tuple(idx)
+        yc, gxc, gsc, gzc = lsq_forward_backward(x[idx], g[idx], float(scales[c]), float(zps[c]),
+                                                 qmin, qmax, gscale, learn_zp=learn_zp)
+        y[idx], gx[idx], gs[c] = yc, gxc, gsc
+        gz[c] = gzc if gzc is not None else 0.0
+    return y, gx, gs, gz
+
+
+def lsq_module_grad_scale(x_shape, qmax, per_channel, config_act):
+    """LSQFakeQuantize.calculate_grad_scale (lsq_module.py:314-333) x 5000 for activations
+    (line 152): (quant_max * numel[/shape[1] if per-channel]) ** -0.5."""
+    n = int(np.prod(x_shape))
+    if per_channel:
+        n /= x_shape[1]
+    gs = (qmax * n) ** -0.5
+    return gs * 5000 if config_act else gs
+
+
 # --------------------------------------------------------------------------- fused activation (K5)
 def act_forward(c, act):
     """The fused layers' activation before quantize_out (modules/fused.py:133):

@@ -336,6 +336,48 @@ for act in ("relu", "silu"):
         cases.append(rec)
         act_idx += 1
 
+# ---------------------------------------------------------------------------
+# 7. LSQFakeQuantize (quantizers/lsq_module.py:73-166): the torch.ao-based LSQ module
+#    with learnable fp32 scale_param / zero_point_param_float.  Calibrate with the
+#    observer (3 batches), disable it, then one learnable fwd + bwd.  Per-channel
+#    along axis 1 (the demo qconfig, lsq_module.py:509-517) and per-tensor; config_act
+#    multiplies the gradient scale by 5000 (line 152).
+# ---------------------------------------------------------------------------
+from quantizers.lsq_module import LSQFakeQuantize  # noqa: E402
+
+lsqm_idx = 0
+for per_channel, config_act in ((True, False), (True, True), (False, False), (False, True)):
+    torch.manual_seed(700 + lsqm_idx)
+    if per_channel:
+        fq = LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                             observer=torch.quantization.MovingAveragePerChannelMinMaxObserver,
+                             quant_min=0, quant_max=255, dtype=torch.quint8,
+                             qscheme=torch.per_channel_affine, reduce_range=False,
+                             averaging_constant=0.01, ch_axis=1)
+    else:
+        fq = LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                             observer=torch.quantization.MovingAverageMinMaxObserver,
+                             quant_min=0, quant_max=255, dtype=torch.quint8,
+                             qscheme=torch.per_tensor_affine, reduce_range=False)
+    shape = (4, 6, 9, 9)
+    for _ in range(3):
+        fq(torch.randn(shape) * 1.5 + 0.3)
+    fq.disable_observer()
+    x = torch.randn(shape) * 1.5 + 0.3
+    gg = torch.randn(shape)
+    xr = x.clone().requires_grad_(True)
+    y = fq(xr)
+    y.backward(gg)
+    key = f"lsqm{lsqm_idx}"
+    lsqm_idx += 1
+    cases.append(dict(kind="lsq_fake_quantize", key=key, per_channel=per_channel, config_act=config_act,
+                      qmin=0, qmax=255, x=put(key + "_x", x), g=put(key + "_g", gg), y=put(key + "_y", y),
+                      grad_x=put(key + "_gx", xr.grad),
+                      scale=put(key + "_scale", fq.scale_param.detach()),
+                      zp=put(key + "_zp", fq.zero_point_param_float.detach()),
+                      scale_grad=put(key + "_sgrad", fq.scale_param.grad),
+                      zp_grad=put(key + "_zgrad", fq.zero_point_param_float.grad)))
+
 np.savez_compressed(os.path.join(OUT, "fakequant_goldens.npz"), **arrays)
 with open(os.path.join(OUT, "cases.json"), "w") as f:
     json.dump({"generator": "tests/golden/gen_goldens.py", "torch": torch.__version__,

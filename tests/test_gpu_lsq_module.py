@@ -1,0 +1,103 @@
+"""K6 + LSQFakeQuantize / learnable per-channel on MI355X vs the reference goldens and
+the oracle.  Bars: y and grad_x bit-exact; parameter gradients <= 1e-4 relative to
+the reference's fp32 autograd sums, <= 1e-9 to the oracle's f64 closed form."""
+import numpy as np
+import pytest
+import torch
+
+import vsiquantization_amd as V
+from vsiquantization_amd import fakequant as FQ
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def cu(a, grad=False):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t.requires_grad_(grad) if grad else t
+
+
+def npy(t):
+    return t.detach().cpu().numpy()
+
+
+def _module(per_channel, config_act):
+    if per_channel:
+        return V.LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                                 observer=torch.quantization.MovingAveragePerChannelMinMaxObserver,
+                                 quant_min=0, quant_max=255, dtype=torch.quint8,
+                                 qscheme=torch.per_channel_affine, reduce_range=False,
+                                 averaging_constant=0.01, ch_axis=1).to(DEV)
+    return V.LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                             observer=torch.quantization.MovingAverageMinMaxObserver, quant_min=0,
+                             quant_max=255, dtype=torch.quint8, qscheme=torch.per_tensor_affine,
+                             reduce_range=False).to(DEV)
+
+
+@pytest.mark.parametrize("case", G.cases("lsq_fake_quantize"), ids=lambda c: c["key"])
+def test_golden_lsq_fake_quantize(case):
+    fq = _module(case["per_channel"], case["config_act"])
+    x = cu(G.arr(case["x"]))
+    fq(x)                                           # registers scale_param / zero_point_param_float
+    fq.scale_param.data.copy_(cu(G.arr(case["scale"])))
+    fq.zero_point_param_float.data.copy_(cu(G.arr(case["zp"])))
+    fq.disable_observer()
+    xg = cu(G.arr(case["x"]), grad=True)
+    y = fq(xg)
+    y.backward(cu(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    np.testing.assert_allclose(npy(fq.scale_param.grad), G.arr(case["scale_grad"]), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(npy(fq.zero_point_param_float.grad), G.arr(case["zp_grad"]), rtol=1e-4,
+                               atol=1e-6)
+
+
+@pytest.mark.parametrize("shape,axis", [((512, 3, 56, 56), 1), ((8, 64, 80, 80), 1), ((256, 27), 0),
+                                        ((1024, 1024, 3, 3), 0), ((2, 5, 7), 1), ((3, 5), 1)])
+def test_pc_lsq_vs_oracle(shape, axis):
+    rng = np.random.default_rng(sum(shape))
+    x = (rng.standard_normal(shape) * 2).astype(np.float32)
+    g = rng.standard_normal(shape).astype(np.float32)
+    C = shape[axis]
+    s = rng.uniform(0.01, 0.1, C)
+    z = np.rint(rng.uniform(0, 255, C)) + 0.2
+    gscale = (255 * x.size / C) ** -0.5
+    sp = torch.nn.Parameter(torch.tensor(s, dtype=torch.float64, device=DEV))
+    zp = torch.nn.Parameter(torch.tensor(z, dtype=torch.float64, device=DEV))
+    xg = cu(x, grad=True)
+    y = FQ.PerChannelLearnFn.apply(xg, sp, zp, 0, 255, gscale, True, axis)
+    y.backward(cu(g))
+    yo, gxo, gso, gzo = O.pc_lsq_forward_backward(x, g, s, z, 0, 255, gscale, axis=axis)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(xg.grad), gxo, "grad_x")
+    np.testing.assert_allclose(npy(sp.grad), gso, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(npy(zp.grad), gzo, rtol=1e-9, atol=1e-12)
+
+
+def test_learnable_per_channel_quantizer_weights():
+    """PerChannelUniformQuantizer learnable on an OIHW weight (axis 0, scale [C] f64)."""
+    rng = np.random.default_rng(3)
+    w = (rng.standard_normal((64, 32, 3, 3)) * 0.05).astype(np.float32)
+    g = rng.standard_normal(w.shape).astype(np.float32)
+    q = V.PerChannelUniformQuantizer(4, True)
+    s = rng.uniform(0.005, 0.02, 64)
+    sp = torch.nn.Parameter(torch.tensor(s, dtype=torch.float64, device=DEV))
+    wg = cu(w, grad=True)
+    y = q.quantize(wg, sp, 0, True)
+    y.backward(cu(g))
+    gscale = (q.qmax * w.size / 64) ** -0.5
+    yo, gxo, gso, _ = O.pc_lsq_forward_backward(w, g, s, np.zeros(64), q.qmin, q.qmax, gscale, axis=0,
+                                                learn_zp=False)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(wg.grad), gxo, "grad_w")
+    np.testing.assert_allclose(npy(sp.grad), gso, rtol=1e-9, atol=1e-12)
+
+
+def test_lsq_fake_quantize_axis_mismatch_raises_like_reference():
+    fq = _module(True, False)
+    fq(torch.randn(2, 6, 4, 4, device=DEV))
+    fq.disable_observer()
+    with pytest.raises(RuntimeError):
+        fq(torch.randn(6, 5, 4, 4, device=DEV))    # weights with C_out != C_in

@@ -143,3 +143,21 @@ def test_act_fq(case):
     else:
         G.assert_fq_close(y, G.arr(case["y"]), s, "y")
         G.assert_close_f32(gc, G.arr(case["grad_x"]), "grad_c")
+
+
+@pytest.mark.parametrize("case", G.cases("lsq_fake_quantize"), ids=lambda c: c["key"])
+def test_lsq_fake_quantize(case):
+    """LSQFakeQuantize learnable fwd+bwd (per-channel axis 1 / per-tensor, x5000 for acts)."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    s, z = G.arr(case["scale"]).reshape(-1), G.arr(case["zp"]).reshape(-1)
+    gsc = O.lsq_module_grad_scale(x.shape, case["qmax"], case["per_channel"], case["config_act"])
+    if case["per_channel"]:
+        y, gx, gs, gz = O.pc_lsq_forward_backward(x, g, s, z, case["qmin"], case["qmax"], gsc, axis=1)
+    else:
+        y, gx, gs0, gz0 = O.lsq_forward_backward(x, g, float(s[0]), float(z[0]), case["qmin"], case["qmax"],
+                                                 gsc, learn_zp=True)
+        gs, gz = np.array([gs0]), np.array([gz0])
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+    np.testing.assert_allclose(gs, G.arr(case["scale_grad"]).reshape(-1), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(gz, G.arr(case["zp_grad"]).reshape(-1), rtol=1e-4, atol=1e-6)

@@ -8,8 +8,9 @@ Importing the package registers the quantizer/observer classes by name in
   LSQQuantizer, LSQObserver                         (names the reference README advertises)
   PerChannelUniformQuantizer, PerChannelMinMaxObserver  (per-channel, axis 0)
 
-All arithmetic runs in the HIP kernels of ``csrc/vsiq_kernels.hip`` through the
-C ABI of ``include/vsiq.h``; there is no CPU path.
+plus ``LSQFakeQuantize`` (quantizers/lsq_module.py, the torch.ao-based LSQ module).
+All fake-quant arithmetic runs in the HIP kernels of ``csrc/`` through the C ABI of
+``include/vsiq.h``; there is no CPU path.
 """
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
@@ -24,5 +25,6 @@ from .observers.lsq import LSQObserver  # noqa: F401
 from .observers.per_channel import PerChannelMinMaxObserver  # noqa: F401
 from .quantizers.quantization_manager import QuantizationManager  # noqa: F401
 from .quantizers.fake_quantize import FakeQuantize  # noqa: F401
+from .quantizers.lsq_module import LSQFakeQuantize  # noqa: F401
 
 __version__ = "0.1.0"

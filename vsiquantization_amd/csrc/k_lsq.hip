@@ -187,6 +187,94 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
   return launch_rc();
 }
 
+// ----------------------------------------------------------------------------
+// K6: per-channel learnable (LSQ) backward -- LSQFakeQuantize's per-channel path
+// (quantizers/lsq_module.py:134-166) and a learnable PerChannelUniformQuantizer.
+// A [rows, rowlen] view; row r uses the qparams of channel r % channels.
+// Stage 1: workgroup (row, chunk) of kPcmGroups groups per lane -> grad_x and one
+//          {sum t, sum z} record.  Stage 2: one workgroup per channel folds its
+//          records (rows c, c+C, ...; chunks in order) -> grad_scale[c], grad_zp[c].
+// ----------------------------------------------------------------------------
+constexpr int kPcmGroups = 4;
+
+inline int64_t pcm_chunks(int64_t rowlen) { return cdiv(cdiv(rowlen, 4), (int64_t)kBlock * kPcmGroups); }
+
+template <bool VEC, bool NT, bool ZPL>
+__global__ __launch_bounds__(kBlock) void k_pcm_lsq_bwd(const float *__restrict__ g,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ gx, int64_t rowlen,
+                                                        uint32_t chunks, int64_t channels,
+                                                        const double *__restrict__ scale,
+                                                        const double *__restrict__ zp, float lo,
+                                                        float hi, double *__restrict__ ws) {
+  const int64_t row = blockIdx.x / chunks;
+  const int64_t chunk = blockIdx.x % chunks;
+  const int64_t c = row % channels;
+  const QPSrc src{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0};
+  const QP p = load_qp(src);
+  LsqAcc acc{0.0, 0.0};
+  const int64_t ng = cdiv(rowlen, 4);
+  const float *xr = x + row * rowlen, *gr = g + row * rowlen;
+  float *gxr = gx + row * rowlen;
+  const int64_t base = chunk * kBlock * kPcmGroups + threadIdx.x;
+  f4 xv[kPcmGroups], gv[kPcmGroups];
+#pragma unroll
+  for (int k = 0; k < kPcmGroups; ++k) {
+    xv[k] = load_group_c<VEC, NT>(xr, base + k * kBlock, ng, rowlen);
+    gv[k] = load_group_c<VEC, NT>(gr, base + k * kBlock, ng, rowlen);
+  }
+#pragma unroll
+  for (int k = 0; k < kPcmGroups; ++k)
+    lsq_group<VEC, NT, ZPL, kActNone>(gxr, base + k * kBlock, ng, rowlen, xv[k], gv[k], p, acc);
+  lsq_block_reduce(acc);
+  if (threadIdx.x == 0) {
+    ws[2 * (int64_t)blockIdx.x] = acc.t;
+    ws[2 * (int64_t)blockIdx.x + 1] = acc.z;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pcm_lsq_fold(const double *__restrict__ ws, int64_t rows,
+                                                         uint32_t chunks, int64_t channels,
+                                                         const double *__restrict__ zp, int zp_learn,
+                                                         float lo, float hi, double gscale,
+                                                         double *__restrict__ gs_out,
+                                                         double *__restrict__ gz_out) {
+  const int64_t c = blockIdx.x;
+  const int64_t per = rows / channels * chunks;   // records of channel c, in (row, chunk) order
+  LsqAcc acc{0.0, 0.0};
+  for (int64_t k = threadIdx.x; k < per; k += kBlock) {
+    const int64_t rec = ((k / chunks) * channels + c) * chunks + k % chunks;
+    acc.t += ws[2 * rec];
+    acc.z += ws[2 * rec + 1];
+  }
+  lsq_block_reduce(acc);
+  if (threadIdx.x == 0) {
+    gs_out[c] = acc.t * gscale;
+    if (gz_out) {
+      double gz = 0.0;
+      if (zp_learn) {   // ClampBackward of the rounded zero point (lsq_module.py:339-343)
+        const double zr = __builtin_rint(zp ? zp[c] : 0.0);
+        gz = (zr >= (double)lo && zr <= (double)hi) ? acc.z * gscale : 0.0;
+      }
+      gz_out[c] = gz;
+    }
+  }
+}
+
+template <bool VEC, bool NT>
+void launch_pcm_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                    int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
+                    float hi, double *ws, hipStream_t st) {
+  const int64_t chunks = pcm_chunks(rowlen);
+  const dim3 grid((unsigned)(rows * chunks)), block(kBlock);
+  if (zp_learn)
+    hipLaunchKernelGGL((k_pcm_lsq_bwd<VEC, NT, true>), grid, block, 0, st, g, x, gx, rowlen,
+                       (uint32_t)chunks, channels, scale, zp, lo, hi, ws);
+  else
+    hipLaunchKernelGGL((k_pcm_lsq_bwd<VEC, NT, false>), grid, block, 0, st, g, x, gx, rowlen,
+                       (uint32_t)chunks, channels, scale, zp, lo, hi, ws);
+}
+
 }  // namespace vsiq
 
 using namespace vsiq;
@@ -209,6 +297,32 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
                          void *stream) {
   return lsq_bwd(g, c, gc, n, act, scale_dev, scale_host, zp_dev, zp_host, zp_learn, qmin, qmax,
                  gscale, grad_out, ws, ws_len, counter, stream);
+}
+
+int64_t vsiq_pcm_workspace_doubles(int64_t rows, int64_t rowlen) {
+  if (rows < 0 || rowlen <= 0) return VSIQ_E_ARG;
+  return 2 * rows * pcm_chunks(rowlen);
+}
+
+int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                         int64_t channels, const double *scale, const double *zp, int zp_learn,
+                         int qmin, int qmax, double gscale, double *grad_scale_out,
+                         double *grad_zp_out, double *ws, int64_t ws_len, void *stream) {
+  if (rows <= 0 || rowlen <= 0 || channels <= 0 || rows % channels || qmin > qmax || !g || !x ||
+      !gx || !scale || !grad_scale_out || !ws || (zp_learn && !zp))
+    return VSIQ_E_ARG;
+  const int64_t chunks = pcm_chunks(rowlen);
+  if (rows * chunks > 0x7fffffffLL || channels > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (ws_len < 2 * rows * chunks) return VSIQ_E_WS;
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
+  const bool nt = g_tune.nontemporal != 0;
+  VSIQ_B2(launch_pcm_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
+          (float)qmax, ws, st);
+  hipLaunchKernelGGL(k_pcm_lsq_fold, dim3((unsigned)channels), dim3(kBlock), 0, st, ws, rows,
+                     (uint32_t)chunks, channels, zp, zp_learn, (float)qmin, (float)qmax, gscale,
+                     grad_scale_out, grad_zp_out);
+  return launch_rc();
 }
 
 }  // extern "C"

@@ -47,15 +47,19 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
 // ----------------------------------------------------------------------------
 // per-channel fake-quant with given per-row qparams: grid (rows, chunks)
 // ----------------------------------------------------------------------------
+// row r uses qparams [r % channels]: channels == rows for axis 0 of a [C, ...]
+// tensor; channels == C for axis 1 of an [N, C, ...] tensor viewed as [N*C, HW...]
 struct PCFixed {
   int64_t rowlen;
-  const double *scale, *zp;
+  const double *scale, *zp;   // zp nullable: 0
   int zp_round;
   float lo, hi;
+  int64_t channels;
 };
 
 __device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
-  QPSrc s{nullptr, a.scale + row, a.zp + row, 0.0, 0.0, a.lo, a.hi, a.zp_round, 0};
+  const int64_t c = row % a.channels;
+  QPSrc s{nullptr, a.scale + c, a.zp ? a.zp + c : nullptr, 0.0, 0.0, a.lo, a.hi, a.zp_round, 0};
   return load_qp(s);
 }
 
@@ -140,19 +144,28 @@ int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint64_t *mask
   return launch_pc<false, false, false>(x, y, c, mask, a, st);
 }
 
-int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
-                       int64_t rowlen, const double *scale, const double *zp, int zp_round,
-                       int qmin, int qmax, void *stream) {
-  if (rows < 0 || rowlen <= 0 || qmin > qmax) return VSIQ_E_ARG;
+int vsiq_pcm_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
+                        int64_t rowlen, int64_t channels, const double *scale, const double *zp,
+                        int zp_round, int qmin, int qmax, void *stream) {
+  if (rows < 0 || rowlen <= 0 || qmin > qmax || channels <= 0) return VSIQ_E_ARG;
   if (rows == 0) return 0;
-  if (!x || !y || !scale || !zp || rows * oneshot_grid(cdiv(rowlen, 4)) > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (!x || !y || !scale || rows % channels || rows * oneshot_grid(cdiv(rowlen, 4)) > 0x7fffffffLL)
+    return VSIQ_E_ARG;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
-  PCFixed a{rowlen, scale, zp, zp_round, (float)qmin, (float)qmax};
+  PCFixed a{rowlen, scale, zp, zp_round, (float)qmin, (float)qmax, channels};
   const bool vec = (rowlen % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
   const bool nt = g_tune.nontemporal != 0;
   uint8_t *c = (uint8_t *)codes;
   VSIQ_B2(launch_pc_fixed, vec, nt, x, y, c, mask, a, rows, (hipStream_t)stream);
   return launch_rc();
+}
+
+int vsiq_pc_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, int64_t rows,
+                       int64_t rowlen, const double *scale, const double *zp, int zp_round,
+                       int qmin, int qmax, void *stream) {
+  if (rows > 0 && !zp) return VSIQ_E_ARG;
+  return vsiq_pcm_fq_fwd_f32(x, y, codes, mask, rows, rowlen, rows > 0 ? rows : 1, scale, zp, zp_round,
+                             qmin, qmax, stream);
 }
 
 }  // extern "C"

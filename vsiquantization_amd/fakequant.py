@@ -270,40 +270,114 @@ def stats_from_row_sums(row_stats: torch.Tensor, numel: int) -> torch.Tensor:
     return out.to(torch.float32).to(torch.float64)
 
 
-def per_channel_fake_quant(x, scale: torch.Tensor, zp: torch.Tensor, qmin, qmax, *, zp_round=False,
-                           want_mask=False, want_codes=False):
-    """Per-channel fake quant with given f64 [C] qparams."""
+def _pc_view(x: torch.Tensor, axis: int):
+    """(rows, rowlen, channels) of the row view of x for per-channel axis 0 or 1."""
+    if axis not in (0, 1) or x.dim() <= axis:
+        raise ValueError(f"per-channel axis must be 0 or 1 of a tensor with more dims, got {axis}")
+    C = x.shape[axis]
+    rows = C if axis == 0 else x.shape[0] * C
+    if rows == 0:
+        return 0, 1, max(C, 1)
+    return rows, x.numel() // rows, C
+
+
+def _per_channel_f64(v, C, dev, what):
+    t = v.detach().to(dev, torch.float64).reshape(-1).contiguous()
+    if t.numel() == 1 and C > 1:
+        t = t.expand(C).contiguous()
+    if t.numel() != C:
+        raise RuntimeError(f"per-channel {what} has {t.numel()} entries, the tensor has {C} channels")
+    return t
+
+
+def per_channel_fake_quant(x, scale: torch.Tensor, zp, qmin, qmax, *, zp_round=False,
+                           want_mask=False, want_codes=False, axis=0):
+    """Per-channel fake quant with given [C] qparams (any float dtype; zp may be None = 0)
+    along ``axis`` 0 ([C, ...] weights) or 1 ([N, C, ...] activations)."""
     x = H.require_device_f32(x)
     dev = x.device
-    C = x.shape[0]
+    rows, rowlen, C = _pc_view(x, axis)
     y = torch.empty_like(x)
-    mask = H.mask_buffer(C, x.numel() // C, dev) if want_mask else None
+    mask = H.mask_buffer(rows, rowlen, dev) if want_mask else None
     codes = (torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev)
              if want_codes else None)
-    s = scale.detach().to(dev, torch.float64).contiguous()
-    z = zp.detach().to(dev, torch.float64).contiguous()
-    rc = H.lib().vsiq_pc_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(C),
-                                    _i64(x.numel() // C), H.ptr(s), H.ptr(z), int(bool(zp_round)),
-                                    int(qmin), int(qmax), H.stream_of(dev))
-    H.check(rc, "vsiq_pc_fq_fwd_f32")
+    s = _per_channel_f64(scale, C, dev, "scale")
+    z = _per_channel_f64(zp, C, dev, "zero point") if zp is not None else None
+    rc = H.lib().vsiq_pcm_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(rows),
+                                     _i64(rowlen), _i64(C), H.ptr(s), H.ptr(z), int(bool(zp_round)),
+                                     int(qmin), int(qmax), H.stream_of(dev))
+    H.check(rc, "vsiq_pcm_fq_fwd_f32")
     return y, mask, codes
 
 
 class PerChannelFQFn(torch.autograd.Function):
-    """Per-channel fake quant with given f64 [C] qparams and the STE backward."""
+    """Per-channel fake quant with given [C] qparams and the STE backward."""
 
     @staticmethod
-    def forward(ctx, x, scale, zp, qmin, qmax):
-        y, mask, _ = per_channel_fake_quant(x, scale, zp, qmin, qmax, want_mask=True)
-        s = scale.detach().to(x.device, torch.float64).contiguous()
+    def forward(ctx, x, scale, zp, qmin, qmax, axis=0):
+        y, mask, _ = per_channel_fake_quant(x, scale, zp, qmin, qmax, want_mask=True, axis=axis)
+        rows, rowlen, C = _pc_view(x, axis)
+        s = _per_channel_f64(scale, C, x.device, "scale")
+        if rows != C:   # axis 1: the STE kernel takes one scale per row
+            s = s.repeat(rows // C)
         ctx.save_for_backward(mask, s)
-        ctx.rowlen = x.numel() // x.shape[0]
+        ctx.rowlen = rowlen
         return y
 
     @staticmethod
     def backward(ctx, gy):
         mask, scale = ctx.saved_tensors
-        return ste_backward(gy.contiguous(), mask, scale, ctx.rowlen), None, None, None, None
+        return ste_backward(gy.contiguous(), mask, scale, ctx.rowlen), None, None, None, None, None
+
+
+def pc_lsq_backward(g, x, scale, zp, qmin, qmax, gscale, learn_zp, axis):
+    """K6: (grad_x, grad_scale f64 [C], grad_zp f64 [C])."""
+    g = H.require_device_f32(g, "grad_output")
+    dev = g.device
+    rows, rowlen, C = _pc_view(x, axis)
+    s = _per_channel_f64(scale, C, dev, "scale")
+    z = _per_channel_f64(zp, C, dev, "zero point") if zp is not None else None
+    gx = torch.empty_like(g)
+    gs = torch.empty(C, dtype=torch.float64, device=dev)
+    gz = torch.empty(C, dtype=torch.float64, device=dev)
+    ws = torch.empty(max(1, int(H.lib().vsiq_pcm_workspace_doubles(rows, rowlen))), dtype=torch.float64,
+                     device=dev)
+    rc = H.lib().vsiq_pcm_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(rows), _i64(rowlen), _i64(C),
+                                      H.ptr(s), H.ptr(z), int(bool(learn_zp)), int(qmin), int(qmax),
+                                      float(gscale), H.ptr(gs), H.ptr(gz), H.ptr(ws), _i64(ws.numel()),
+                                      H.stream_of(dev))
+    H.check(rc, "vsiq_pcm_lsq_bwd_f32")
+    return gx, gs, gz
+
+
+class PerChannelLearnFn(torch.autograd.Function):
+    """Learnable per-channel fake quant (K3-fixed forward, K6 backward): LSQFakeQuantize's
+    per-channel path (quantizers/lsq_module.py:134-166) and the learnable
+    PerChannelUniformQuantizer.  scale / zero_point are [C]-element tensors (any shape
+    with C elements, any float dtype); their gradients come back in that shape/dtype,
+    already multiplied by ``gscale`` (ScaleGradient, uniform.py:242-255)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, axis):
+        x = H.require_device_f32(x)
+        y, _, _ = per_channel_fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, axis=axis)
+        ctx.save_for_backward(x)
+        ctx.scale, ctx.zp = scale, zero_point
+        ctx.args = (qmin, qmax, gscale, learn_zp, axis)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        qmin, qmax, gscale, learn_zp, axis = ctx.args
+        s, z = ctx.scale, ctx.zp
+        gx, gs, gz = pc_lsq_backward(gy.contiguous(), x, s, z, qmin, qmax, gscale, learn_zp, axis)
+        out_s = out_z = None
+        if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
+            out_s = gs.to(device=s.device, dtype=s.dtype).reshape(s.shape)
+        if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
+            out_z = gz.to(device=z.device, dtype=z.dtype).reshape(z.shape)
+        return gx, out_s, out_z, None, None, None, None, None
 
 
 class PerChannelObserveFQFn(torch.autograd.Function):

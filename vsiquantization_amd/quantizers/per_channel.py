@@ -3,17 +3,20 @@ with one (scale, zero point) per out-channel (axis 0), build-defined (SURVEY §8
 
 ``quantize(x, scale, zero_point, is_learning_scale)`` takes float64 [C] device
 tensors (PerChannelMinMaxObserver's output).  Scalars fall back to the
-per-tensor UniformQuantizer behaviour.  A learnable per-channel scale is the
-"next" row of SURVEY §8f (LSQFakeQuantize-style) and raises for now.
+per-tensor UniformQuantizer behaviour.  Learnable (``is_learning_scale``): a [C]
+scale Parameter (QuantizationManager.make_learn_qparameter) trained with the
+per-channel LSQ backward (K6, the kernel LSQFakeQuantize's per-channel path uses),
+gradient scale (qmax * numel / C) ** -0.5 -- the per-scale element count, as
+LSQFakeQuantize.calculate_grad_scale does (quantizers/lsq_module.py:326-330).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
-from ..fakequant import PerChannelFQFn, per_channel_fake_quant
+from ..fakequant import PerChannelFQFn, PerChannelLearnFn, per_channel_fake_quant
 from ..utils.registry import register_class
-from .uniform import UniformQuantizer
+from .uniform import UniformQuantizer, _reduce_gscale
 
 
 _ACTS = {"relu": F.relu, "silu": F.silu}
@@ -32,14 +35,18 @@ class PerChannelUniformQuantizer(UniformQuantizer):
             return super().quantize(x, scale, zero_point, is_learning_scale, act=act)
         if act is not None:   # per-channel activations: activation first (torch), then K3-fixed
             x = _ACTS[act](x)
-        if is_learning_scale:
-            raise NotImplementedError("learnable per-channel scale: planned (SURVEY §8f row 2)")
         C = x.shape[0]
+        if is_learning_scale:
+            gscale = float((self.qmax * x.numel() / C) ** -0.5) * _reduce_gscale(self.calib_grad_scale)
+            learn_zp = isinstance(zero_point, torch.Tensor) and zero_point.requires_grad
+            z = zero_point if isinstance(zero_point, torch.Tensor) else torch.full(
+                (C,), float(zero_point), dtype=torch.float64, device=x.device)
+            return PerChannelLearnFn.apply(x, scale, z, self.qmin, self.qmax, gscale, learn_zp, 0)
         s = scale if isinstance(scale, torch.Tensor) else torch.full((C,), float(scale), dtype=torch.float64)
         z = zero_point if isinstance(zero_point, torch.Tensor) else torch.full((C,), float(zero_point),
                                                                                 dtype=torch.float64)
         if s.numel() != C or z.numel() != C:
             raise ValueError(f"per-channel qparams have {s.numel()}/{z.numel()} entries, x has {C} channels")
         if x.requires_grad and torch.is_grad_enabled():
-            return PerChannelFQFn.apply(x, s, z, self.qmin, self.qmax)
+            return PerChannelFQFn.apply(x, s, z, self.qmin, self.qmax, 0)
         return per_channel_fake_quant(x, s, z, self.qmin, self.qmax)[0]
