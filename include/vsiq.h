@@ -257,6 +257,16 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
                          int qmin, int qmax, double gscale, double *grad_scale_out,
                          double *grad_zp_out, double *ws, int64_t ws_len, void *stream);
 
+/*
+ * BatchNorm folding (modules/fused.py:100-108, :294-300), fp32, reference order:
+ *   f = gamma / sqrt(running_var + eps);  w_out[r,:] = w[r,:] * f[r]
+ *   b_out[r] = beta[r] + (b[r] - running_mean[r]) * f[r]      (b NULL: 0; b_out nullable)
+ * rows = out-channels, rowlen = elements per out-channel.  In-place (w_out == w) allowed.
+ */
+int vsiq_bn_fold_f32(const float *w, const float *b, const float *gamma, const float *beta,
+                     const float *running_mean, const float *running_var, float eps, float *w_out,
+                     float *b_out, int64_t rows, int64_t rowlen, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

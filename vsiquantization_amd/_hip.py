@@ -69,6 +69,7 @@ _SIGS = {
     "vsiq_pcm_workspace_doubles": ([c_i64, c_i64], c_i64),
     "vsiq_pcm_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p,
                               c_p, c_p, c_i64, c_p], c_int),
+    "vsiq_bn_fold_f32": ([c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_i64, c_i64, c_p], c_int),
     "vsiq_act_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_d, c_p, c_d, c_int, c_int,
                              c_int, c_int, c_p], c_int),
     "vsiq_act_observe_f32": ([c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p],

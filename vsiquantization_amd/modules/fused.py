@@ -27,13 +27,36 @@ def _clone_conv(cv: nn.Conv2d, with_bias: bool) -> nn.Conv2d:
 
 
 def _bn_fold(weight, bias, bn, view):
-    """(W * gamma/std, beta + (b - mean) * gamma/std) with std = sqrt(running_var + eps)."""
+    """(W * gamma/std, beta + (b - mean) * gamma/std) with std = sqrt(running_var + eps).
+
+    On a GPU module this is one HIP launch (vsiq_bn_fold_f32); a module still on the host
+    (the usual fuse-then-.cuda() flow) folds with the same torch ops as the reference."""
+    if weight.device.type == "cuda" and weight.dtype == torch.float32:
+        return bn_fold_device(weight, bias, bn)
     gamma = bn.weight.data.clone()
     beta = bn.bias.data.clone()
     std = torch.sqrt(bn.running_var.data.clone() + bn.eps)
     w = weight * (gamma / std).reshape(view)
     b = beta + (bias - bn.running_mean.data.clone()) * (gamma / std)
     return w, b
+
+
+def bn_fold_device(weight, bias, bn):
+    """BatchNorm fold on the device (k_bnfold.hip), bit-identical to the torch ops above."""
+    from .. import _hip as H
+    dev = weight.device
+    w = weight.detach().contiguous()
+    rows = w.shape[0]
+    f32 = lambda t: t.detach().to(dev, torch.float32).contiguous()   # noqa: E731
+    b = f32(bias) if isinstance(bias, torch.Tensor) else None
+    w_out = torch.empty_like(w)
+    b_out = torch.empty(rows, dtype=torch.float32, device=dev)
+    rc = H.lib().vsiq_bn_fold_f32(H.ptr(w), H.ptr(b), H.ptr(f32(bn.weight)), H.ptr(f32(bn.bias)),
+                                  H.ptr(f32(bn.running_mean)), H.ptr(f32(bn.running_var)), float(bn.eps),
+                                  H.ptr(w_out), H.ptr(b_out), H.c_i64(rows), H.c_i64(w.numel() // max(rows, 1)),
+                                  H.stream_of(dev))
+    H.check(rc, "vsiq_bn_fold_f32")
+    return w_out, b_out
 
 
 def _activation(x, is_relu):

@@ -90,3 +90,28 @@ def data_calib(model, calib_loader, device, num_batches=16):
         if i == num_batches - 1:
             break
     model.train()
+
+
+def load_partial_checkpoint(model, checkpoint_path):
+    """Load the entries of a saved state_dict whose names and shapes match the model
+    (reference: utils/util.py:17-40).  The learnable qparams are float64 Parameters named
+    ``<layer>.weight_quantizer.scale`` / ``.activation_quantizer.scale`` once
+    activate_learning_qparam has run (yolov8_qat.py:299 saves them).  Loads with
+    ``weights_only=True`` (tensors only, nothing executed from the file)."""
+    import torch
+    checkpoint_state_dict = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+    model_state_dict = model.state_dict()
+    matched = {}
+    for name, param in checkpoint_state_dict.items():
+        if name in model_state_dict:
+            if model_state_dict[name].shape == param.shape:
+                matched[name] = param
+            else:
+                print(f"Skip loading parameter: {name} due to shape mismatch "
+                      f"({param.shape} vs {model_state_dict[name].shape})")
+        else:
+            print(f"Skip loading parameter: {name} as it's not in the model")
+    model_state_dict.update(matched)
+    model.load_state_dict(model_state_dict)
+    print(f"Loaded {len(matched)} layers from checkpoint.")
+    return len(matched)
