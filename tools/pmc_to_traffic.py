@@ -10,35 +10,46 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
-KERNEL_KEYS = {  # kernel-name fragment -> bench.py kernel label
-    "k_pc_observe_fq<": "pc_observe_fq_fwd",
-    "k_ste_bwd<": "ste_bwd",
-    "k_fq_fwd<": "fq_fwd",
-    "k_lsq_bwd<": "lsq_bwd",
+# workload -> {kernel-name fragment: (bench.py kernel label, launches of it per step)}
+KERNEL_KEYS = {
+    "c2": {"k_pc_observe_fq<": ("pc_observe_fq_fwd", 1), "k_ste_bwd<": ("ste_bwd", 1)},
+    "c3": {"k_fq_fwd<": ("fq_fwd", 1), "k_lsq_bwd<": ("lsq_bwd", 1)},
+    # C4: per step 27 weight + 27 fused-ReLU activation launches each way
+    "c4": {"k_fq_fwd<": ("fwd_all_layers", 54), "k_lsq_bwd<": ("bwd_all_layers", 54)},
+    # C5: 27 fused-ReLU observer launches per calibration batch
+    "c5": {"k_observe<": ("observe_all_layers", 27)},
 }
 
 
-def per_kernel(d, counter):
+def per_kernel(d, counter, keys):
+    """Mean counter value per dispatch of each label x launches per step."""
     acc = collections.defaultdict(list)
     for f in glob.glob(f"{d}/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            for frag, label in KERNEL_KEYS.items():
+            for frag, (label, _) in keys.items():
                 if frag in r["Kernel_Name"]:
                     acc[label].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    per = {label: mult for _, (label, mult) in keys.items()}
+    return {k: sum(v) / len(v) * per[k] for k, v in acc.items()}
 
 
 def main():
     out = sys.argv[1]
-    res = {"note": "HBM bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 corrections)"}
+    res = {"note": "HBM bytes per launch (C4/C5: per step, all of the label's launches) = "
+                   "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 corrections)"}
+    if os.path.exists(out):   # keep workloads not re-measured in this call
+        old = json.load(open(out))
+        res.update({k: v for k, v in old.items() if k != "note"})
     for arg in sys.argv[2:]:
         wl, dirs = arg.split("=")
         fdir, wdir = dirs.split(",")
-        fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+        keys = KERNEL_KEYS[wl]
+        fetch, write = per_kernel(fdir, "FETCH_SIZE", keys), per_kernel(wdir, "WRITE_SIZE", keys)
         res[wl] = {k: {"fetch_bytes": 2 * fetch[k] * 1024, "write_bytes": write.get(k, 0.0) * 1024,
                        "hbm_bytes_per_launch": 2 * fetch[k] * 1024 + write.get(k, 0.0) * 1024}
                    for k in fetch}

@@ -14,13 +14,18 @@ run() {
   return $rc
 }
 export TMPDIR=/tmp
-for W in ${WORKLOADS:-c2 c3}; do
-  run bench_$W 600 python3 -u bench.py --workload $W --steps 200 --warmup 20 ${BENCH_EXTRA:-} || exit $?
+for W in ${WORKLOADS:-c2 c3 c4 c5}; do
+  case $W in
+    c4) S=20; WU=4; SP=8; WP=2 ;;
+    c5) S=16; WU=2; SP=16; WP=2 ;;
+    *)  S=200; WU=20; SP=40; WP=5 ;;
+  esac
+  run bench_$W 600 python3 -u bench.py --workload $W --steps $S --warmup $WU ${BENCH_EXTRA:-} || exit $?
   run prof_$W 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$W -o run --output-format csv \
-      -- python3 -u bench.py --workload $W --steps 200 --warmup 20 --no-cpu-baseline || exit $?
+      -- python3 -u bench.py --workload $W --steps $S --warmup $WU --no-cpu-baseline || exit $?
   for C in FETCH_SIZE WRITE_SIZE; do
     run pmc_${W}_$C 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${TAG}_${W}_$C -o run --output-format csv \
-        -- python3 -u bench.py --workload $W --steps 40 --warmup 5 --no-cpu-baseline || exit $?
+        -- python3 -u bench.py --workload $W --steps $SP --warmup $WP --no-cpu-baseline || exit $?
   done
 done
 exit 0

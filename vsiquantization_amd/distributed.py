@@ -78,12 +78,18 @@ def replay_minmax_tensor(init_min, init_max, recs: torch.Tensor):
     values are the same bits except +-0, which a strict compare never swaps), else the
     initial value; NaN calls are skipped."""
     nan_call = recs[..., H.ST_NAN] > 0
-    inf = torch.tensor(float("inf"), dtype=recs.dtype, device=recs.device)
-    mins = torch.where(nan_call, inf, recs[..., H.ST_MIN]).amin(dim=-1)
-    maxs = torch.where(nan_call, -inf, recs[..., H.ST_MAX]).amax(dim=-1)
-    init_min = torch.as_tensor(init_min, dtype=recs.dtype, device=recs.device)
-    init_max = torch.as_tensor(init_max, dtype=recs.dtype, device=recs.device)
-    return torch.where(mins < init_min, mins, init_min), torch.where(maxs > init_max, maxs, init_max)
+    mins = recs[..., H.ST_MIN].masked_fill(nan_call, float("inf")).amin(dim=-1)
+    maxs = recs[..., H.ST_MAX].masked_fill(nan_call, float("-inf")).amax(dim=-1)
+
+    def as_t(v):   # python numbers stay host scalars (no host->device copy, no sync)
+        if isinstance(v, torch.Tensor):
+            return v.to(recs.device, recs.dtype)
+        if isinstance(v, (list, tuple)):
+            return torch.tensor(v, dtype=recs.dtype).to(recs.device, non_blocking=True)
+        return torch.full_like(mins, float(v))
+
+    lo, hi = as_t(init_min), as_t(init_max)
+    return torch.where(mins < lo, mins, lo), torch.where(maxs > hi, maxs, hi)
 
 
 def _deferred_managers(model):
