@@ -81,6 +81,8 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_PC_ROWS_PER_BLOCK 1  /* K3 rows per workgroup, 0 = auto */
 #define VSIQ_TUNE_NONTEMPORAL 2        /* 1 = nontemporal streamed loads/stores (default) */
 #define VSIQ_TUNE_PC_BLOCK 5           /* K3 workgroup size 256 / 512 / 1024, 0 = auto */
+#define VSIQ_TUNE_STORE_DEFER 6        /* one-round grids: hold stores back N x 512 clocks after
+                                          the loads (-1 = auto, 0 = off, max 64) */
 int vsiq_set_tuning(int key, int value);
 
 /*

@@ -59,6 +59,21 @@ def test_argument_validation_without_gpu():
                                 null, 0, null, null) == -1
 
 
+def test_tuning_keys_match_header_and_bounds():
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "vsiq.h")).read()
+    keys = dict(re.findall(r"#define VSIQ_(TUNE_\w+) (\d+)", hdr))
+    for name in ("TUNE_PC_ROWS_PER_BLOCK", "TUNE_NONTEMPORAL", "TUNE_PC_BLOCK", "TUNE_STORE_DEFER"):
+        assert int(keys[name]) == getattr(H, name), name
+    lib = H.lib()
+    assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, 65) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, -2) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, 4) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, -1) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_PC_BLOCK, 384) != 0
+    assert lib.vsiq_set_tuning(99, 0) != 0
+
+
 def test_no_cpu_fallback_in_product():
     """The product package never imports the oracle."""
     pkg = os.path.join(ROOT, "vsiquantization_amd")

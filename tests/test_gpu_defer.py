@@ -1,0 +1,77 @@
+"""Deferred store phase (defer_stores, VSIQ_TUNE_STORE_DEFER) of the STE backward.
+
+The deferral only changes when a workgroup's stores are issued, never what they hold:
+the one-round 9-groups-per-lane path (automatic for 384..1024 workgroups) must equal
+the plain kFlatU path bit for bit, and the oracle (oracle/fakequant_np.py
+fq_backward_fixed / per_channel_backward_fixed / act_backward, reference
+quantizers/uniform.py:54-55,95 autograd) on the same inputs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import fakequant as FQ
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TUNE_STORE_DEFER = H.TUNE_STORE_DEFER
+
+
+@pytest.fixture
+def defer_tuning():
+    yield lambda v: H.set_tuning(TUNE_STORE_DEFER, v)
+    H.set_tuning(TUNE_STORE_DEFER, -1)
+
+
+def _inputs(rows, rowlen, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((rows, rowlen)) * 0.05).astype(np.float32)
+    g = rng.standard_normal((rows, rowlen)).astype(np.float32)
+    g.flat[::9973] = np.nan
+    g.flat[5::10007] = np.inf
+    g.flat[7::8191] = np.float32(1e-41)   # denormal -> IEEE fallback group
+    return x, g
+
+
+@pytest.mark.parametrize("rows", [512, 768, 1024])
+def test_per_channel_ste_deferred_equals_plain_and_oracle(rows, defer_tuning):
+    rowlen = 9216
+    x, g = _inputs(rows, rowlen, rows)
+    scales = np.linspace(2e-4, 3e-3, rows)
+    # per-row forward with clamping (tight scales) to get a non-trivial mask
+    xd = torch.from_numpy(x).to(DEV)
+    sd = torch.from_numpy(scales).to(DEV)
+    _, mask, _ = FQ.per_channel_fake_quant(xd, sd, None, -128, 127, want_mask=True)
+    m = G.unpack_mask(mask.cpu().numpy(), rows, rowlen)
+    assert 0 < m.sum() < m.size
+    gd = torch.from_numpy(g).to(DEV)
+    outs = {}
+    for v in (-1, 0, 3):
+        defer_tuning(v)
+        outs[v] = FQ.ste_backward(gd, mask, sd, rowlen).cpu().numpy()
+    want = O.per_channel_backward_fixed(g, m, scales)
+    for v, got in outs.items():
+        G.assert_bitwise_f32(got, want, f"defer={v}")
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+def test_flat_ste_deferred_equals_plain(act, defer_tuning):
+    n = 1024 * 9216   # one-round grid of 1024 workgroups: automatic deferral
+    x, g = _inputs(1, n, 7)
+    c = torch.from_numpy(x.reshape(-1) * 40).to(DEV)
+    s = 0.021
+    _, mask, _ = FQ.fake_quant(c, s, 0, -8, 7, want_mask=True, act=act)
+    gd = torch.from_numpy(g.reshape(-1)).to(DEV)
+    outs = {}
+    for v in (-1, 0, 5):
+        defer_tuning(v)
+        outs[v] = FQ.ste_backward(gd, mask, s, pre=c if act else None, act=act).cpu().numpy()
+    G.assert_bitwise_f32(outs[-1], outs[0], "auto vs plain")
+    G.assert_bitwise_f32(outs[5], outs[0], "forced vs plain")
+    if act is None:
+        m = G.unpack_mask(mask.cpu().numpy(), 1, n).reshape(-1)
+        G.assert_bitwise_f32(outs[-1], O.fq_backward_fixed(g.reshape(-1), m, s), "oracle")
+

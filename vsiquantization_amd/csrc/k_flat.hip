@@ -266,6 +266,19 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   return launch_rc();
 }
 
+// CU count of the current device (cached; 256 on MI355X)
+int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
 }  // namespace vsiq
 
 using namespace vsiq;
@@ -298,6 +311,10 @@ int vsiq_set_tuning(int key, int value) {
   switch (key) {
     case VSIQ_TUNE_PC_ROWS_PER_BLOCK: g_tune.pc_rows_per_block = value; return 0;
     case VSIQ_TUNE_NONTEMPORAL: g_tune.nontemporal = value; return 0;
+    case VSIQ_TUNE_STORE_DEFER:
+      if (value < -1 || value > 64) return VSIQ_E_ARG;
+      g_tune.store_defer = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;

@@ -20,6 +20,7 @@ struct PCArgs {
   int sym;
   float lo, hi;
   double qden, eps;
+  uint32_t defer;      // deferred store phase (defer_stores units), 0 = off
 };
 
 struct RowSums {
@@ -139,6 +140,7 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
     go[k] = fq_out_row<VEC, CODES, MASK>(v[k], p, threadIdx.x + k * BS, a.rowlen);
     if (MASK) mask_put(mlo, mhi, k, go[k].b);
   }
+  if (a.defer) defer_stores(a.defer);   // after pc_row_qparams' barrier
   const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {

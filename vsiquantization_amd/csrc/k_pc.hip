@@ -33,10 +33,12 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
   // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
   int rpb = g_tune.pc_rows_per_block;
   if (rpb <= 0) rpb = 1;
+  PCArgs b = a;
+  b.defer = (bs == 256 && rpb == 1) ? store_defer_units(a.rows, false) : 0;
   bool ok = false;
-  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, a, rpb, st);
-  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, a, rpb, st);
-  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, a, rpb, st);
+  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, b, rpb, st);
+  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, b, rpb, st);
+  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, b, rpb, st);
   if (!ok)
     hipLaunchKernelGGL((k_pc_observe_fq_long<VEC, NT>), dim3((unsigned)a.rows), dim3(kBlock), 0, st, x,
                        y, c, m, a);
@@ -131,7 +133,7 @@ int vsiq_pc_observe_fq_f32(const float *x, float *y, void *codes, uint64_t *mask
   if (rows > 0x7fffffffLL) return VSIQ_E_ARG;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
   PCArgs a{rows, rowlen, run_min, run_max, scale_out, zp_out, row_stats, symmetric, (float)qmin,
-           (float)qmax, qden, eps};
+           (float)qmax, qden, eps, 0u};
   const bool vec = (rowlen % 4 == 0) && aligned16(x) && (!y || aligned16(y)) && (!codes || aligned4(codes));
   const bool nt = g_tune.nontemporal != 0;
   hipStream_t st = (hipStream_t)stream;

@@ -7,18 +7,19 @@ namespace vsiq {
 // STE backward with the saved 1-bit mask: gx = (m ? g*s : 0) / s, grid (rows, chunks)
 // (division: ste_quot in vsiq_common.cuh)
 // ----------------------------------------------------------------------------
-// one-shot: workgroup b covers chunk b % chunks of row b / chunks (kFlatU groups per
-// lane).  A wave's 64 groups are one 256-element mask chunk: its four mask words
-// are wave-uniform, read with scalar loads and used directly as lane masks.
+// one-shot: workgroup b covers chunk b % chunks of row b / chunks (U groups per lane:
+// kFlatU, or 9 for a one-round grid with a deferred store phase, see defer_stores).
+// A wave's 64 groups are one 256-element mask chunk: its four mask words are
+// wave-uniform, read with scalar loads and used directly as lane masks.
 // ACT (K5): `pre` holds the pre-activation c of a fused ReLU/SiLU; the result is
 // the activation's backward applied to the quantizer's grad_x.
-template <bool VEC, bool NT, int ACT>
+template <bool VEC, bool NT, int ACT, int U>
 __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     const uint64_t *__restrict__ mask,
                                                     const float *__restrict__ pre,
                                                     float *__restrict__ gx, int64_t rowlen,
                                                     uint32_t chunks, const double *__restrict__ sdev,
-                                                    double shost) {
+                                                    double shost, uint32_t defer) {
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
   const SteDiv d = make_stediv((float)(sdev ? sdev[row] : shost));
@@ -27,25 +28,25 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
   const float *gr = g + row * rowlen;
   float *xr = gx + row * rowlen;
   const uint64_t *mr = mask + row * mask_words_per_row(rowlen);
-  const int64_t base = chunk * kBlock * kFlatU + threadIdx.x;
+  const int64_t base = chunk * kBlock * U + threadIdx.x;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-  f4 v[kFlatU], cv[kFlatU];
-  uint64_t w[kFlatU][4];
+  f4 v[U], cv[U];
+  uint64_t w[U][4];
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
     v[u] = load_group<VEC, NT>(gr, i < ng ? i : ng - 1, rowlen);
     if (ACT) cv[u] = load_group<VEC, NT>(pre + row * rowlen, i < ng ? i : ng - 1, rowlen);
-    int64_t c = chunk * (kBlock / kWave) * kFlatU + u * (kBlock / kWave) + wave0;
+    int64_t c = chunk * (kBlock / kWave) * U + u * (kBlock / kWave) + wave0;
     c = c < nchunk ? c : nchunk - 1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[u][j] = mr[4 * c + j];
   }
   // all groups computed before the first store: a (predicated, hence branched-around)
   // store ahead of a load's use would make hipcc wait for the store as well
-  f4 o[kFlatU];
+  f4 o[U];
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const bool m0 = __builtin_amdgcn_inverse_ballot_w64(w[u][0]);
     const bool m1 = __builtin_amdgcn_inverse_ballot_w64(w[u][1]);
     const bool m2 = __builtin_amdgcn_inverse_ballot_w64(w[u][2]);
@@ -62,8 +63,12 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
     }
     if (ACT) o[u] = act_bwd4<ACT>(o[u], cv[u]);
   }
+  if (defer) {   // kernel-uniform
+    __syncthreads();
+    defer_stores(defer);
+  }
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
     if (i < ng) store_group<VEC, NT>(xr, i, rowlen, o[u]);
   }
@@ -73,9 +78,17 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
 template <int ACT, bool VEC, bool NT>
 void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *gx, int64_t rows,
                     int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
-  const int64_t chunks = oneshot_grid(cdiv(rowlen, 4));
-  hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0, st, g,
-                     m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost);
+  const int64_t ng = cdiv(rowlen, 4);
+  const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
+  const uint32_t defer = chunks9 * kBlock * 9 - ng <= ng / 8 ? store_defer_units(rows * chunks9, true) : 0;
+  if (defer) {
+    hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock), 0, st,
+                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer);
+    return;
+  }
+  const int64_t chunks = oneshot_grid(ng);
+  hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, kFlatU>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0,
+                     st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u);
 }
 
 template <int ACT>

@@ -50,6 +50,7 @@ struct Tuning {
   int pc_rows_per_block = 0;   // K3 rows per workgroup (0 = auto)
   int pc_block = 0;            // K3 workgroup size 256/512/1024 (0 = auto)
   int nontemporal = 1;         // nt hints on streamed loads/stores
+  int store_defer = -1;        // deferred store phase, units of 512 clocks (-1 = auto, 0 = off)
 };
 extern Tuning g_tune;
 
@@ -744,6 +745,32 @@ __device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_n
 inline bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 inline bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
 inline bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
+
+// Deferred store phase.  A grid that streams its whole input in one round (every
+// workgroup resident at once, all loads issued at t = 0) runs faster on MI355X's HBM3E
+// when a workgroup holds its stores back for ~2 us after its loads have landed: the
+// device then reads, and then writes, instead of interleaving the two from the first
+// returned load on (C2 size, 1024 workgroups of 256 lanes x 9 groups: STE 14.0 ->
+// 11.9 us, 5.4 -> 6.3 TB/s; measured, tools/exp/phase_*).  Called after a barrier, with
+// a wave-uniform unit count (512 clocks each); a pure delay, never a correctness issue.
+__device__ __forceinline__ void defer_stores(uint32_t units) {
+  for (uint32_t k = 0; k < units; ++k) __builtin_amdgcn_s_sleep(8);
+}
+
+// host: defer_stores units for a one-round grid of `grid` workgroups of 256 lanes x 9
+// groups (override: vsiq_set_tuning(VSIQ_TUNE_STORE_DEFER, units)).  Automatic only
+// where it was measured to pay (`auto_ok`: the STE backward, 9216-element rows x 512 /
+// 768 / 1024 rows: -8 / -15 / -16 %): 1.5..4 workgroups per CU, ~0.3 x the read phase
+// (2.5 units per workgroup per CU).  K3's row reduction already delays its stores
+// (deferring further only cost time there), and grids of more than one round lose.
+int device_cus();
+inline uint32_t store_defer_units(int64_t grid, bool auto_ok) {
+  if (g_tune.store_defer >= 0) return (uint32_t)g_tune.store_defer;
+  if (!auto_ok) return 0;
+  const int64_t cus = device_cus();
+  if (2 * grid < 3 * cus || grid > 4 * cus) return 0;
+  return (uint32_t)((5 * grid + cus) / (2 * cus));
+}
 
 // one-shot streaming grid: every lane owns kFlatU groups, no loop (a loop around
 // loads + stores makes hipcc wait for the stores at the loop header: on CDNA the
