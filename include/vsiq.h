@@ -19,10 +19,10 @@
  *     PyTorch CPU path.  Quantization parameters are computed in float64 on
  *     the device exactly as the reference does on the host in Python floats.
  *   - Workspaces: `ws` is a float64 device buffer of at least
- *     vsiq_workspace_doubles(n) entries and `counter` one uint32 device word
- *     that is 0 before the first call; every reducing kernel resets it to 0
- *     when it finishes (stream-ordered reuse is safe, concurrent reuse on two
- *     streams is not).
+ *     vsiq_workspace_doubles(n) entries and `counter` VSIQ_COUNTER_WORDS uint32
+ *     device words that are 0 before the first call; every reducing kernel
+ *     leaves them 0 when it finishes (stream-ordered reuse is safe, concurrent
+ *     reuse on two streams is not).
  *   - Straight-through masks are ONE BIT per element (1 = the rounded value was
  *     inside [qmin, qmax], ClampBackward1 semantics), packed in uint64 words:
  *     a tensor is viewed as `rows` rows of `rowlen` elements (per-tensor: one
@@ -42,7 +42,10 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 2
+#define VSIQ_ABI_VERSION 3
+
+/* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
+#define VSIQ_COUNTER_WORDS 64
 
 #define VSIQ_E_ARG (-1)      /* invalid argument (null pointer, bad size, qmin>qmax) */
 #define VSIQ_E_ALIGN (-2)    /* misaligned pointer where alignment is required */
@@ -81,6 +84,8 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_PC_ROWS_PER_BLOCK 1  /* K3 rows per workgroup, 0 = auto */
 #define VSIQ_TUNE_NONTEMPORAL 2        /* 1 = nontemporal streamed loads/stores (default) */
 #define VSIQ_TUNE_PC_BLOCK 5           /* K3 workgroup size 256 / 512 / 1024, 0 = auto */
+#define VSIQ_TUNE_OBS_KERNEL 7         /* K2 observer: 0 auto, 1 one-shot, 2 grid-stride */
+#define VSIQ_TUNE_OBS_GRID 8           /* K2 grid-stride workgroups, 0 = auto (512), max 2048 */
 #define VSIQ_TUNE_STORE_DEFER 6        /* one-round grids: hold stores back N x 512 clocks after
                                           the loads (-1 = auto, 0 = off, max 64) */
 int vsiq_set_tuning(int key, int value);

@@ -25,7 +25,8 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
 ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)
@@ -33,6 +34,7 @@ ST_LEN = 10
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6
+TUNE_OBS_KERNEL, TUNE_OBS_GRID = 7, 8
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
@@ -157,7 +159,7 @@ class _Workspace:
 
     def __init__(self, device, n):
         self.device = device
-        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
+        self.counter = torch.zeros(COUNTER_WORDS, dtype=torch.int32, device=device)
         self.ws = None
         self.ws_len = 0
         self.reserve(n)

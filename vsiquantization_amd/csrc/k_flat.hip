@@ -71,28 +71,13 @@ __device__ __forceinline__ void obs_block_reduce(ObsAcc &a) {
   __syncthreads();
 }
 
-// One-shot: G groups per lane (grid = ng / (256 G)), all G loads issued up front
-// (no loop: the loads of a wave stay in flight together and s_waitcnt is exact).
-template <bool VEC, bool NT, int ACT, int G>
-__global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x, int64_t n,
-                                                    double *__restrict__ stats_out,
-                                                    float *__restrict__ run_minmax,
-                                                    double *__restrict__ qp_out, int sym,
-                                                    double qden, double eps,
-                                                    double *__restrict__ ws,
-                                                    uint32_t *__restrict__ counter) {
-  ObsAcc a;
-  obs_init(a);
-  const int64_t ng = cdiv(n, 4);
-  const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
-  f4 v[G];
-#pragma unroll
-  for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
-#pragma unroll
-  for (int k = 0; k < G; ++k) {
-    const int64_t i = base + k * kBlock;
-    if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
-  }
+// Block partial -> workspace record; the last block to arrive folds all records in a
+// fixed order, writes the stats record and applies the running update.
+__device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *__restrict__ stats_out,
+                                                 float *__restrict__ run_minmax,
+                                                 double *__restrict__ qp_out, int sym, double qden,
+                                                 double eps, double *__restrict__ ws,
+                                                 uint32_t *__restrict__ counter) {
   obs_block_reduce(a);
   if (threadIdx.x == 0) {
     double *r = ws + (int64_t)blockIdx.x * kPartials;
@@ -142,6 +127,64 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
     observer_update(a.mn, a.mx, has_nan, run_minmax, qp_out, sym, qden, eps);
     *counter = 0u;   // ready for the next stream-ordered launch
   }
+}
+
+// One-shot: G groups per lane (grid = ng / (256 G)), all G loads issued up front
+// (no loop: the loads of a wave stay in flight together and s_waitcnt is exact).
+template <bool VEC, bool NT, int ACT, int G>
+__global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x, int64_t n,
+                                                    double *__restrict__ stats_out,
+                                                    float *__restrict__ run_minmax,
+                                                    double *__restrict__ qp_out, int sym,
+                                                    double qden, double eps,
+                                                    double *__restrict__ ws,
+                                                    uint32_t *__restrict__ counter) {
+  ObsAcc a;
+  obs_init(a);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
+  f4 v[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const int64_t i = base + k * kBlock;
+    if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+  }
+  observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+}
+
+// Grid-stride: a fixed grid (at most kObsGrid workgroups, independent of the device, so
+// the accumulation order is fixed per n) walks the tensor U groups per lane per step.
+// A pure read (no stores share vmcnt with the loads), latency hidden by the other
+// waves of the CU.  Fewer, longer-lived workgroups than the one-shot form: fewer
+// partial records to fold and arrivals to serialize (MI355X, C5 layer sizes:
+// 52M elements 53.2 -> 38.6 us, 1.6M 10.1 -> 9.4 us; tools/exp/obs_bench.py).
+template <bool VEC, bool NT, int ACT, int U>
+__global__ __launch_bounds__(kBlock) void k_observe_loop(const float *__restrict__ x, int64_t n,
+                                                          double *__restrict__ stats_out,
+                                                          float *__restrict__ run_minmax,
+                                                          double *__restrict__ qp_out, int sym,
+                                                          double qden, double eps,
+                                                          double *__restrict__ ws,
+                                                          uint32_t *__restrict__ counter) {
+  ObsAcc a;
+  obs_init(a);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t nfull = n / 4;
+  const int64_t step = (int64_t)gridDim.x * kBlock * U;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock * U; b < ng; b += step) {
+    f4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = b + threadIdx.x + k * kBlock;
+      if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+      else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+    }
+  }
+  observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
 }
 
 // Finalize from an externally reduced stats record (multi-GPU: stats all-reduced
@@ -231,14 +274,35 @@ void launch_observe_g(const float *x, int64_t n, double *stats_out, float *run_m
                      stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
 }
 
+template <int ACT, bool VEC, bool NT>
+void launch_observe_loop(const float *x, int64_t n, double *stats_out, float *run_minmax, double *qp_out,
+                         int sym, double qden, double eps, double *ws, uint32_t *counter, int64_t grid,
+                         hipStream_t st) {
+  hipLaunchKernelGGL((k_observe_loop<VEC, NT, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x,
+                     n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+}
+
+// K2 grid: grid-stride kernel (default) or the one-shot kernel (VSIQ_TUNE_OBS_KERNEL 1)
+inline int64_t observe_grid(int64_t ng) {
+  if (g_tune.obs_kernel == 1) return lsq_grid(ng);
+  const int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : kObsGrid;
+  return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(ng, (int64_t)kBlock * kObsU)));
+}
+
 template <int ACT>
 void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_out, float *run_minmax,
                     double *qp_out, int sym, double qden, double eps, double *ws, uint32_t *counter,
                     hipStream_t st) {
-  // same groups-per-lane rule and grid as K4 (lsq_grid), so vsiq_workspace_doubles covers both
   const int64_t ng = cdiv(n, 4);
+  const int64_t grid = observe_grid(ng);
+  if (g_tune.obs_kernel != 1) {
+    if (vec && nt) launch_observe_loop<ACT, true, true>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
+    else if (vec) launch_observe_loop<ACT, true, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
+    else launch_observe_loop<ACT, false, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
+    return;
+  }
+  // one-shot: same groups-per-lane rule and grid as K4 (lsq_grid)
   const int per_lane = lsq_groups_per_lane(ng);
-  const int64_t grid = lsq_grid(ng, per_lane);
 #define VSIQ_OBS(V, N)                                                                              \
   (per_lane == kLsqGroups                                                                           \
        ? launch_observe_g<ACT, V, N, kLsqGroups>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, \
@@ -258,7 +322,7 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
             void *stream) {
   if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
   const bool vec = aligned16(x) && n % 4 == 0;
-  const int64_t grid = lsq_grid(cdiv(n, 4));
+  const int64_t grid = observe_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < grid * kPartials) return VSIQ_E_WS;
   VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
@@ -311,6 +375,14 @@ int vsiq_set_tuning(int key, int value) {
   switch (key) {
     case VSIQ_TUNE_PC_ROWS_PER_BLOCK: g_tune.pc_rows_per_block = value; return 0;
     case VSIQ_TUNE_NONTEMPORAL: g_tune.nontemporal = value; return 0;
+    case VSIQ_TUNE_OBS_KERNEL:
+      if (value < 0 || value > 2) return VSIQ_E_ARG;
+      g_tune.obs_kernel = value;
+      return 0;
+    case VSIQ_TUNE_OBS_GRID:
+      if (value != 0 && (value < 1 || value > kMaxReduceGrid)) return VSIQ_E_ARG;
+      g_tune.obs_grid = value;
+      return 0;
     case VSIQ_TUNE_STORE_DEFER:
       if (value < -1 || value > 64) return VSIQ_E_ARG;
       g_tune.store_defer = value;

@@ -35,6 +35,11 @@ constexpr int kWave = 64;
 constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // minimum partial-record slots of a workspace
 constexpr int kPartials = 8;           // doubles per partial record
+constexpr int kArriveFlat = 128;       // grids above this arrive in two levels (arrive_last)
+constexpr int kArriveGroups = 32;      // level-1 arrival counters (counter words 1..32)
+static_assert(1 + kArriveGroups <= VSIQ_COUNTER_WORDS, "counter words");
+constexpr int kObsGrid = 512;          // K2 grid-stride: workgroups (fixed: order independent of device)
+constexpr int kObsU = 8;               // K2 grid-stride: groups per lane per step
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
 constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workgroups -> fewer partials)
 #ifndef VSIQ_LSQ_PREFETCH
@@ -51,6 +56,8 @@ struct Tuning {
   int pc_block = 0;            // K3 workgroup size 256/512/1024 (0 = auto)
   int nontemporal = 1;         // nt hints on streamed loads/stores
   int store_defer = -1;        // deferred store phase, units of 512 clocks (-1 = auto, 0 = off)
+  int obs_kernel = 0;          // K2: 0 auto (grid-stride), 1 one-shot, 2 grid-stride
+  int obs_grid = 0;            // K2 grid-stride workgroups (0 = kObsGrid)
 };
 extern Tuning g_tune;
 
@@ -658,14 +665,34 @@ __device__ __forceinline__ double partial_load(const double *p) {
 }
 
 // Call after thread 0 has partial_store()d its record; returns true (block-uniform)
-// in the last workgroup to arrive.
+// in the last workgroup to arrive.  Arrivals on one address serialize at the memory
+// side (~10 ns each: +5 us per 512 workgroups, measured on K2), so grids above
+// kArriveFlat arrive in two levels: workgroup b bumps group counter 1 + b % G, the
+// group's last arrival resets it and bumps counter[0]; the last of the G group-lasts
+// is the last workgroup.  counter: VSIQ_COUNTER_WORDS words, counter[0] is reset by
+// the caller's epilogue.
 __device__ __forceinline__ bool arrive_last(uint32_t *counter) {
   __shared__ int s_last;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == gridDim.x - 1);
+    const uint32_t nb = gridDim.x;
+    int last;
+    if (nb <= (uint32_t)kArriveFlat) {
+      const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (t == nb - 1);
+    } else {
+      const uint32_t g = blockIdx.x % kArriveGroups;
+      const uint32_t members = (nb - g + kArriveGroups - 1) / kArriveGroups;
+      const uint32_t t =
+          __hip_atomic_fetch_add(counter + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = 0;
+      if (t == members - 1) {
+        __hip_atomic_store(counter + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t0 =
+            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t0 == (uint32_t)kArriveGroups - 1);
+      }
+    }
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
