@@ -44,6 +44,9 @@ def parse():
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                   help="experiments: vsiq_set_tuning(KEY, VALUE) before the workload is built "
+                        "(keys: include/vsiq.h VSIQ_TUNE_*)")
     return p.parse_args()
 
 
@@ -442,6 +445,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
+    from vsiquantization_amd import _hip as H
+    for kv in a.tune:
+        k, v = kv.split("=")
+        H.set_tuning(int(k), int(v))
 
     if a.workload == "c4":
         W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch)
@@ -526,6 +533,8 @@ def main():
                              parallelism=f"dp x{world} (128 images per GPU per batch; deferred "
                                          "observer sync: 2 all-reduces per calibration run)",
                              note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
+    if a.tune:
+        out["config"]["tuning"] = a.tune
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
     if rank == 0:

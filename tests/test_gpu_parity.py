@@ -293,16 +293,44 @@ def test_lsq_c3_full_size(sym):
         assert float(zp.grad) == pytest.approx(gzo, rel=1e-9)
 
 
-@pytest.mark.parametrize("n", [1, 4099, 295_000, 3_276_800, 13_107_200])
-def test_lsq_groups_per_lane_sizes(n):
-    """K4 picks 2 / 4 / 16 groups per lane by tensor size (grid >= 2048 workgroups):
-    every variant bitwise on grad_x, f64 scale gradient vs the closed form."""
+@pytest.mark.parametrize("groups", [0, 2, 4, 16])
+@pytest.mark.parametrize("n", [1, 4099, 295_000, 525_000, 3_276_800, 13_107_200])
+def test_lsq_groups_per_lane_sizes(n, groups):
+    """K4 at 2 / 4 / 16 groups per lane (VSIQ_TUNE_LSQ_GROUPS; 0 = default 4), grids from 1
+    to >12k workgroups (flat and two-level partial folds): grad_x bitwise, f64 scale
+    gradient vs the oracle's closed form."""
     x = _rand(n, n % 97, 0.5)
     g = _rand(n, n % 89 + 1)
-    gx, grads = FQ.lsq_backward(cu(g), cu(x), 0.01, 0, -8, 7, 0.37, False)
+    H.set_tuning(H.TUNE_LSQ_GROUPS, groups)
+    try:
+        gx, grads = FQ.lsq_backward(cu(g), cu(x), 0.01, 0, -8, 7, 0.37, False)
+    finally:
+        H.set_tuning(H.TUNE_LSQ_GROUPS, 0)
     _, gxo, gso, _ = O.lsq_forward_backward(x, g, 0.01, 0, -8, 7, 0.37)
     G.assert_bitwise_f32(npy(gx), gxo, "grad_x")
     assert float(grads[0]) == pytest.approx(gso, rel=1e-9, abs=1e-12)
+
+
+@pytest.mark.parametrize("obs_kernel", [1, 2])
+@pytest.mark.parametrize("n", [1, 4099, 525_000, 3_276_800, 13_107_200])
+def test_observer_kernels_sizes(n, obs_kernel):
+    """K2 one-shot (flat and two-level folds) and grid-stride forms against the oracle."""
+    x = _rand(n, n % 61 + 3, 0.7)
+    H.set_tuning(H.TUNE_OBS_KERNEL, obs_kernel)
+    try:
+        qp, st = FQ.observe_tensor(cu(x), symmetric=False)
+    finally:
+        H.set_tuning(H.TUNE_OBS_KERNEL, 0)
+    mn, mx = O.observe_minmax(x)
+    st = npy(st)
+    assert (st[H.ST_MIN], st[H.ST_MAX]) == (float(x.min()), float(x.max()))
+    x64 = x.astype(np.float64)   # sums: f64 over fp32 partials of 4 elements (<= 1e-6)
+    assert st[H.ST_SUMABS] == pytest.approx(np.abs(x64).sum(), rel=1e-6)
+    assert st[H.ST_SUM] == pytest.approx(x64.sum(), rel=1e-6, abs=1e-6 * np.abs(x64).sum())
+    assert st[H.ST_SUMSQ] == pytest.approx((x64 * x64).sum(), rel=1e-6)
+    scale, zp = O.minmax_qparams(mn, mx, False)
+    q = npy(qp)
+    assert (q[H.QP_SCALE], q[H.QP_ZP]) == (scale, zp)
 
 
 def test_reductions_deterministic():

@@ -234,3 +234,32 @@ extern "C" int exp_wallclock_khz() {
   hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, 0);
   return v;
 }
+
+// ---- 2-read / 1-write streaming ceiling (x, g -> x*g), one-shot U groups per lane
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_tri(const float *__restrict__ x, const float *__restrict__ g,
+                                                float *__restrict__ y, int64_t n) {
+  const int64_t ng = n / 4;
+  const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+  f4 a[U], b[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kBlock;
+    a[u] = ld4<true>(x + 4 * (i < ng ? i : ng - 1));
+    b[u] = ld4<true>(g + 4 * (i < ng ? i : ng - 1));
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * kBlock;
+    if (i < ng) st4<true>(y + 4 * i, a[u] * b[u]);
+  }
+}
+
+extern "C" int exp_tri(const float *x, const float *g, float *y, int64_t n, int u, void *st) {
+  auto s = (hipStream_t)st;
+  const int64_t ng = n / 4;
+#define TRI(U) if (u == U) { hipLaunchKernelGGL((k_tri<U>), dim3((unsigned)cdiv(ng, (int64_t)kBlock * U)), dim3(kBlock), 0, s, x, g, y, n); return (int)hipGetLastError(); }
+  TRI(1) TRI(2) TRI(4) TRI(8) TRI(16)
+#undef TRI
+  return 1;
+}

@@ -71,8 +71,25 @@ __device__ __forceinline__ void obs_block_reduce(ObsAcc &a) {
   __syncthreads();
 }
 
-// Block partial -> workspace record; the last block to arrive folds all records in a
-// fixed order, writes the stats record and applies the running update.
+struct ObsFold {   // partial record {min, max, nan count, sum|x|, sum x, sum x^2}
+  static constexpr int K = 6;
+  __device__ static void init(double (&a)[6]) {
+    a[0] = __builtin_inf(); a[1] = -__builtin_inf();
+    a[2] = a[3] = a[4] = a[5] = 0.0;
+  }
+  __device__ static void add(double (&a)[6], const double (&r)[6]) {
+    a[0] = __builtin_fmin(a[0], r[0]); a[1] = __builtin_fmax(a[1], r[1]);
+    a[2] += r[2]; a[3] += r[3]; a[4] += r[4]; a[5] += r[5];
+  }
+  __device__ static void wave(double (&a)[6]) {
+    a[0] = wave_reduce(a[0], MinD()); a[1] = wave_reduce(a[1], MaxD());
+#pragma unroll
+    for (int k = 2; k < 6; ++k) a[k] = wave_reduce(a[k], AddD());
+  }
+};
+
+// Block partial -> workspace record; the workgroup holding the fold of every record
+// writes the stats record and applies the running update.
 __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *__restrict__ stats_out,
                                                  float *__restrict__ run_minmax,
                                                  double *__restrict__ qp_out, int sym, double qden,
@@ -84,26 +101,12 @@ __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *_
     partial_store(r + 0, a.mn); partial_store(r + 1, a.mx); partial_store(r + 2, (double)a.nan);
     partial_store(r + 3, a.sa); partial_store(r + 4, a.s1); partial_store(r + 5, a.s2);
   }
-  if (!arrive_last(counter)) return;
-
-  // ---- epilogue in the last block: fixed-order combine of the partials ----
-  obs_init(a);
-  double nanc = 0.0;
-  fold_partials<6>(ws, (int)gridDim.x, [&](const double (&r)[6]) {
-    a.mn = fminf(a.mn, (float)r[0]);
-    a.mx = fmaxf(a.mx, (float)r[1]);
-    nanc += r[2];
-    a.sa += r[3]; a.s1 += r[4]; a.s2 += r[5];
-  });
-  {
-    __shared__ double s_nanc[kWaves];
-    nanc = wave_reduce(nanc, AddD());
-    if (threadIdx.x % kWave == 0) s_nanc[threadIdx.x / kWave] = nanc;
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int i = 1; i < kWaves; ++i) nanc += s_nanc[i];
-  }
-  obs_block_reduce(a);
+  double f[6];
+  if (!fold_arrivals<ObsFold>(ws, counter, f)) return;
+  a.mn = (float)f[0];
+  a.mx = (float)f[1];
+  const double nanc = f[2];
+  a.sa = f[3]; a.s1 = f[4]; a.s2 = f[5];
   if (threadIdx.x == 0) {
     const double dn = (double)n;
     const bool has_nan = nanc > 0.0;
@@ -324,7 +327,7 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   const bool vec = aligned16(x) && n % 4 == 0;
   const int64_t grid = observe_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
-  if (ws_len < grid * kPartials) return VSIQ_E_WS;
+  if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
   VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
            symmetric, qden, eps, ws, counter, (hipStream_t)stream);
   return launch_rc();
@@ -363,7 +366,7 @@ const char *vsiq_error_string(int code) {
 
 int64_t vsiq_workspace_doubles(int64_t n) {
   const int64_t g = std::max<int64_t>(kMaxReduceGrid, lsq_grid(cdiv(std::max<int64_t>(n, 0), 4)));
-  return g * kPartials;
+  return (g + kArriveGroups) * kPartials;
 }
 
 int64_t vsiq_mask_words(int64_t rows, int64_t rowlen) {
@@ -382,6 +385,10 @@ int vsiq_set_tuning(int key, int value) {
     case VSIQ_TUNE_OBS_GRID:
       if (value != 0 && (value < 1 || value > kMaxReduceGrid)) return VSIQ_E_ARG;
       g_tune.obs_grid = value;
+      return 0;
+    case VSIQ_TUNE_LSQ_GROUPS:
+      if (value != 0 && value != 2 && value != 4 && value != 16) return VSIQ_E_ARG;
+      g_tune.lsq_groups = value;
       return 0;
     case VSIQ_TUNE_STORE_DEFER:
       if (value < -1 || value > 64) return VSIQ_E_ARG;

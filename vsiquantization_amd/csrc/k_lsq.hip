@@ -23,7 +23,10 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
   const float t1 = g * (q - p.z);           // MulBackward0 (other)
   const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
   const float t2 = (-gm) * xs;              // DivBackward0 (other)
-  if (valid) {
+#ifndef VSIQ_EXP_K4
+#define VSIQ_EXP_K4 0
+#endif
+  if ((VSIQ_EXP_K4 & 1) == 0 && valid) {
     acc.t += (double)t1 + (double)t2;
     if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
   }
@@ -38,6 +41,16 @@ __device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
   const float gm = m ? g * p.s : 0.0f;
   return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
 }
+
+struct LsqFold {   // partial record {sum t, sum z}
+  static constexpr int K = 2;
+  __device__ static void init(double (&a)[2]) { a[0] = a[1] = 0.0; }
+  __device__ static void add(double (&a)[2], const double (&r)[2]) { a[0] += r[0]; a[1] += r[1]; }
+  __device__ static void wave(double (&a)[2]) {
+    a[0] = wave_reduce(a[0], AddD());
+    a[1] = wave_reduce(a[1], AddD());
+  }
+};
 
 __device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
   __shared__ double s[2][kWaves];
@@ -58,8 +71,8 @@ __device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int6
                                           const QP &p, LsqAcc &c) {
   const f4 xv = act_fwd4<ACT>(xc);
   const int nv = i < ng ? valid_in_group(i, n) : 0;
-  const uint32_t ok = lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
-                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p);
+  const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
+                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p));
   f4 o;
   if (ok) {
     o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
@@ -110,13 +123,9 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
     partial_store(r + 0, c.t);
     partial_store(r + 1, c.z);
   }
-  if (!arrive_last(counter)) return;
-  c = LsqAcc{0.0, 0.0};
-  fold_partials<2>(ws, (int)gridDim.x, [&](const double (&r)[2]) {
-    c.t += r[0];
-    c.z += r[1];
-  });
-  lsq_block_reduce(c);
+  double f[2];
+  if (!fold_arrivals<LsqFold>(ws, counter, f)) return;
+  c = LsqAcc{f[0], f[1]};
   if (threadIdx.x == 0) {
     grad_out[0] = c.t * gscale;
     double gz = 0.0;
@@ -178,7 +187,7 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
   const int64_t grid = lsq_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
-  if (ws_len < (int64_t)grid * kPartials) return VSIQ_E_WS;
+  if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
   // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
   const bool nt = g_tune.nontemporal != 0;

@@ -46,7 +46,6 @@ constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workg
 #define VSIQ_LSQ_PREFETCH 2
 #endif
 constexpr int kLsqPrefetch = VSIQ_LSQ_PREFETCH;   // K4 groups in flight ahead of the one computing
-constexpr int kLsqMinGrid = 64;        // K4: shrink groups per lane only below this grid
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -58,6 +57,7 @@ struct Tuning {
   int store_defer = -1;        // deferred store phase, units of 512 clocks (-1 = auto, 0 = off)
   int obs_kernel = 0;          // K2: 0 auto (grid-stride), 1 one-shot, 2 grid-stride
   int obs_grid = 0;            // K2 grid-stride workgroups (0 = kObsGrid)
+  int lsq_groups = 0;          // K4 groups per lane 2 / 4 / 16 (0 = by size)
 };
 extern Tuning g_tune;
 
@@ -637,6 +637,14 @@ struct MaxOp {
   static __device__ float identity() { return -__builtin_inff(); }
   __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
 };
+struct MinD {
+  static __device__ double identity() { return __builtin_inf(); }
+  __device__ double operator()(double a, double b) const { return __builtin_fmin(a, b); }
+};
+struct MaxD {
+  static __device__ double identity() { return -__builtin_inf(); }
+  __device__ double operator()(double a, double b) const { return __builtin_fmax(a, b); }
+};
 struct AddD {
   static __device__ double identity() { return 0.0; }
   __device__ double operator()(double a, double b) const { return a + b; }
@@ -723,6 +731,96 @@ __device__ __forceinline__ void fold_partials(const double *ws, int nrec, F &&f)
   }
 }
 
+// ----------------------------------------------------------------------------
+// Two-level fold of per-workgroup partial records (K doubles each, record b at
+// ws + b * kPartials, stored by thread 0 with partial_store).  Op supplies
+//   static constexpr int K;  init(double (&)[K]);  add(double (&)[K], const double (&)[K]);
+//   wave(double (&)[K])  (wave_reduce of every field, any lane holds the result).
+// Grids up to kArriveFlat: the last workgroup folds every record.  Larger grids:
+// workgroup b belongs to group b % G; the group's last arrival folds the group's
+// records (b = g, g + G, ...) into group record nb + g, and the last of the G group
+// folds combines those.  Fixed assignment and trees: deterministic for a given grid.
+// The workspace needs nb + kArriveGroups records (vsiq_workspace_doubles).
+// ----------------------------------------------------------------------------
+template <typename Op>
+__device__ __forceinline__ void fold_block(const double *ws, uint32_t first, uint32_t count, uint32_t stride,
+                                           double (&a)[Op::K]) {
+  constexpr int K = Op::K;
+  Op::init(a);
+  for (uint32_t j0 = threadIdx.x; j0 < count; j0 += 4 * kBlock) {
+    double r[4][K];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t j = j0 + u * kBlock < count ? j0 + u * kBlock : count - 1;
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[u][k] = partial_load(ws + (int64_t)(first + j * stride) * kPartials + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j0 + u * kBlock < count) Op::add(a, r[u]);
+  }
+  __shared__ double s_w[kWaves][K];
+  Op::wave(a);
+  if (threadIdx.x % kWave == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) s_w[threadIdx.x / kWave][k] = a[k];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < kWaves; ++w) {
+      double r[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[k] = s_w[w][k];
+      Op::add(a, r);
+    }
+  __syncthreads();
+}
+
+// Returns true (block-uniform) in the workgroup that holds the fold of every record,
+// in thread 0's `a`; counter: VSIQ_COUNTER_WORDS words, counter[0] reset by the caller.
+template <typename Op>
+__device__ __forceinline__ bool fold_arrivals(double *ws, uint32_t *counter, double (&a)[Op::K]) {
+  const uint32_t nb = gridDim.x;
+  if (nb <= (uint32_t)kArriveFlat) {
+    if (!arrive_last(counter)) return false;
+    fold_block<Op>(ws, 0, nb, 1, a);
+    return true;
+  }
+  __shared__ int s_role;
+  const uint32_t g = blockIdx.x % kArriveGroups;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t members = (nb - g + kArriveGroups - 1) / kArriveGroups;
+    const uint32_t t = __hip_atomic_fetch_add(counter + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int role = (t == members - 1);
+    if (role) {
+      __hip_atomic_store(counter + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_role = role;
+  }
+  __syncthreads();
+  if (!s_role) return false;
+  fold_block<Op>(ws, g, (nb - g + kArriveGroups - 1) / kArriveGroups, kArriveGroups, a);
+  if (threadIdx.x == 0) {
+    double *gr = ws + (int64_t)(nb + g) * kPartials;
+#pragma unroll
+    for (int k = 0; k < Op::K; ++k) partial_store(gr + k, a[k]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t0 = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t0 == (uint32_t)kArriveGroups - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_role = last ? 2 : 0;
+  }
+  __syncthreads();
+  if (s_role != 2) return false;
+  fold_block<Op>(ws + (int64_t)nb * kPartials, 0, kArriveGroups, 1, a);
+  return true;
+}
+
 // f64 qparams from the running min/max (observers/minmax.py:49-74).
 // min_val <= 0 <= max_val always holds (state starts at 0/0, minmax.py:28-29).
 __device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, double qden,
@@ -806,16 +904,15 @@ inline int64_t oneshot_grid(int64_t groups) {
   return std::max<int64_t>(1, cdiv(groups, (int64_t)kBlock * kFlatU));
 }
 
-// K4 groups per lane for a tensor of `groups` 4-element groups.  16 amortizes each
-// workgroup's reduction epilogue (block reduce, partial record, arrival atomic) and
-// keeps a lane's loads streaming: on MI355X it beats 2 or 4 groups per lane even at
-// 3.3M elements with only 200 workgroups (23.6 us vs 27.7 us).  Only tensors too
-// small for 64 workgroups (weights, < ~1M elements) drop to 4 or 2 groups per lane,
-// where the serial 16-deep chain dominated (17 us -> 6 us for a 295K-element weight).
+// K4 groups per lane: 4.  Since the two-level fold (fold_arrivals) a workgroup's
+// epilogue no longer serializes on one counter, and 4 groups per lane stream better
+// than 16 (16-deep straight-line code) at every size measured on MI355X
+// (tools/exp/k4_sizes.py, fused ReLU: 105M elements 230 -> 216 us, 3.3M 19.1 -> 15.4,
+// 296K 16.4 -> 7.3); 2 per lane pays the epilogue twice as often (105M: 342 us).
+// Override: VSIQ_TUNE_LSQ_GROUPS (2 / 4 / 16).
 inline int lsq_groups_per_lane(int64_t groups) {
-  for (int g : {kLsqGroups, 4})
-    if (cdiv(groups, (int64_t)kBlock * g) >= kLsqMinGrid) return g;
-  return 2;
+  (void)groups;
+  return g_tune.lsq_groups > 0 ? g_tune.lsq_groups : 4;
 }
 
 inline int64_t lsq_grid(int64_t groups, int per_lane) {
@@ -824,6 +921,9 @@ inline int64_t lsq_grid(int64_t groups, int per_lane) {
 
 inline int64_t lsq_grid(int64_t groups) { return lsq_grid(groups, lsq_groups_per_lane(groups));
 }
+
+// partial records a reducing grid writes (its own + the group records of fold_arrivals)
+inline int64_t fold_records(int64_t grid) { return grid + (grid > kArriveFlat ? kArriveGroups : 0); }
 
 
 inline int launch_rc() {
