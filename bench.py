@@ -284,14 +284,15 @@ class C4Backbone:
 class C5Calibration:
     """C5: calibration of the YOLOv8n backbone's 27 activation quantizers (MinMaxObserver,
     sym) on batches of 128 images per GPU (1024 over 8 GPUs): per batch and layer one
-    observer pass over the fused ReLU of the conv output (K2-relu, 4 B/elem read), each
-    writing its per-call statistics record on the device (deferred mode, no sync); after
-    the last batch ONE deferred sync -- two RCCL all-reduces over all records of all
-    layers -- and the exact replay of every layer's running min/max (the path of
-    QuantizationManager.dist_defer + distributed.sync_calibration, here driven through the
-    C ABI so the Python manager's per-call host cost is not what is measured).  min/max are
-    bit-identical to a 1-GPU run (tests/test_dist_gloo.py).  Synthetic conv outputs stand
-    in for the conv (MIOpen, out of scope)."""
+    deferred observer pass over the fused ReLU of the conv output (K2p-relu, 4 B/elem
+    read), each writing its partial records into its own device slot (no fold, no
+    atomics, no sync); after the last batch ONE deferred sync -- one fold launch over all
+    slots of all layers and batches, two RCCL all-reduces over the records, and the exact
+    replay of every layer's running min/max (the path of calibrate_qat_model(...,
+    defer_observers=True) / QuantizationManager.dist_defer + distributed.sync_calibration,
+    here driven through the C ABI so the Python manager's per-call host cost is not what
+    is measured).  min/max are bit-identical to a 1-GPU run (tests/test_dist_gloo.py).
+    Synthetic conv outputs stand in for the conv (MIOpen, out of scope)."""
 
     name = "C5 YOLOv8n backbone calibration: fused-ReLU MinMax observers, deferred RCCL sync"
 
@@ -308,10 +309,10 @@ class C5Calibration:
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.steps = steps
         L = len(self.layers)
-        self.rec = torch.zeros(steps, L, H.ST_LEN, dtype=torch.float64, device=dev)
-        self.ws = H.workspace(dev, max(a.numel() for a in self.acts))
-        self.qd = qden(True, 8, 1e-8)
-        self.f = lib.vsiq_act_observe_f32
+        from vsiquantization_amd.fakequant import part_slot_doubles
+        self.stride = max(part_slot_doubles(a.numel()) for a in self.acts)
+        self.parts = torch.zeros(steps, L, self.stride, dtype=torch.float64, device=dev)
+        self.f = lib.vsiq_act_observe_part_f32
         self.ptrs = [H.ptr(a) for a in self.acts]
         self.n = sum(a.numel() for a in self.acts)
         self.slots = [None]
@@ -321,19 +322,22 @@ class C5Calibration:
     def _observe(self, step):
         H = self.H
         rc = 0
-        base = self.rec[step % self.steps]
+        base = self.parts[step % self.steps]
         for j, (p, a) in enumerate(zip(self.ptrs, self.acts)):
-            rc |= self.f(p, H.c_i64(a.numel()), H.ACT_RELU, H.ptr(base[j]), None, None, 1, self.qd, 1e-8,
-                         H.ptr(self.ws.ws), H.c_i64(self.ws.ws_len), H.ptr(self.ws.counter), self.st)
+            rc |= self.f(p, H.c_i64(a.numel()), H.ACT_RELU, H.ptr(base[j]), H.c_i64(self.stride), self.st)
         return rc
 
     def launch(self, i):
         return self._observe(i)
 
     def _sync(self, k):
-        """The deferred sync over the first k batches: all-reduce + running-state replay."""
+        """The deferred sync over the first k batches: one fold launch over every slot,
+        all-reduce, running-state replay."""
         from vsiquantization_amd.distributed import allreduce_stats, replay_minmax_tensor
-        recs = self.rec[:k].transpose(0, 1).contiguous()          # [layers, calls, ST_LEN]
+        from vsiquantization_amd.fakequant import fold_parts
+        L = len(self.layers)
+        recs = fold_parts(self.parts[:k].reshape(k * L, self.stride))
+        recs = recs.reshape(k, L, -1).transpose(0, 1).contiguous()   # [layers, calls, ST_LEN]
         if self.world > 1:
             allreduce_stats(recs)
         self.minmax = replay_minmax_tensor(0.0, 0.0, recs)         # stays on the device

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 3
+#define VSIQ_ABI_VERSION 4
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -156,6 +156,28 @@ int vsiq_observe_f32(const float *x, int64_t n, double *stats_out, float *run_mi
  */
 int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out, int symmetric,
                           double qden, double eps, void *stream);
+
+/*
+ * Deferred-calibration observer (K2p): the K2 pass over act(c) WITHOUT the
+ * cross-workgroup fold.  Replaces, like vsiq_act_observe_f32, minmax.py:42-43 +
+ * quantization_manager.py:66-68 for an observe-only call (calibrate_qat_model,
+ * utils/quantize_manager.py:4-31), whose result nothing reads until calibration ends.
+ * Writes vsiq_observe_part_records(n) partial records of VSIQ_PART_LEN doubles
+ *   {min, max, nan count, sum|x|, sum x, sum x^2, n, record count}
+ * into parts[parts_len] (no workspace, no counter, no running-state update: any
+ * number of calls may be in flight on any streams).  vsiq_observe_fold_parts then
+ * folds ncalls such slots (call_stride doubles apart, each >= the call's records)
+ * into ncalls stats records stats_out[ncalls][VSIQ_ST_LEN] in one launch; the
+ * running min/max is replayed from those records (minmax.py:42-47, NaN calls skipped).
+ * min/max/nan/n are exact; the sums differ from vsiq_act_observe_f32's only in
+ * float64 summation order.
+ */
+#define VSIQ_PART_LEN 8
+int64_t vsiq_observe_part_records(int64_t n);
+int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
+                              void *stream);
+int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride,
+                            double *stats_out, void *stream);
 
 /*
  * Per-channel fused observe + qparams + fake-quant forward (K3), axis 0 of a

@@ -57,6 +57,16 @@ def test_argument_validation_without_gpu():
                                       -128, 127, 127.0, 1e-8, null) == 0
     assert lib.vsiq_lsq_bwd_f32(null, null, null, 0, null, 1.0, null, 0.0, 0, -128, 127, 1.0, null,
                                 null, 0, null, null) == -1
+    # deferred observer (K2p): record count from n, slot size checked, no-op fold of 0 calls
+    assert lib.vsiq_observe_part_records(0) == -1
+    assert lib.vsiq_observe_part_records(1) == 1
+    assert lib.vsiq_observe_part_records(1 << 40) == 512
+    assert lib.vsiq_act_observe_part_f32(null, 16, 0, null, 0, null) == -1
+    assert lib.vsiq_act_observe_part_f32(1, 16, 0, 1, H.PART_LEN - 1, null) == -3   # slot too small
+    assert lib.vsiq_act_observe_part_f32(1, 16, 3, 1, 64, null) == -1               # bad activation
+    assert lib.vsiq_observe_fold_parts(null, 0, 8, null, null) == 0
+    assert lib.vsiq_observe_fold_parts(null, 1, 8, null, null) == -1
+    assert lib.vsiq_observe_fold_parts(1, 1, 7, 1, null) == -1                       # stride < record
 
 
 def test_tuning_keys_match_header_and_bounds():

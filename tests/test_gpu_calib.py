@@ -51,3 +51,61 @@ def test_async_observers_equal_sync():
     # the flag is restored and nothing stays pending
     assert all(not m.activation_quantizer.async_observer for m in a)
     assert all(m.activation_quantizer._side is None for m in a)
+
+
+def test_deferred_calibration_equals_sync():
+    """defer_observers (K2p partial records + one fold + replay at the end) gives the
+    reference's running min/max and qparams exactly, and its mean|x| / mean / std lists."""
+    a = _model()
+    b = copy.deepcopy(a)
+    calibrate_qat_model(a, _loader(), data_calib, DEV, defer_observers=True)
+    calibrate_qat_model(b, _loader(), data_calib, DEV)
+    sa, sb = _state(a), _state(b)
+    for x, y in zip(sa, sb):
+        assert (x[0], x[1]) == (y[0], y[1])
+        for i in (2, 3, 4):
+            np.testing.assert_allclose(x[i], y[i], rtol=1e-6, atol=0)
+    for ma, mb in zip(a, b):
+        for qa, qb in ((ma.weight_quantizer, mb.weight_quantizer),
+                       (ma.activation_quantizer, mb.activation_quantizer)):
+            assert float(qa.scale) == float(qb.scale)
+            assert float(qa.zero_point) == float(qb.zero_point)
+            assert not qa.dist_defer and not qa._pending_records
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+@pytest.mark.parametrize("n", [1, 7, 4096, 1000003, 3 * 2**20 + 5, 13107200])
+def test_observe_parts_fold_equals_k2(n, act):
+    """K2p slots folded in one launch == the K2 per-call stats record: min/max/nan/n
+    exact, sums to float64 reordering."""
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd import fakequant as FQ
+    g = torch.Generator(device=DEV).manual_seed(n)
+    xs = [torch.randn(n, device=DEV, generator=g) * 3 for _ in range(3)]
+    xs[1][n // 2] = float("nan")
+    xs.append(torch.randn(n + 1, device=DEV, generator=g)[1:])   # misaligned view
+    stride = FQ.part_slot_doubles(1 << 62)
+    slots = torch.full((len(xs), stride), float("nan"), dtype=torch.float64, device=DEV)
+    for i, x in enumerate(xs):
+        FQ.observe_parts(x, out=slots[i], act=act)
+    got = FQ.fold_parts(slots).cpu()
+    for i, x in enumerate(xs):
+        _, st = FQ.observe_tensor(x, symmetric=True, want_qp=False, act=act)
+        want = st.cpu()
+        exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
+        assert torch.equal(got[i, exact], want[exact]), (i, got[i], want)
+        np.testing.assert_allclose(got[i, H.ST_SUMABS:H.ST_SUMSQ + 1].numpy(),
+                                   want[H.ST_SUMABS:H.ST_SUMSQ + 1].numpy(), rtol=1e-12, atol=1e-300)
+        np.testing.assert_allclose(got[i, H.ST_MEANABS:].numpy(), want[H.ST_MEANABS:].numpy(),
+                                   rtol=1e-6, equal_nan=True)
+
+
+def test_fold_parts_unwritten_slot_folds_nothing():
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd import fakequant as FQ
+    stride = FQ.part_slot_doubles(1 << 62)
+    slots = torch.zeros(2, stride, dtype=torch.float64, device=DEV)
+    slots[1, 7] = 1e30   # garbage record count: ignored, never read out of range
+    st = FQ.fold_parts(slots).cpu()
+    assert torch.all(st[:, H.ST_N] == 0)
+    assert torch.all(torch.isinf(st[:, H.ST_MIN])) and torch.all(st[:, H.ST_MIN] > 0)

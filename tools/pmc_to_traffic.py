@@ -20,7 +20,7 @@ KERNEL_KEYS = {
     # C4: per step 27 weight + 27 fused-ReLU activation launches each way
     "c4": {"k_fq_fwd<": ("fwd_all_layers", 54), "k_lsq_bwd<": ("bwd_all_layers", 54)},
     # C5: 27 fused-ReLU observer launches per calibration batch
-    "c5": {"k_observe<": ("observe_all_layers", 27)},
+    "c5": {"k_observe_part<": ("observe_all_layers", 27)},
 }
 
 

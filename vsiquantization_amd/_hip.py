@@ -25,12 +25,13 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
 ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)
 ST_LEN = 10
+PART_LEN = 8   # VSIQ_PART_LEN: doubles per K2p partial record
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6
@@ -76,6 +77,9 @@ _SIGS = {
                              c_int, c_int, c_p], c_int),
     "vsiq_act_observe_f32": ([c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p],
                              c_int),
+    "vsiq_observe_part_records": ([c_i64], c_i64),
+    "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
+    "vsiq_observe_fold_parts": ([c_p, c_i64, c_i64, c_p, c_p], c_int),
     "vsiq_act_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_i64, c_d, c_p], c_int),
     "vsiq_act_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d,
                               c_p, c_p, c_i64, c_p, c_p], c_int),

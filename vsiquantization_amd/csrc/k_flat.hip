@@ -88,6 +88,27 @@ struct ObsFold {   // partial record {min, max, nan count, sum|x|, sum x, sum x^
   }
 };
 
+// The stats record (VSIQ_ST_*) of one call from its folded {min, max, nan count,
+// sum|x|, sum x, sum x^2}: quantization_manager.py:66-68's fp32 mean(|x|) / mean /
+// unbiased std, NaN when the call held a NaN (torch's fp32 reductions are NaN then).
+__device__ __forceinline__ void write_stats(double *__restrict__ st, const double (&f)[6], int64_t n) {
+  const double dn = (double)n;
+  const bool has_nan = f[2] > 0.0;
+  st[VSIQ_ST_MIN] = (double)(float)f[0];   // NaN-ignoring; see VSIQ_ST_NAN
+  st[VSIQ_ST_MAX] = (double)(float)f[1];
+  st[VSIQ_ST_NAN] = f[2];
+  st[VSIQ_ST_SUMABS] = f[3];
+  st[VSIQ_ST_SUM] = f[4];
+  st[VSIQ_ST_SUMSQ] = f[5];
+  st[VSIQ_ST_N] = dn;
+  const double mean = f[4] / dn;
+  const double var = (f[5] - f[4] * mean) / (dn - 1.0);
+  st[VSIQ_ST_MEANABS] = has_nan ? __builtin_nan("") : (double)(float)(f[3] / dn);
+  st[VSIQ_ST_MEAN] = has_nan ? __builtin_nan("") : (double)(float)mean;
+  st[VSIQ_ST_STD] = (has_nan || n < 2) ? __builtin_nan("")
+                                       : (double)(float)__builtin_sqrt(var > 0.0 ? var : 0.0);
+}
+
 // Block partial -> workspace record; the workgroup holding the fold of every record
 // writes the stats record and applies the running update.
 __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *__restrict__ stats_out,
@@ -103,32 +124,31 @@ __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *_
   }
   double f[6];
   if (!fold_arrivals<ObsFold>(ws, counter, f)) return;
-  a.mn = (float)f[0];
-  a.mx = (float)f[1];
-  const double nanc = f[2];
-  a.sa = f[3]; a.s1 = f[4]; a.s2 = f[5];
   if (threadIdx.x == 0) {
-    const double dn = (double)n;
-    const bool has_nan = nanc > 0.0;
-    if (stats_out) {
-      stats_out[VSIQ_ST_MIN] = (double)a.mn;   // NaN-ignoring; see VSIQ_ST_NAN
-      stats_out[VSIQ_ST_MAX] = (double)a.mx;
-      stats_out[VSIQ_ST_NAN] = nanc;
-      stats_out[VSIQ_ST_SUMABS] = a.sa;
-      stats_out[VSIQ_ST_SUM] = a.s1;
-      stats_out[VSIQ_ST_SUMSQ] = a.s2;
-      stats_out[VSIQ_ST_N] = dn;
-      // NaN inputs make torch's fp32 mean/std NaN as well
-      const double mean = a.s1 / dn;
-      const double var = (a.s2 - a.s1 * mean) / (dn - 1.0);
-      stats_out[VSIQ_ST_MEANABS] = has_nan ? __builtin_nan("") : (double)(float)(a.sa / dn);
-      stats_out[VSIQ_ST_MEAN] = has_nan ? __builtin_nan("") : (double)(float)mean;
-      stats_out[VSIQ_ST_STD] = (has_nan || n < 2)
-                                   ? __builtin_nan("")
-                                   : (double)(float)__builtin_sqrt(var > 0.0 ? var : 0.0);
-    }
-    observer_update(a.mn, a.mx, has_nan, run_minmax, qp_out, sym, qden, eps);
+    if (stats_out) write_stats(stats_out, f, n);
+    observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax, qp_out, sym, qden, eps);
     *counter = 0u;   // ready for the next stream-ordered launch
+  }
+}
+
+// Grid-stride accumulation of a fixed grid over x (U groups per lane per step): the
+// body shared by k_observe_loop and k_observe_part.
+template <bool VEC, bool NT, int ACT, int U>
+__device__ __forceinline__ void observe_stride(const float *__restrict__ x, int64_t n, ObsAcc &a) {
+  obs_init(a);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t nfull = n / 4;
+  const int64_t step = (int64_t)gridDim.x * kBlock * U;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock * U; b < ng; b += step) {
+    f4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = b + threadIdx.x + k * kBlock;
+      if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+      else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+    }
   }
 }
 
@@ -172,22 +192,62 @@ __global__ __launch_bounds__(kBlock) void k_observe_loop(const float *__restrict
                                                           double *__restrict__ ws,
                                                           uint32_t *__restrict__ counter) {
   ObsAcc a;
-  obs_init(a);
-  const int64_t ng = cdiv(n, 4);
-  const int64_t nfull = n / 4;
-  const int64_t step = (int64_t)gridDim.x * kBlock * U;
-  for (int64_t b = (int64_t)blockIdx.x * kBlock * U; b < ng; b += step) {
-    f4 v[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int64_t i = b + threadIdx.x + k * kBlock;
-      if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
-      else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
-    }
-  }
+  observe_stride<VEC, NT, ACT, U>(x, n, a);
   observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+}
+
+// K2p: the grid-stride pass of k_observe_loop WITHOUT the cross-workgroup fold.  Each
+// workgroup stores its block record {min, max, nan count, sum|x|, sum x, sum x^2, n,
+// grid} (VSIQ_PART_LEN doubles, plain stores) and exits: no arrival atomics, no
+// last-block fold, no running update.  For calibration, where nothing consumes an
+// observer's result before the calibration ends: k_observe_fold_parts folds every
+// call's records at once (deferred sync), and the running min/max is replayed there.
+template <bool VEC, bool NT, int ACT, int U>
+__global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict__ x, int64_t n,
+                                                          double *__restrict__ parts) {
+  ObsAcc a;
+  observe_stride<VEC, NT, ACT, U>(x, n, a);
+  obs_block_reduce(a);
+  if (threadIdx.x == 0) {
+    double *r = parts + (int64_t)blockIdx.x * VSIQ_PART_LEN;
+    r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan; r[3] = a.sa;
+    r[4] = a.s1; r[5] = a.s2; r[6] = (double)n; r[7] = (double)gridDim.x;
+  }
+}
+
+// Fold of deferred K2p records: workgroup c folds call c's records (call_stride doubles
+// apart; the count is the grid stored in every record) in a fixed order -> its stats
+// record (VSIQ_ST_LEN).  Deterministic; min/max exact, sums in float64.
+__global__ __launch_bounds__(kBlock) void k_observe_fold_parts(const double *__restrict__ parts,
+                                                               int64_t call_stride,
+                                                               double *__restrict__ stats_out) {
+  const double *P = parts + (int64_t)blockIdx.x * call_stride;
+  const int64_t maxrec = call_stride / VSIQ_PART_LEN;
+  const double dg = P[7], dn = P[6];
+  // a slot that was never written (or garbage) folds nothing instead of reading out of range
+  const int64_t nrec = (dg >= 1.0 && dg <= (double)maxrec) ? (int64_t)dg : 0;
+  double f[6];
+  ObsFold::init(f);
+  for (int64_t i = threadIdx.x; i < nrec; i += kBlock) {
+    const double *r = P + i * VSIQ_PART_LEN;
+    const double rr[6] = {r[0], r[1], r[2], r[3], r[4], r[5]};
+    ObsFold::add(f, rr);
+  }
+  ObsFold::wave(f);
+  __shared__ double s[kWaves][6];
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[w][k] = f[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kWaves; ++i) {
+      const double rr[6] = {s[i][0], s[i][1], s[i][2], s[i][3], s[i][4], s[i][5]};
+      ObsFold::add(f, rr);
+    }
+    write_stats(stats_out + (int64_t)blockIdx.x * VSIQ_ST_LEN, f, nrec ? (int64_t)dn : 0);
+  }
 }
 
 // Finalize from an externally reduced stats record (multi-GPU: stats all-reduced
@@ -333,6 +393,23 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   return launch_rc();
 }
 
+template <int ACT>
+void launch_observe_part(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
+                         hipStream_t st) {
+  if (vec && nt)
+    hipLaunchKernelGGL((k_observe_part<true, true, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+  else if (vec)
+    hipLaunchKernelGGL((k_observe_part<true, false, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+  else
+    hipLaunchKernelGGL((k_observe_part<false, false, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+}
+
+// K2p grid: the grid-stride rule of K2 (fixed per n)
+inline int64_t observe_part_grid(int64_t n) {
+  const int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : kObsGrid;
+  return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(cdiv(n, 4), (int64_t)kBlock * kObsU)));
+}
+
 // CU count of the current device (cached; 256 on MI355X)
 int device_cus() {
   static int cus[64] = {0};
@@ -435,6 +512,31 @@ int vsiq_act_observe_f32(const float *c, int64_t n, int act, double *stats_out, 
   if (act < kActNone || act > kActSilu) return VSIQ_E_ARG;
   return observe(c, n, act, stats_out, run_minmax, qp_out, symmetric, qden, eps, ws, ws_len, counter,
                  stream);
+}
+
+int64_t vsiq_observe_part_records(int64_t n) {
+  if (n <= 0) return VSIQ_E_ARG;
+  return observe_part_grid(n);
+}
+
+int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
+                              void *stream) {
+  if (n <= 0 || !c || !parts || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  const int64_t grid = observe_part_grid(n);
+  if (parts_len < grid * VSIQ_PART_LEN) return VSIQ_E_WS;
+  const bool vec = aligned16(c) && n % 4 == 0;
+  VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, (hipStream_t)stream);
+  return launch_rc();
+}
+
+int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride, double *stats_out,
+                            void *stream) {
+  if (ncalls < 0 || ncalls > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (ncalls == 0) return 0;
+  if (!parts || !stats_out || call_stride < VSIQ_PART_LEN) return VSIQ_E_ARG;
+  hipLaunchKernelGGL(k_observe_fold_parts, dim3((unsigned)ncalls), dim3(kBlock), 0, (hipStream_t)stream,
+                     parts, call_stride, stats_out);
+  return launch_rc();
 }
 
 int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out, int symmetric,

@@ -16,9 +16,12 @@ Two modes:
 * per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): two tiny
   all-reduces per observer call, needed when the same call also fake-quantizes
   (observe+quantize mode, §3.4);
-* deferred  (``dist_defer`` True, calibration): each rank only records its local
-  per-call statistics; ``sync_calibration(model)`` all-reduces ALL records of ALL
-  layers in two collectives and replays the running min/max per layer.
+* deferred  (``dist_defer`` True, calibration): each rank only writes its local
+  per-call partial records (K2p, no cross-workgroup fold, no atomics);
+  ``sync_calibration(model)`` folds ALL calls of ALL layers in one launch,
+  all-reduces the records in two collectives and replays the running min/max per
+  layer.  With ``dist_group`` None it is a single-GPU deferred calibration (no
+  collective).
 """
 from __future__ import annotations
 
@@ -100,15 +103,31 @@ def _deferred_managers(model):
 
 
 def sync_calibration(model, group=None):
-    """Deferred calibration sync: two all-reduces for every recorded call of every layer."""
+    """Deferred calibration sync: ONE fold launch over every recorded call of every layer
+    (K2p slots -> stats records), then -- across ranks -- two all-reduces, then the exact
+    running-state replay per layer.  ``group``: the process group of the all-reduce;
+    None = the managers' own ``dist_group`` (no collective when that is None too: a
+    single-GPU deferred calibration)."""
+    from .fakequant import fold_parts
     mgrs = list(_deferred_managers(model))
     if not mgrs:
         return 0
     for m in mgrs:
         m._join()   # records may still be in flight on an observer side stream
-    recs = [torch.stack(m._pending_records) for m in mgrs]
-    counts = [r.shape[0] for r in recs]
-    host = allreduce_stats(torch.cat(recs), group=group).cpu()
+    counts = [len(m._pending_records) for m in mgrs]
+    stats = fold_parts(torch.stack([p for m in mgrs for p in m._pending_records]))
+    if group is None:
+        groups = {id(m.dist_group): m.dist_group for m in mgrs if m.dist_group is not None}
+        if len(groups) > 1:
+            raise RuntimeError("sync_calibration: managers use different dist_group values; "
+                               "pass group= explicitly")
+        group = next(iter(groups.values()), None)
+        collective = group is not None
+    else:
+        collective = True
+    if collective:
+        stats = allreduce_stats(stats, group=group)
+    host = stats.cpu()
     for m, part in zip(mgrs, host.split(counts)):
         m._apply_synced_records(part)
     return len(mgrs)

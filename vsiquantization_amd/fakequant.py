@@ -213,6 +213,43 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     return qp, st
 
 
+def part_slot_doubles(n: int) -> int:
+    """Doubles of one deferred-observer slot for n elements (K2p records x VSIQ_PART_LEN)."""
+    r = int(H.lib().vsiq_observe_part_records(_i64(n)))
+    H.check(r if r < 0 else 0, "vsiq_observe_part_records")
+    return r * H.PART_LEN
+
+
+def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) -> torch.Tensor:
+    """Deferred observer pass (K2p): the per-workgroup partial records of act(x) into
+    ``out`` (f64, >= part_slot_doubles(numel) entries; allocated when None), no fold,
+    no running update.  Fold with ``fold_parts``."""
+    x = H.require_device_f32(x)
+    if x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    need = part_slot_doubles(x.numel())
+    if out is None:
+        out = torch.empty(need, dtype=torch.float64, device=x.device)
+    elif out.dtype != torch.float64 or out.device != x.device or not out.is_contiguous():
+        raise ValueError("observe_parts: out must be a contiguous float64 tensor on x's device")
+    rc = H.lib().vsiq_act_observe_part_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), H.ptr(out),
+                                           _i64(out.numel()), H.stream_of(x.device))
+    H.check(rc, "vsiq_act_observe_part_f32")
+    return out
+
+
+def fold_parts(parts: torch.Tensor) -> torch.Tensor:
+    """Fold deferred observer slots ``parts`` [calls, stride] (f64, one call per row) into
+    stats records f64 [calls, ST_LEN] in one launch."""
+    if parts.dim() != 2 or parts.dtype != torch.float64 or not parts.is_cuda or not parts.is_contiguous():
+        raise ValueError("fold_parts: parts must be a contiguous CUDA float64 [calls, stride] tensor")
+    st = torch.empty(parts.shape[0], H.ST_LEN, dtype=torch.float64, device=parts.device)
+    rc = H.lib().vsiq_observe_fold_parts(H.ptr(parts), _i64(parts.shape[0]), _i64(parts.shape[1]),
+                                         H.ptr(st), H.stream_of(parts.device))
+    H.check(rc, "vsiq_observe_fold_parts")
+    return st
+
+
 def observe_finalize(stats: torch.Tensor, run_minmax, *, symmetric, num_bits=8, eps=1e-8):
     """Running update + qparams from an (all-reduced) stats record; returns qp f64[QP_LEN]."""
     dev = stats.device

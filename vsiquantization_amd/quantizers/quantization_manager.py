@@ -27,7 +27,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _hip as H
-from ..fakequant import observe_finalize, observe_tensor, stats_from_row_sums
+from ..fakequant import (observe_finalize, observe_parts, observe_tensor, part_slot_doubles,
+                         stats_from_row_sums)
 from ..observers.minmax import MinMaxObserver
 from ..observers.per_channel import PerChannelMinMaxObserver
 from ..utils.registry import CLASS_REGISTRY
@@ -92,7 +93,7 @@ class QuantizationManager(nn.Module):
         # multi-GPU observer (vsiquantization_amd.distributed): process group, deferred mode
         self.dist_group = None
         self.dist_defer = False
-        self._pending_records = []   # deferred: local per-call stats records f64[ST_LEN]
+        self._pending_records = []   # deferred: per-call K2p partial-record slots (f64)
         self._calib_init = None
         # observe-only calls queued on a side stream (see _observer_stream).  Off by
         # default (then scale / zero_point are plain stream-ordered device tensors);
@@ -162,7 +163,7 @@ class QuantizationManager(nn.Module):
             rs = self.observer.observe(x, want_row_stats=True)
             self._record_stats(stats_from_row_sums(rs, x.numel()))
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
-        elif self.dist_group is not None:
+        elif self.dist_group is not None or self.dist_defer:
             self._collect_distributed(x, act)
         else:
             qp, st = self.observer.observe_device(x, act=act)
@@ -182,16 +183,19 @@ class QuantizationManager(nn.Module):
     def _collect_distributed(self, x, act=None):
         from ..distributed import allreduce_stats
         obs = self.observer
-        _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
-                               run_minmax=None, want_qp=False, want_stats=True, act=act)
         if self.dist_defer:
+            # deferred (calibration): K2p partial records only -- no fold, no running
+            # update, no collective -- until sync_calibration folds every call at once
             if self.is_quantize:
                 raise RuntimeError("deferred observer sync (dist_defer) needs is_quantize=False "
                                    "(calibration); use per-call mode to quantize while observing")
             if not self._pending_records:
                 self._calib_init = (obs.min_val, obs.max_val)
-            self._pending_records.append(st)
+            slot = torch.empty(part_slot_doubles(1 << 62), dtype=torch.float64, device=x.device)
+            self._pending_records.append(observe_parts(x, out=slot, act=act))
             return
+        _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
+                               run_minmax=None, want_qp=False, want_stats=True, act=act)
         allreduce_stats(st, group=self.dist_group)
         state = obs.device_state(x.device)
         qp = observe_finalize(st, state, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps)

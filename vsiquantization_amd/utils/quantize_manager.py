@@ -24,14 +24,21 @@ def join_observers(model):
                 qm._join()
 
 
-def calibrate_qat_model(model, dataloader, data_calib, device=None, async_observers=False):
+def calibrate_qat_model(model, dataloader, data_calib, device=None, async_observers=False,
+                        defer_observers=False):
     """Observe-only mode on every manager, eval(), then ``data_calib(model, dataloader, device)``.
 
-    MI355X option ``async_observers``: queue each observer pass on a side stream
-    (``QuantizationManager.async_observer``) so the next layers do not wait for its
-    reduction tail; all are joined before returning.  Off by default: it costs ~10 us
-    of host time per call (stream hand-off), which only pays when the model's own
-    kernels are short enough that the observers' tails are exposed."""
+    MI355X options (results identical to the default path):
+    * ``async_observers``: queue each observer pass on a side stream
+      (``QuantizationManager.async_observer``) so the next layers do not wait for its
+      reduction tail; all are joined before returning.  Costs ~10 us of host time per
+      call (stream hand-off), which only pays when the model's own kernels are short
+      enough that the observers' tails are exposed.
+    * ``defer_observers``: per-tensor observers write partial records only (K2p: no
+      cross-workgroup fold, no atomics, no running update per call) and ONE
+      ``distributed.sync_calibration`` at the end folds every call of every layer,
+      all-reduces across ranks where a manager has a ``dist_group``, and replays the
+      running min/max exactly (minmax.py:42-47)."""
     mgrs = []
     for module in model.modules():
         for qm in _managers(module):
@@ -39,15 +46,20 @@ def calibrate_qat_model(model, dataloader, data_calib, device=None, async_observ
             qm.is_learning_scale = False
             qm.is_quantize = False
             if hasattr(qm, "async_observer"):
-                mgrs.append((qm, qm.async_observer))
+                mgrs.append((qm, qm.async_observer, qm.dist_defer))
                 qm.async_observer = async_observers
+                qm.dist_defer = qm.dist_defer or defer_observers
     model.eval()
     try:
         data_calib(model, dataloader, device)
     finally:
-        for qm, prev in mgrs:
+        for qm, prev, prev_defer in mgrs:
             qm.async_observer = prev
+            qm.dist_defer = prev_defer
         join_observers(model)
+    if defer_observers:
+        from ..distributed import sync_calibration
+        sync_calibration(model)
 
 
 def activate_learning_qparam(model, layer_names=None, use_init=True, active=True):
