@@ -194,9 +194,10 @@ def yolov8n_backbone(img=320, width=(3, 16, 32, 64, 128, 256), depth=(1, 2, 2)):
 
 class C4Backbone:
     """C4: the YOLOv8n backbone's 27 ConvBnReLU quantizers at 320x320, batch 256, in the
-    learning phase: per layer the learnable weight fake quant (K1 fwd, K4 bwd) and the fused
-    ReLU + learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd).  The conv itself
-    is MIOpen and out of scope: synthetic conv outputs of the right shapes stand in for it."""
+    learning phase: the 27 learnable weight fake quants as one multi-tensor launch each way
+    (k_multi.hip, the path of enable_multi_tensor_weights) and per layer the fused ReLU +
+    learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd).  The conv itself is
+    MIOpen and out of scope: synthetic conv outputs of the right shapes stand in for it."""
 
     name = "C4 YOLOv8n backbone ConvBnReLU fake-quant (weights + fused ReLU/act), learnable"
 
@@ -212,6 +213,7 @@ class C4Backbone:
         self.bits = (bits_w, bits_a)
         gen = torch.Generator(device=dev).manual_seed(seed_base)
         self.fwd, self.bwd, self.keep = [], [], []
+        wdesc = []
         n_act = n_w = 0
         for cin, cout, k, s_, h in self.layers:
             w = torch.randn(cout, cin, k, k, device=dev, generator=gen) * (2.0 / (cin * k * k)) ** 0.5
@@ -224,27 +226,38 @@ class C4Backbone:
                      sa=torch.tensor(2 * 0.8 / (qa[1] ** 0.5), dtype=torch.float64, device=dev),
                      grads_w=torch.empty(2, dtype=torch.float64, device=dev),
                      grads_a=torch.empty(2, dtype=torch.float64, device=dev))
-            t["ws_w"] = torch.empty(lib.vsiq_workspace_doubles(w.numel()), dtype=torch.float64, device=dev)
             t["ws_a"] = torch.empty(lib.vsiq_workspace_doubles(c.numel()), dtype=torch.float64, device=dev)
-            t["cnt_w"] = torch.zeros(1, dtype=torch.int32, device=dev)
-            t["cnt_a"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            t["cnt_a"] = torch.zeros(H.COUNTER_WORDS, dtype=torch.int32, device=dev)
             P = {kk: H.ptr(v) for kk, v in t.items()}
             nw, na = w.numel(), c.numel()
             gsw, gsa = (qw[1] * nw) ** -0.5, (qa[1] * na) ** -0.5
-            self.fwd.append((lib.vsiq_fq_fwd_f32, (P["w"], P["wq"], None, None, H.c_i64(nw), None, P["sw"],
-                                                   0.0, None, 0.0, 0, 0, qw[0], qw[1], st)))
             self.fwd.append((lib.vsiq_act_fq_fwd_f32, (P["c"], P["y"], None, None, H.c_i64(na), H.ACT_RELU,
                                                        None, P["sa"], 0.0, None, 0.0, 0, 0, qa[0], qa[1], st)))
             self.bwd.append((lib.vsiq_act_lsq_bwd_f32, (P["g"], P["c"], P["gc"], H.c_i64(na), H.ACT_RELU,
                                                         P["sa"], 0.0, None, 0.0, 0, qa[0], qa[1], gsa,
                                                         P["grads_a"], P["ws_a"], H.c_i64(t["ws_a"].numel()),
                                                         P["cnt_a"], st)))
-            self.bwd.append((lib.vsiq_lsq_bwd_f32, (P["gw"], P["w"], P["gwx"], H.c_i64(nw), P["sw"], 0.0,
-                                                    None, 0.0, 0, qw[0], qw[1], gsw, P["grads_w"], P["ws_w"],
-                                                    H.c_i64(t["ws_w"].numel()), P["cnt_w"], st)))
+            wdesc.append(dict(x=w.data_ptr(), y=t["wq"].data_ptr(), g=gw.data_ptr(), gx=t["gwx"].data_ptr(),
+                              scale_dev=t["sw"].data_ptr(), grad_out=t["grads_w"].data_ptr(), n=nw,
+                              gscale=gsw, qmin=qw[0], qmax=qw[1]))
             self.keep.append(t)
             n_act += na
             n_w += nw
+        # the 27 weight quantizers: ONE multi-tensor launch each way (quantizers/foreach.py,
+        # enable_multi_tensor_weights): all weight fake quants before the first conv, all
+        # weight backwards once autograd has every weight gradient
+        import ctypes
+        self.wdesc = (H.LsqTensor * len(wdesc))()
+        for i, d in enumerate(wdesc):
+            for k, v in d.items():
+                setattr(self.wdesc[i], k, v)
+        wp = ctypes.cast(self.wdesc, ctypes.c_void_p)
+        need = int(lib.vsiq_lsq_multi_workspace_doubles(wp, len(wdesc)))
+        self.ws_w = torch.empty(max(need, 1), dtype=torch.float64, device=dev)
+        self.cnt_w = torch.zeros(H.COUNTER_WORDS, dtype=torch.int32, device=dev)
+        self.fwd.insert(0, (lib.vsiq_lsq_fwd_multi_f32, (wp, len(wdesc), st)))
+        self.bwd.append((lib.vsiq_lsq_bwd_multi_f32, (wp, len(wdesc), H.ptr(self.ws_w), H.c_i64(self.ws_w.numel()),
+                                                      H.ptr(self.cnt_w), st)))
         self.n = n_act + n_w
         self.n_act, self.n_w = n_act, n_w
         self.slots = [None]

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 4
+#define VSIQ_ABI_VERSION 5
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -231,6 +231,44 @@ int vsiq_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n,
                      double zp_host, int zp_learn, int qmin, int qmax, double gscale,
                      double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
                      void *stream);
+
+/*
+ * Multi-tensor ("foreach") learnable fake quant: `count` independent per-tensor
+ * LSQ quantizers -- typically the weight quantizer of every fused layer of a model
+ * (quantizers/fake_quantize.py:62-63 -> uniform.py:47-56, once per layer and
+ * forward in the reference) -- in one forward and one backward launch (up to 32
+ * tensors per launch; larger counts are split).  Each tensor's results are
+ * bit-identical to vsiq_fq_fwd_f32(x, y, ..., scale_dev, scale_host, zp_dev,
+ * zp_host, zp_round = zp_learn) and vsiq_lsq_bwd_f32 on that tensor alone
+ * (same element math, blocks and fold order).  The descriptor array is HOST
+ * memory; the library copies it into the launch arguments.
+ *   forward : y = fq(x), reads x, scale_dev/zp_dev (g, gx, grad_out unused)
+ *   backward: gx, grad_out[2] = {grad_scale, grad_zp} from g and x
+ * ws / counter as for vsiq_lsq_bwd_f32, ws >= vsiq_lsq_multi_workspace_doubles()
+ * doubles; a tensor above 2^19 elements is handed to the single-tensor kernel
+ * within the same call.
+ */
+typedef struct vsiq_lsq_tensor {
+  const float *x;           /* quantizer input (e.g. a conv weight), n floats */
+  float *y;                 /* forward output */
+  const float *g;           /* backward: dL/dy */
+  float *gx;                /* backward: dL/dx */
+  const double *scale_dev;  /* f64 learnable scale (NULL: scale_host) */
+  const double *zp_dev;     /* f64 zero point (NULL: zp_host) */
+  double *grad_out;         /* backward: f64[2] {grad_scale, grad_zp}, overwritten */
+  int64_t n;
+  double scale_host;
+  double zp_host;
+  double gscale;            /* ScaleGradient factor (uniform.py:48, 58-71) */
+  int32_t qmin;
+  int32_t qmax;
+  int32_t zp_learn;         /* learnable zp: clamp(rint(zp)) in the forward, grad_zp */
+  int32_t reserved;
+} vsiq_lsq_tensor;
+int64_t vsiq_lsq_multi_workspace_doubles(const vsiq_lsq_tensor *tensors, int count);
+int vsiq_lsq_fwd_multi_f32(const vsiq_lsq_tensor *tensors, int count, void *stream);
+int vsiq_lsq_bwd_multi_f32(const vsiq_lsq_tensor *tensors, int count, double *ws, int64_t ws_len,
+                           uint32_t *counter, void *stream);
 
 /*
  * Fused activation + activation fake-quant (K5).  Replaces, in the fused layers,

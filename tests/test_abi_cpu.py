@@ -67,6 +67,21 @@ def test_argument_validation_without_gpu():
     assert lib.vsiq_observe_fold_parts(null, 0, 8, null, null) == 0
     assert lib.vsiq_observe_fold_parts(null, 1, 8, null, null) == -1
     assert lib.vsiq_observe_fold_parts(1, 1, 7, 1, null) == -1                       # stride < record
+    # multi-tensor learnable launches: host-side descriptor checks, nothing launched
+    import ctypes
+    assert ctypes.sizeof(H.LsqTensor) == 104
+    arr = (H.LsqTensor * 2)()
+    p = ctypes.cast(arr, ctypes.c_void_p)
+    assert lib.vsiq_lsq_fwd_multi_f32(p, 0, null) == 0
+    assert lib.vsiq_lsq_fwd_multi_f32(p, -1, null) == -1
+    assert lib.vsiq_lsq_fwd_multi_f32(p, 2, null) == -1           # n == 0 / null pointers
+    arr[0].x, arr[0].y, arr[0].n, arr[0].qmin, arr[0].qmax = 16, 16, 8, 1, 0
+    assert lib.vsiq_lsq_fwd_multi_f32(p, 1, null) == -1           # qmin > qmax
+    arr[0].qmin, arr[0].qmax = -2, 1
+    assert lib.vsiq_lsq_bwd_multi_f32(p, 1, null, 0, null, null) == -1   # no g / gx / grad_out / ws
+    arr[0].g, arr[0].gx, arr[0].grad_out = 16, 16, 16
+    assert lib.vsiq_lsq_multi_workspace_doubles(p, 1) == 8       # one block record
+    assert lib.vsiq_lsq_bwd_multi_f32(p, 1, 16, 7, 16, null) == -3       # workspace too small
 
 
 def test_tuning_keys_match_header_and_bounds():

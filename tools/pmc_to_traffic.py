@@ -13,29 +13,36 @@ import json
 import os
 import sys
 
-# workload -> {kernel-name fragment: (bench.py kernel label, launches of it per step)}
+# workload -> [(kernel-name fragment, bench.py kernel label, launches of it per step)];
+# a label's bytes per step = sum over its fragments of (mean per dispatch x launches)
 KERNEL_KEYS = {
-    "c2": {"k_pc_observe_fq<": ("pc_observe_fq_fwd", 1), "k_ste_bwd<": ("ste_bwd", 1)},
-    "c3": {"k_fq_fwd<": ("fq_fwd", 1), "k_lsq_bwd<": ("lsq_bwd", 1)},
-    # C4: per step 27 weight + 27 fused-ReLU activation launches each way
-    "c4": {"k_fq_fwd<": ("fwd_all_layers", 54), "k_lsq_bwd<": ("bwd_all_layers", 54)},
-    # C5: 27 fused-ReLU observer launches per calibration batch
-    "c5": {"k_observe_part<": ("observe_all_layers", 27)},
+    "c2": [("k_pc_observe_fq<", "pc_observe_fq_fwd", 1), ("k_ste_bwd<", "ste_bwd", 1)],
+    "c3": [("k_fq_fwd<", "fq_fwd", 1), ("k_lsq_bwd<", "lsq_bwd", 1)],
+    # C4: per step 27 fused-ReLU activation launches each way + ONE multi-tensor launch
+    # each way for the 27 weights
+    "c4": [("k_fq_fwd<", "fwd_all_layers", 27), ("k_lsq_fwd_multi<", "fwd_all_layers", 1),
+           ("k_lsq_bwd<", "bwd_all_layers", 27), ("k_lsq_bwd_multi<", "bwd_all_layers", 1)],
+    # C5: 27 fused-ReLU deferred observer launches per calibration batch
+    "c5": [("k_observe_part<", "observe_all_layers", 27)],
 }
 
 
 def per_kernel(d, counter, keys):
-    """Mean counter value per dispatch of each label x launches per step."""
+    """Bytes per step of each label: mean counter value per dispatch x launches per step,
+    summed over the label's kernels."""
     acc = collections.defaultdict(list)
     for f in glob.glob(f"{d}/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            for frag, (label, _) in keys.items():
+            for frag, _, _ in keys:
                 if frag in r["Kernel_Name"]:
-                    acc[label].append(float(r["Counter_Value"]))
-    per = {label: mult for _, (label, mult) in keys.items()}
-    return {k: sum(v) / len(v) * per[k] for k, v in acc.items()}
+                    acc[frag].append(float(r["Counter_Value"]))
+    out = collections.defaultdict(float)
+    for frag, label, mult in keys:
+        if acc[frag]:
+            out[label] += sum(acc[frag]) / len(acc[frag]) * mult
+    return dict(out)
 
 
 def main():

@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
@@ -80,11 +80,22 @@ _SIGS = {
     "vsiq_observe_part_records": ([c_i64], c_i64),
     "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
     "vsiq_observe_fold_parts": ([c_p, c_i64, c_i64, c_p, c_p], c_int),
+    "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
+    "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),
+    "vsiq_lsq_bwd_multi_f32": ([c_p, c_int, c_p, c_i64, c_p, c_p], c_int),
     "vsiq_act_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_i64, c_d, c_p], c_int),
     "vsiq_act_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d,
                               c_p, c_p, c_i64, c_p, c_p], c_int),
 }
 EXPORTED = tuple(_SIGS)
+
+
+class LsqTensor(ctypes.Structure):
+    """vsiq_lsq_tensor (include/vsiq.h): one tensor of a multi-tensor learnable launch."""
+    _fields_ = [("x", c_p), ("y", c_p), ("g", c_p), ("gx", c_p), ("scale_dev", c_p), ("zp_dev", c_p),
+                ("grad_out", c_p), ("n", c_i64), ("scale_host", c_d), ("zp_host", c_d), ("gscale", c_d),
+                ("qmin", ctypes.c_int32), ("qmax", ctypes.c_int32), ("zp_learn", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class VsiqError(RuntimeError):
@@ -169,7 +180,9 @@ class _Workspace:
         self.reserve(n)
 
     def reserve(self, n):
-        need = int(lib().vsiq_workspace_doubles(int(n)))
+        return self.reserve_doubles(int(lib().vsiq_workspace_doubles(int(n))))
+
+    def reserve_doubles(self, need):
         if need > self.ws_len:
             self.ws = torch.empty(need, dtype=torch.float64, device=self.device)
             self.ws_len = need

@@ -1,41 +1,17 @@
 // k_fq.hip — K1 per-tensor fake-quant forward (optionally behind a fused ReLU/SiLU,
 // K5), and its C ABI entry points.
-#include "vsiq_common.cuh"
+#include "k_body.cuh"
 
 namespace vsiq {
 
-// ----------------------------------------------------------------------------
-// K1: y = fq(act(x)), one-shot (kFlatU groups per lane, no loop: exact vmcnt)
-// ----------------------------------------------------------------------------
+// K1 kernel: one tensor, block body in k_body.cuh
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
 __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                    uint8_t *__restrict__ codes,
                                                    uint64_t *__restrict__ mask, int64_t n,
                                                    QPSrc src) {
   const QP p = load_qp(src);
-  const int64_t ng = cdiv(n, 4);
-  const int64_t base = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x;   // lanes chunk-aligned
-  f4 v[kFlatU];
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
-  GroupOut go[kFlatU];
-  uint32_t mlo = 0, mhi = 0;
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
-    go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4<ACT>(v[u]), p, base + u * kBlock, n);
-    if (MASK) mask_put(mlo, mhi, u, go[u].b);
-  }
-  const int lane = threadIdx.x % kWave;
-#pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
-    const int64_t i = base + u * kBlock;
-    if (i - lane >= ng) break;   // whole wave past the end (uniform)
-    fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[u]);
-  }
-  if (MASK && lane < 4 * kFlatU) {   // lane 4u+j: word j of slot u's chunk
-    const int64_t first = base - lane + (lane >> 2) * kBlock;
-    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
-  }
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT>(x, y, codes, mask, n, p, blockIdx.x);
 }
 
 template <int ACT, bool VEC, bool NT>

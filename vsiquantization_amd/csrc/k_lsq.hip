@@ -1,92 +1,8 @@
 // k_lsq.hip — K4 learnable (LSQ) backward: grad_x + f64 scale / zero-point gradient
 // sums (optionally through a fused ReLU/SiLU, K5), and its C ABI entry points.
-#include "vsiq_common.cuh"
+#include "k_body.cuh"
 
 namespace vsiq {
-
-// ----------------------------------------------------------------------------
-// K4: learnable (LSQ) backward, grad_x + f64 scale / zp gradient sums
-// ----------------------------------------------------------------------------
-struct LsqAcc {
-  double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
-};
-
-// one element of the learnable backward; returns grad_x, adds the f64 gradient terms
-template <bool ZPL, bool IEEE>
-__device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
-  const float u = fdiv_t<IEEE>(x, p.d);
-  const float r = __builtin_rintf(u + p.z);
-  const float q = fq_clamp(r, p.lo, p.hi);
-  const bool m = (r >= p.lo && r <= p.hi);
-  const float gq = g * p.s;                 // MulBackward0 (self)
-  const float gm = m ? gq : 0.0f;           // ClampBackward1
-  const float t1 = g * (q - p.z);           // MulBackward0 (other)
-  const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
-  const float t2 = (-gm) * xs;              // DivBackward0 (other)
-#ifndef VSIQ_EXP_K4
-#define VSIQ_EXP_K4 0
-#endif
-  if ((VSIQ_EXP_K4 & 1) == 0 && valid) {
-    acc.t += (double)t1 + (double)t2;
-    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
-  }
-  return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
-}
-
-// all three divisions of an element inside the fast-division range?
-__device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
-  const float u = fdiv_fast(x, p.d);
-  const float r = __builtin_rintf(u + p.z);
-  const bool m = (r >= p.lo && r <= p.hi);
-  const float gm = m ? g * p.s : 0.0f;
-  return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
-}
-
-struct LsqFold {   // partial record {sum t, sum z}
-  static constexpr int K = 2;
-  __device__ static void init(double (&a)[2]) { a[0] = a[1] = 0.0; }
-  __device__ static void add(double (&a)[2], const double (&r)[2]) { a[0] += r[0]; a[1] += r[1]; }
-  __device__ static void wave(double (&a)[2]) {
-    a[0] = wave_reduce(a[0], AddD());
-    a[1] = wave_reduce(a[1], AddD());
-  }
-};
-
-__device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
-  __shared__ double s[2][kWaves];
-  c.t = wave_reduce(c.t, AddD());
-  c.z = wave_reduce(c.z, AddD());
-  const int w = threadIdx.x / kWave;
-  if (threadIdx.x % kWave == 0) { s[0][w] = c.t; s[1][w] = c.z; }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int i = 1; i < kWaves; ++i) { c.t += s[0][i]; c.z += s[1][i]; }
-  __syncthreads();
-}
-
-// xc: the loaded input -- the quantizer input itself, or (ACT) the pre-activation c
-// whose act(c) the forward quantized; grad_x then goes through the act's backward
-template <bool VEC, bool NT, bool ZPL, int ACT>
-__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv,
-                                          const QP &p, LsqAcc &c) {
-  const f4 xv = act_fwd4<ACT>(xc);
-  const int nv = i < ng ? valid_in_group(i, n) : 0;
-  const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
-                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p));
-  f4 o;
-  if (ok) {
-    o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
-    o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);
-    o.z = lsq_elem<ZPL, false>(xv.z, gv.z, p, c, nv > 2);
-    o.w = lsq_elem<ZPL, false>(xv.w, gv.w, p, c, nv > 3);
-  } else {   // rare (divergent): an element outside the fast-division range
-    o.x = lsq_elem<ZPL, true>(xv.x, gv.x, p, c, nv > 0);
-    o.y = lsq_elem<ZPL, true>(xv.y, gv.y, p, c, nv > 1);
-    o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
-    o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
-  }
-  if (nv > 0) store_group<VEC, NT>(gx, i, n, act_bwd4<ACT>(o, xc));
-}
 
 template <bool VEC, bool NT, bool ZPL, int ACT, int G>
 __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
@@ -98,25 +14,8 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     uint32_t *__restrict__ counter) {
   const QP p = load_qp(src);
   LsqAcc c{0.0, 0.0};
-  const int64_t ng = cdiv(n, 4);
   (void)prefetch;
-  // G groups per lane, straight-line (fully unrolled): group k+kLsqPrefetch is loaded
-  // while group k computes, so x/g loads stay in flight and s_waitcnt counts are exact
-  const int64_t base = (int64_t)blockIdx.x * kBlock * G + threadIdx.x;
-  f4 xv[G], gv[G];
-#pragma unroll
-  for (int k = 0; k < kLsqPrefetch && k < G; ++k) {
-    xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
-    gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
-  }
-#pragma unroll
-  for (int k = 0; k < G; ++k) {
-    if (k + kLsqPrefetch < G) {
-      xv[k + kLsqPrefetch] = load_group_c<VEC, NT>(x, base + (k + kLsqPrefetch) * kBlock, ng, n);
-      gv[k + kLsqPrefetch] = load_group_c<VEC, NT>(g, base + (k + kLsqPrefetch) * kBlock, ng, n);
-    }
-    lsq_group<VEC, NT, ZPL, ACT>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
-  }
+  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, gx, n, p, blockIdx.x, c);
   lsq_block_reduce(c);
   if (threadIdx.x == 0) {
     double *r = ws + (int64_t)blockIdx.x * kPartials;
@@ -128,14 +27,7 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   c = LsqAcc{f[0], f[1]};
   if (threadIdx.x == 0) {
     grad_out[0] = c.t * gscale;
-    double gz = 0.0;
-    if (ZPL) {
-      // ClampBackward of zero_point_rounding (uniform.py:101): in-range test on round(zp)
-      const double zr = __builtin_rint(src.zdev ? *src.zdev : src.zhost);   // NaN -> not in range
-      const bool zin = zr >= (double)p.lo && zr <= (double)p.hi;
-      gz = zin ? c.z * gscale : 0.0;
-    }
-    grad_out[1] = gz;
+    grad_out[1] = ZPL ? lsq_grad_zp(c.z, src, p, gscale) : 0.0;
     *counter = 0u;
   }
 }

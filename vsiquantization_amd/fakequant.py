@@ -9,6 +9,8 @@ eager torch ops in the reference:
   per_channel_observe_fq   per-channel MinMax + UniformQuantizer (K3)
   FakeQuantFixedFn         autograd of uniform.py:55,95 with fixed qparams (STE)
   FakeQuantLearnFn         autograd of uniform.py:47-56 (LSQ: ScaleGradient, STE) (K4)
+  FakeQuantLearnMultiFn    FakeQuantLearnFn over many tensors in one launch each way
+  observe_parts/fold_parts deferred-calibration observer (K2p) and its one-launch fold
 
 Every op takes an optional ``act`` ("relu" / "silu", K5): the op is then applied
 to act(x) without materializing it -- the fused layers' F.relu / F.silu before
@@ -17,6 +19,7 @@ the backward ops return the gradient with respect to the pre-activation x.
 """
 from __future__ import annotations
 
+import ctypes
 import numbers
 
 import numpy as np
@@ -189,6 +192,103 @@ class FakeQuantLearnFn(torch.autograd.Function):
         if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
             gz = grads[1].to(device=z.device, dtype=z.dtype).reshape(z.shape)
         return gx, gs, gz, None, None, None, None, None
+
+
+# --------------------------------------------------------------------------- multi-tensor learnable
+class LsqSpec:
+    """One tensor of a multi-tensor learnable fake quant: qmin/qmax, the ScaleGradient
+    factor, whether the zero point is learned, and scale / zero point as device f64
+    tensors or host numbers (exactly the arguments of FakeQuantLearnFn)."""
+
+    __slots__ = ("scale", "zero_point", "qmin", "qmax", "gscale", "learn_zp")
+
+    def __init__(self, scale, zero_point, qmin, qmax, gscale, learn_zp):
+        self.scale, self.zero_point = scale, zero_point
+        self.qmin, self.qmax, self.gscale, self.learn_zp = int(qmin), int(qmax), float(gscale), bool(learn_zp)
+
+
+def _lsq_descs(specs, xs, ys=None, gs=None, gxs=None, grads=None):
+    """ctypes array of vsiq_lsq_tensor + the device f64 scale/zp copies it points to."""
+    arr = (H.LsqTensor * len(specs))()
+    keep = []
+    for i, (sp, x) in enumerate(zip(specs, xs)):
+        d = arr[i]
+        sd, sh = scalar_source(sp.scale, x.device)
+        zd, zh = scalar_source(sp.zero_point, x.device)
+        keep += [sd, zd]
+        d.x = x.data_ptr()
+        d.y = ys[i].data_ptr() if ys is not None else None
+        d.g = gs[i].data_ptr() if gs is not None else None
+        d.gx = gxs[i].data_ptr() if gxs is not None else None
+        d.scale_dev = sd.data_ptr() if sd is not None else None
+        d.zp_dev = zd.data_ptr() if zd is not None else None
+        d.grad_out = grads[i].data_ptr() if grads is not None else None
+        d.n, d.scale_host, d.zp_host, d.gscale = x.numel(), sh, zh, sp.gscale
+        d.qmin, d.qmax, d.zp_learn = sp.qmin, sp.qmax, int(sp.learn_zp)
+    return arr, keep
+
+
+class FakeQuantLearnMultiFn(torch.autograd.Function):
+    """FakeQuantLearnFn over many tensors at once (k_multi.hip): one forward launch and
+    one backward launch for all of them; per tensor bit-identical to FakeQuantLearnFn.
+
+    apply(specs, *xs, *scale_and_zp_tensors): the learnable tensors referenced by the
+    specs are passed again as inputs so autograd routes their gradients."""
+
+    @staticmethod
+    def forward(ctx, specs, *inputs):
+        k = len(specs)
+        xs = [H.require_device_f32(x) for x in inputs[:k]]
+        if not xs:
+            return ()
+        dev = xs[0].device
+        if any(x.device != dev for x in xs):
+            raise ValueError("multi-tensor fake quant: all tensors must be on one device")
+        ys = [torch.empty_like(x) for x in xs]
+        arr, keep = _lsq_descs(specs, xs, ys=ys)
+        H.check(H.lib().vsiq_lsq_fwd_multi_f32(ctypes.cast(arr, ctypes.c_void_p), k, H.stream_of(dev)),
+                "vsiq_lsq_fwd_multi_f32")
+        ctx.save_for_backward(*xs)
+        ctx.specs = specs
+        ctx.params = inputs[k:]
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        xs = ctx.saved_tensors
+        specs = ctx.specs
+        k = len(specs)
+        dev = xs[0].device
+        gs = [H.require_device_f32(g, "grad_output") for g in gys]
+        gxs = [torch.empty_like(x) for x in xs]
+        grads = torch.empty(k, 2, dtype=torch.float64, device=dev)
+        arr, keep = _lsq_descs(specs, xs, gs=gs, gxs=gxs, grads=grads)
+        p = ctypes.cast(arr, ctypes.c_void_p)
+        need = int(H.lib().vsiq_lsq_multi_workspace_doubles(p, k))
+        H.check(need if need < 0 else 0, "vsiq_lsq_multi_workspace_doubles")
+        w = H.workspace(dev).reserve_doubles(need)
+        rc = H.lib().vsiq_lsq_bwd_multi_f32(p, k, H.ptr(w.ws), _i64(w.ws_len), H.ptr(w.counter),
+                                            H.stream_of(dev))
+        H.check(rc, "vsiq_lsq_bwd_multi_f32")
+        # gradients of the learnable scale / zero-point tensors, in input order
+        out = []
+        j = k
+        for i, sp in enumerate(specs):
+            for col, v, learn in ((0, sp.scale, True), (1, sp.zero_point, sp.learn_zp)):
+                if isinstance(v, torch.Tensor) and v.requires_grad:
+                    g = None
+                    if learn and ctx.needs_input_grad[1 + j]:
+                        g = grads[i, col].to(device=v.device, dtype=v.dtype).reshape(v.shape)
+                    out.append(g)
+                    j += 1
+        return (None, *gxs, *out)
+
+
+def lsq_fake_quant_multi(xs, specs):
+    """Learnable fake quant of every x in ``xs`` with its LsqSpec, in one launch each way."""
+    params = [v for sp in specs for v in (sp.scale, sp.zero_point)
+              if isinstance(v, torch.Tensor) and v.requires_grad]
+    return FakeQuantLearnMultiFn.apply(tuple(specs), *xs, *params)
 
 
 # --------------------------------------------------------------------------- observer (K2)

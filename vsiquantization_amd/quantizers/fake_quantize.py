@@ -43,6 +43,11 @@ class FakeQuantize(nn.Module):
         return conv.weight, conv.bias
 
     def quantize_weights(self, weights):
+        # a result precomputed by a multi-tensor launch (quantizers/foreach.py) for exactly
+        # this weight tensor is used once; anything else takes the per-layer path
+        stash = self.__dict__.pop("_weight_stash", None)
+        if stash is not None and stash[0] is weights:
+            return stash[1]
         return self.weight_quantizer.quantize(weights)
 
     def quantize_activation(self, out):

@@ -77,6 +77,13 @@ class UniformQuantizer(BaseQuantizer):
         act(x) in the same pass (K5); gradients are with respect to ``x``."""
         if not is_learning_scale:
             return fake_quant_fixed(x, scale, zero_point, self.qmin, self.qmax, act=act)
+        gscale, zero_point, learn_zp = self.learn_args(x, zero_point)
+        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp, act)
+
+    def learn_args(self, x, zero_point):
+        """(gscale, zero_point, learn_zp) of the learnable path for input x (uniform.py:47-53):
+        the ScaleGradient factor, and whether the zero point is learned (rounded + clamped
+        in the forward, with a gradient)."""
         gscale = _reduce_gscale(self.calculate_grad_scale(x) * self.calib_grad_scale)
         learn_zp = not self.symmetric
         if learn_zp and not isinstance(zero_point, torch.Tensor):
@@ -85,7 +92,7 @@ class UniformQuantizer(BaseQuantizer):
         if not learn_zp and isinstance(zero_point, torch.Tensor) and zero_point.requires_grad:
             raise NotImplementedError("a gradient-requiring zero point with a symmetric learnable "
                                       "quantizer is not supported")
-        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp, act)
+        return gscale, zero_point, learn_zp
 
     def _int_zero_point_learnable(self, zero_point):
         # Reference behaviour (uniform.py:50-52 -> :100 -> :267): torch.round(<int>) raises.
