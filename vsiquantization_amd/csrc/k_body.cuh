@@ -100,10 +100,11 @@ __device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
 }
 
 // xc: the loaded input -- the quantizer input itself, or (ACT) the pre-activation c
-// whose act(c) the forward quantized; grad_x then goes through the act's backward
-template <bool VEC, bool NT, bool ZPL, int ACT>
-__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv,
-                                          const QP &p, LsqAcc &c) {
+// whose act(c) the forward quantized; grad_x then goes through the act's backward.
+// Returns the group's grad_x (not stored).
+template <bool ZPL, int ACT>
+__device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv, const QP &p,
+                                            LsqAcc &c) {
   const f4 xv = act_fwd4<ACT>(xc);
   const int nv = i < ng ? valid_in_group(i, n) : 0;
   const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
@@ -120,16 +121,23 @@ __device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int6
     o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
     o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
   }
-  if (nv > 0) store_group<VEC, NT>(gx, i, n, act_bwd4<ACT>(o, xc));
+  return act_bwd4<ACT>(o, xc);
+}
+
+template <bool VEC, bool NT, bool ZPL, int ACT>
+__device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv,
+                                          const QP &p, LsqAcc &c) {
+  const f4 o = lsq_group_out<ZPL, ACT>(i, ng, n, xc, gv, p, c);
+  if (i < ng) store_group<VEC, NT>(gx, i, n, o);
 }
 
 // Block `blk` of the K4 grid: G groups per lane, straight-line (fully unrolled):
 // group k+kLsqPrefetch is loaded while group k computes, so x/g loads stay in flight
-// and s_waitcnt counts are exact.  Adds this thread's terms to c (not reduced).
+// and s_waitcnt counts are exact.  Adds this thread's terms to c (not reduced) and
+// leaves grad_x in o[] (stored by lsq_store_block once the block has arrived).
 template <bool VEC, bool NT, bool ZPL, int ACT, int G>
 __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const float *__restrict__ x,
-                                              float *__restrict__ gx, int64_t n, const QP &p, int64_t blk,
-                                              LsqAcc &c) {
+                                              int64_t n, const QP &p, int64_t blk, LsqAcc &c, f4 (&o)[G]) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * G + threadIdx.x;
   f4 xv[G], gv[G];
@@ -144,8 +152,37 @@ __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const
       xv[k + kLsqPrefetch] = load_group_c<VEC, NT>(x, base + (k + kLsqPrefetch) * kBlock, ng, n);
       gv[k + kLsqPrefetch] = load_group_c<VEC, NT>(g, base + (k + kLsqPrefetch) * kBlock, ng, n);
     }
-    lsq_group<VEC, NT, ZPL, ACT>(gx, base + k * kBlock, ng, n, xv[k], gv[k], p, c);
+    o[k] = lsq_group_out<ZPL, ACT>(base + k * kBlock, ng, n, xv[k], gv[k], p, c);
   }
+}
+
+template <bool VEC, bool NT, int G>
+__device__ __forceinline__ void lsq_store_block(float *__restrict__ gx, int64_t n, int64_t blk, const f4 (&o)[G]) {
+  const int64_t ng = cdiv(n, 4);
+  const int64_t base = blk * kBlock * G + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < G; ++k)
+    if (base + k * kBlock < ng) store_group<VEC, NT>(gx, base + k * kBlock, n, o[k]);
+}
+
+// Block sum of the K4 terms with the waves split (wave_arrive): DPP wave sums -> LDS;
+// waves 1..3 store their grad_x and return false; wave 0 passes an LDS-only barrier
+// and gets the block record {sum t, sum z} (fixed order) in every lane.
+template <bool VEC, bool NT, int G>
+__device__ __forceinline__ bool lsq_block_record(LsqAcc c, float *__restrict__ gx, int64_t n, int64_t blk,
+                                                 const f4 (&o)[G], double (&rec)[2]) {
+  __shared__ double s[kWaves][2];
+  c.t = wave_reduce(c.t, AddD());
+  c.z = wave_reduce(c.z, AddD());
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) { s[w][0] = c.t; s[w][1] = c.z; }
+  if (w != 0) lsq_store_block<VEC, NT, G>(gx, n, blk, o);
+  lds_barrier();
+  if (w != 0) return false;
+  rec[0] = s[0][0]; rec[1] = s[0][1];
+#pragma unroll
+  for (int i = 1; i < kWaves; ++i) { rec[0] += s[i][0]; rec[1] += s[i][1]; }
+  return true;
 }
 
 // gradient of the zero point after the fold: ClampBackward of zero_point_rounding

@@ -15,19 +15,16 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   const QP p = load_qp(src);
   LsqAcc c{0.0, 0.0};
   (void)prefetch;
-  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, gx, n, p, blockIdx.x, c);
-  lsq_block_reduce(c);
+  f4 o[G];
+  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o);
+  double rec[2], f[2];
+  if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
+  const bool last = wave_arrive<LsqFold>(ws, 0, gridDim.x, blockIdx.x, counter, rec, f);
+  lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);   // wave 0's grad_x, after its arrival
+  if (!last) return;
   if (threadIdx.x == 0) {
-    double *r = ws + (int64_t)blockIdx.x * kPartials;
-    partial_store(r + 0, c.t);
-    partial_store(r + 1, c.z);
-  }
-  double f[2];
-  if (!fold_arrivals<LsqFold>(ws, counter, f)) return;
-  c = LsqAcc{f[0], f[1]};
-  if (threadIdx.x == 0) {
-    grad_out[0] = c.t * gscale;
-    grad_out[1] = ZPL ? lsq_grad_zp(c.z, src, p, gscale) : 0.0;
+    grad_out[0] = f[0] * gscale;
+    grad_out[1] = ZPL ? lsq_grad_zp(f[1], src, p, gscale) : 0.0;
     *counter = 0u;
   }
 }

@@ -73,27 +73,23 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd_multi(const MBatch b, double
   LsqAcc c{0.0, 0.0};
   // the zero-point sum is always accumulated (only read when T.zpl): the scale sum and
   // grad_x do not depend on it
-  if (T.vec) lsq_bwd_block<true, NT, true, kActNone, kMultiG>(T.g, T.x, T.gx, T.n, p, blk, c);
-  else lsq_bwd_block<false, NT, true, kActNone, kMultiG>(T.g, T.x, T.gx, T.n, p, blk, c);
-  lsq_block_reduce(c);
-  __shared__ int s_last;
-  if (threadIdx.x == 0) {
-    double *r = ws + (int64_t)blockIdx.x * kPartials;
-    partial_store(r + 0, c.t);
-    partial_store(r + 1, c.z);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t k = __hip_atomic_fetch_add(counter + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (k == nb - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    s_last = last;
+  f4 o[kMultiG];
+  double rec[2], f[2];
+  bool w0;
+  if (T.vec) {
+    lsq_bwd_block<true, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, p, blk, c, o);
+    w0 = lsq_block_record<true, NT, kMultiG>(c, T.gx, T.n, blk, o, rec);
+  } else {
+    lsq_bwd_block<false, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, p, blk, c, o);
+    w0 = lsq_block_record<false, NT, kMultiG>(c, T.gx, T.n, blk, o, rec);
   }
-  __syncthreads();
-  if (!s_last) return;
-  double f[2];
-  fold_block<LsqFold>(ws, first, nb, 1, f);
+  if (!w0) return;   // waves 1..3 have stored their grad_x
+  // flat arrival on the tensor's own counter word, records in block order: the
+  // single-tensor kernel's fold for grids <= kArriveFlat, bit for bit
+  const bool last = wave_arrive<LsqFold>(ws, first, nb, (uint32_t)blk, counter + t, rec, f);
+  if (T.vec) lsq_store_block<true, NT, kMultiG>(T.gx, T.n, blk, o);
+  else lsq_store_block<false, NT, kMultiG>(T.gx, T.n, blk, o);
+  if (!last) return;
   if (threadIdx.x == 0) {
     T.gout[0] = f[0] * T.gscale;
     T.gout[1] = T.zpl ? lsq_grad_zp(f[1], src, p, T.gscale) : 0.0;
