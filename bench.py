@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
+    p.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5"], default="c2")
     p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -122,6 +122,52 @@ class C2PerChannel:
         return bool(torch.equal(scale, s["scale"].cpu()))
 
 
+class C1PerTensor:
+    """C1: the reference's minimal config -- MinMaxObserver + UniformQuantizer, per-tensor
+    symmetric int8, on a 256x256 fp32 weight (observers/minmax.py:76-88 then
+    quantizers/uniform.py:34-56): per step one K2 observe (running min/max + f64 qparams
+    on the device) and one K1 fake quant reading those qparams by pointer.  65,536
+    elements: latency-bound (launch + reduction chain), the GB/s are not the point."""
+
+    name = "C1 per-tensor sym int8 MinMax observe + fake-quant fwd, 256x256"
+    shape = (256, 256)
+
+    def __init__(self, dev, slots, seed_base):
+        from vsiquantization_amd import _hip as H
+        from vsiquantization_amd.fakequant import qden
+        self.H = H
+        self.n = n = 256 * 256
+        lib = H.lib()
+        st = H.stream_of(dev)
+        w = H.workspace(dev, n)
+        qd = qden(True, 8, 1e-8)
+        self.slots = []
+        for i in range(slots):
+            gen = torch.Generator(device=dev).manual_seed(seed_base + i)
+            x = torch.randn(self.shape, device=dev, generator=gen)
+            s = dict(x=x, y=torch.empty_like(x), rmm=torch.zeros(2, device=dev),
+                     qp=torch.empty(H.QP_LEN, dtype=torch.float64, device=dev))
+            P = {k: H.ptr(v) for k, v in s.items()}
+            s["fwd"] = (P["x"], H.c_i64(n), None, P["rmm"], P["qp"], 1, qd, 1e-8, H.ptr(w.ws),
+                        H.c_i64(w.ws_len), H.ptr(w.counter), st)
+            s["bwd"] = (P["x"], P["y"], None, None, H.c_i64(n), P["qp"], None, 0.0, None, 0.0, 0, 0, -128, 127, st)
+            self.slots.append(s)
+        self.f_fwd = lib.vsiq_observe_f32
+        self.f_bwd = lib.vsiq_fq_fwd_f32
+        self.kernels = {"observe": 4 * n, "fq_fwd": 8 * n}
+
+    launch = None   # set below (same group structure as C2: all observes, then all fake quants)
+
+    def check(self):
+        """Slot 0 against the reference's formulas in torch on the host (IEEE fp32 x / s)."""
+        s = self.slots[0]
+        x = s["x"].cpu()
+        mn, mx = min(0.0, float(x.min())), max(0.0, float(x.max()))
+        scale = max(abs(mn), abs(mx)) / (2 ** 7 - 1 + 1e-8)
+        want = torch.clamp(torch.round(x / scale), -128, 127) * scale
+        return bool(torch.equal(s["y"].cpu().view(torch.int32), want.view(torch.int32)))
+
+
 class C3Lsq:
     """LSQ learnable symmetric int8 fwd + STE bwd on a 512x3x224x224 activation."""
 
@@ -164,6 +210,10 @@ class C3Lsq:
 
     def check(self):
         return True
+
+
+C1PerTensor.launch = C2PerChannel.launch
+C1PerTensor.launch_group = C2PerChannel.launch_group
 
 
 def yolov8n_backbone(img=320, width=(3, 16, 32, 64, 128, 256), depth=(1, 2, 2)):
@@ -386,7 +436,17 @@ def cpu_baseline(workload, seconds):
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     gen = torch.Generator().manual_seed(0)
-    if workload == "c2":
+    if workload == "c1":
+        from oracle.fakequant_np import minmax_qparams
+        x = torch.randn(256, 256, generator=gen)
+
+        def fn():   # observers/minmax.py:76-88 (two .item()) then uniform.py:54-55,95
+            mn, mx = E.observe(x)
+            s, z = minmax_qparams(mn, mx, True, 8)
+            return E.fake_quant(x, s, z, -128, 127)
+        n = x.numel()
+        sample = "the whole 256x256 workload (observe + fake quant per call)"
+    elif workload == "c2":
         rows = 64   # bounded sample: 64 of the 1024 out-channels (same row length 9216)
         w = torch.randn(rows, 1024, 3, 3, generator=gen) * 0.05
         g = torch.randn(rows, 1024, 3, 3, generator=gen)
@@ -472,7 +532,7 @@ def main():
     elif a.workload == "c5":
         W = C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=max(a.steps, a.warmup))
     else:
-        W = (C2PerChannel if a.workload == "c2" else C3Lsq)(dev, a.slots, 1000 * rank)
+        W = {"c1": C1PerTensor, "c2": C2PerChannel, "c3": C3Lsq}[a.workload](dev, a.slots, 1000 * rank)
     for i in range(a.warmup):
         assert W.launch(i) == 0
     torch.cuda.synchronize()
@@ -511,7 +571,8 @@ def main():
                   for k in names}
 
     total_elems = W.n * a.steps * world
-    metrics = {"c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
+    metrics = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + achieved HBM GB/s vs roofline",
+               "c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
                "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
                "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
                      "HBM GB/s vs roofline",

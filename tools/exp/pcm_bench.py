@@ -1,0 +1,35 @@
+"""K6 / per-channel fake quant (LSQFakeQuantize per-channel, axis 1) at YOLOv8n activation
+shapes, batch 256, and axis-0 weights. Experiment only: prints us and GB/s per launch."""
+import os, sys, torch
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import vsiquantization_amd  # noqa
+from vsiquantization_amd import fakequant as FQ
+
+dev = torch.device("cuda:0")
+
+
+def t(fn, reps):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize(); s.record()
+    for _ in range(reps):
+        fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3
+
+
+for shape, axis in (((256, 16, 160, 160), 1), ((256, 64, 40, 40), 1), ((256, 256, 10, 10), 1),
+                    ((256, 128, 20, 20), 1), ((1024, 1024, 3, 3), 0)):
+    x = torch.randn(shape, device=dev)
+    g = torch.randn(shape, device=dev)
+    C = shape[axis]
+    s = torch.rand(C, dtype=torch.float64, device=dev) * 0.05 + 0.01
+    z = torch.zeros(C, dtype=torch.float64, device=dev)
+    n = x.numel()
+    reps = max(10, min(200, (4 << 30) // (12 * n)))
+    fwd = t(lambda: FQ.per_channel_fake_quant(x, s, z, -128, 127, axis=axis), reps)
+    bwd = t(lambda: FQ.pc_lsq_backward(g, x, s, z, -128, 127, 1e-4, True, axis), reps)
+    print(f"{str(shape):22s} axis {axis}  fwd {fwd:8.2f} us ({8 * n / fwd / 1e3:5.0f} GB/s)   "
+          f"bwd(K6) {bwd:8.2f} us ({12 * n / bwd / 1e3:5.0f} GB/s)", flush=True)
