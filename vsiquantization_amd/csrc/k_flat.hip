@@ -471,6 +471,10 @@ int vsiq_set_tuning(int key, int value) {
       if (value < -1 || value > 64) return VSIQ_E_ARG;
       g_tune.store_defer = value;
       return 0;
+    case VSIQ_TUNE_PC_PACKED:
+      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      g_tune.pc_packed = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;

@@ -159,6 +159,82 @@ __global__ __launch_bounds__(kBlock) void k_pcm_lsq_fold(const double *__restric
   }
 }
 
+// K6 stage 1 on packed short rows (pc_packed): R whole rows per workgroup (see
+// k_pcp_fq_fwd); each group's {t, z} terms go to LDS, then wave w sums rows w, w+4,
+// ... (lanes over the row's groups in order, DPP tree) into the row's record -- the
+// same ws layout as k_pcm_lsq_bwd with one chunk per row, folded by k_pcm_lsq_fold.
+template <bool VEC, bool NT, bool ZPL>
+__global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict__ g,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ gx, int64_t rows,
+                                                        int64_t rowlen, uint32_t rpb, int64_t channels,
+                                                        const double *__restrict__ scale,
+                                                        const double *__restrict__ zp, float lo,
+                                                        float hi, double *__restrict__ ws) {
+  __shared__ QP s_qp[kPackMaxRows];
+  __shared__ double s_t[kPackGroups * kBlock], s_z[kPackGroups * kBlock];
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const uint32_t nr = (uint32_t)std::min<int64_t>(rpb, rows - r0);
+  const uint32_t gpr = (uint32_t)(rowlen / 4);
+  const int64_t n = rows * rowlen, ng = rows * gpr;
+  const int64_t j0 = r0 * gpr;
+  const uint32_t nj = nr * gpr;
+  f4 xv[kPackGroups], gv[kPackGroups];
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    const int64_t i = j0 + (j < nj ? j : nj - 1);
+    xv[k] = load_group_c<VEC, NT>(x, i, ng, n);
+    gv[k] = load_group_c<VEC, NT>(g, i, ng, n);
+  }
+  if (threadIdx.x < nr) {
+    const int64_t c = (r0 + threadIdx.x) % channels;
+    s_qp[threadIdx.x] = load_qp(QPSrc{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi,
+                                      ZPL ? 1 : 0, 0});
+  }
+  lds_barrier();
+  f4 o[kPackGroups];
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    const uint32_t jj = j < nj ? j : nj - 1;
+    LsqAcc acc{0.0, 0.0};
+    o[k] = lsq_group_out<ZPL, kActNone>(j0 + jj, ng, n, xv[k], gv[k], s_qp[jj / gpr], acc);
+    if (j < nj) { s_t[j] = acc.t; s_z[j] = acc.z; }
+  }
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    if (j < nj) store_group<VEC, NT>(gx, j0 + j, n, o[k]);
+  }
+  lds_barrier();   // the grad_x stores stay in flight
+  const uint32_t w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  for (uint32_t r = w; r < nr; r += kWaves) {   // wave-uniform
+    double t = 0.0, z = 0.0;
+    for (uint32_t q = lane; q < gpr; q += kWave) { t += s_t[r * gpr + q]; z += s_z[r * gpr + q]; }
+    t = wave_reduce(t, AddD());
+    z = wave_reduce(z, AddD());
+    if (lane == 0) {
+      ws[2 * (r0 + r)] = t;
+      ws[2 * (r0 + r) + 1] = z;
+    }
+  }
+}
+
+template <bool VEC, bool NT>
+void launch_pcp_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                    int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
+                    float hi, double *ws, hipStream_t st) {
+  const int64_t rpb = pc_pack_rows(rowlen);
+  const dim3 grid((unsigned)cdiv(rows, rpb)), block(kBlock);
+  if (zp_learn)
+    hipLaunchKernelGGL((k_pcp_lsq_bwd<VEC, NT, true>), grid, block, 0, st, g, x, gx, rows, rowlen,
+                       (uint32_t)rpb, channels, scale, zp, lo, hi, ws);
+  else
+    hipLaunchKernelGGL((k_pcp_lsq_bwd<VEC, NT, false>), grid, block, 0, st, g, x, gx, rows, rowlen,
+                       (uint32_t)rpb, channels, scale, zp, lo, hi, ws);
+}
+
 template <bool VEC, bool NT>
 void launch_pcm_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                     int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
@@ -215,8 +291,12 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
   hipStream_t st = (hipStream_t)stream;
   const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
   const bool nt = g_tune.nontemporal != 0;
-  VSIQ_B2(launch_pcm_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
-          (float)qmax, ws, st);
+  if (pc_packed(rowlen) && g_tune.pc_packed != 0)   // one chunk per row: same record layout
+    VSIQ_B2(launch_pcp_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
+            (float)qmax, ws, st);
+  else
+    VSIQ_B2(launch_pcm_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
+            (float)qmax, ws, st);
   hipLaunchKernelGGL(k_pcm_lsq_fold, dim3((unsigned)channels), dim3(kBlock), 0, st, ws, rows,
                      (uint32_t)chunks, channels, zp, zp_learn, (float)qmin, (float)qmax, gscale,
                      grad_scale_out, grad_zp_out);

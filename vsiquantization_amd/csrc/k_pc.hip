@@ -116,6 +116,56 @@ void launch_pc_fixed(const float *x, float *y, uint8_t *c, uint64_t *m, const PC
   else hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, c, m, ch, a);
 }
 
+// ----------------------------------------------------------------------------
+// Packed short rows (rowlen % 4 == 0, rowlen <= kPackMaxRowlen): one workgroup takes
+// R = kPackElems / rowlen WHOLE rows (up to 256), i.e. a contiguous flat range of
+// groups, 4 per lane.  The one-workgroup-per-row grid above leaves most lanes idle
+// on LSQFakeQuantize's axis-1 activations (rows of H*W = 100..1600 elements: 686 GB/s
+// at 256x256x10x10 on MI355X).  Per-row qparams are built once per workgroup into
+// LDS; each group reads its row's.  No mask output (its word layout assumes one row
+// per wave): a mask request takes the per-row kernel.
+// ----------------------------------------------------------------------------
+template <bool VEC, bool NT, bool CODES>
+__global__ __launch_bounds__(kBlock) void k_pcp_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
+                                                       uint8_t *__restrict__ codes, int64_t rows,
+                                                       uint32_t rpb, PCFixed a) {
+  __shared__ QP s_qp[kPackMaxRows];
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const uint32_t nr = (uint32_t)std::min<int64_t>(rpb, rows - r0);
+  const uint32_t gpr = (uint32_t)(a.rowlen / 4);
+  const int64_t n = rows * a.rowlen, ng = rows * gpr;
+  const int64_t j0 = r0 * gpr;
+  const uint32_t nj = nr * gpr;
+  f4 v[kPackGroups];
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    v[k] = load_group_c<VEC, NT>(x, j0 + (j < nj ? j : nj - 1), ng, n);
+  }
+  if (threadIdx.x < nr) s_qp[threadIdx.x] = pc_fixed_qp(a, r0 + threadIdx.x);
+  lds_barrier();   // the loads stay in flight
+  GroupOut go[kPackGroups];
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    const QP p = s_qp[(j < nj ? j : nj - 1) / gpr];
+    go[k] = fq_out_flat<VEC, CODES, false>(v[k], p, j0 + j, n);
+  }
+#pragma unroll
+  for (int k = 0; k < kPackGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    if (j < nj) fq_store_out<VEC, NT, CODES>(y, codes, j0 + j, ng, n, go[k]);
+  }
+}
+
+template <bool VEC, bool NT>
+void launch_pcp_fixed(const float *x, float *y, uint8_t *c, const PCFixed &a, int64_t rows, hipStream_t st) {
+  const int64_t rpb = pc_pack_rows(a.rowlen);
+  const dim3 grid((unsigned)cdiv(rows, rpb)), block(kBlock);
+  if (c) hipLaunchKernelGGL((k_pcp_fq_fwd<VEC, NT, true>), grid, block, 0, st, x, y, c, rows, (uint32_t)rpb, a);
+  else hipLaunchKernelGGL((k_pcp_fq_fwd<VEC, NT, false>), grid, block, 0, st, x, y, c, rows, (uint32_t)rpb, a);
+}
+
 }  // namespace vsiq
 
 using namespace vsiq;
@@ -158,7 +208,10 @@ int vsiq_pcm_fq_fwd_f32(const float *x, float *y, void *codes, uint64_t *mask, i
   const bool vec = (rowlen % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
   const bool nt = g_tune.nontemporal != 0;
   uint8_t *c = (uint8_t *)codes;
-  VSIQ_B2(launch_pc_fixed, vec, nt, x, y, c, mask, a, rows, (hipStream_t)stream);
+  if (!mask && pc_packed_fwd(rowlen) && g_tune.pc_packed != 0)
+    VSIQ_B2(launch_pcp_fixed, vec, nt, x, y, c, a, rows, (hipStream_t)stream);
+  else
+    VSIQ_B2(launch_pc_fixed, vec, nt, x, y, c, mask, a, rows, (hipStream_t)stream);
   return launch_rc();
 }
 
