@@ -175,6 +175,7 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
  * float64 summation order.
  */
 #define VSIQ_PART_LEN 8
+#define VSIQ_PART_MAX_RECORDS 1024   /* vsiq_observe_part_records(n) <= this for every n */
 int64_t vsiq_observe_part_records(int64_t n);
 int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
                               void *stream);

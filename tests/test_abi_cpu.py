@@ -61,6 +61,8 @@ def test_argument_validation_without_gpu():
     assert lib.vsiq_observe_part_records(0) == -1
     assert lib.vsiq_observe_part_records(1) == 1
     assert lib.vsiq_observe_part_records(1 << 40) == 512
+    assert max(lib.vsiq_observe_part_records(n) for n in range(1, 1 << 24, 4099)) <= H.PART_MAX_RECORDS
+    assert lib.vsiq_observe_part_records(1638400) == 800            # small layers: 2 groups / lane
     assert lib.vsiq_act_observe_part_f32(null, 16, 0, null, 0, null) == -1
     assert lib.vsiq_act_observe_part_f32(1, 16, 0, 1, H.PART_LEN - 1, null) == -3   # slot too small
     assert lib.vsiq_act_observe_part_f32(1, 16, 3, 1, 64, null) == -1               # bad activation

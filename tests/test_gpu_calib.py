@@ -84,7 +84,7 @@ def test_observe_parts_fold_equals_k2(n, act):
     xs = [torch.randn(n, device=DEV, generator=g) * 3 for _ in range(3)]
     xs[1][n // 2] = float("nan")
     xs.append(torch.randn(n + 1, device=DEV, generator=g)[1:])   # misaligned view
-    stride = FQ.part_slot_doubles(1 << 62)
+    stride = FQ.part_slot_doubles()
     slots = torch.full((len(xs), stride), float("nan"), dtype=torch.float64, device=DEV)
     for i, x in enumerate(xs):
         FQ.observe_parts(x, out=slots[i], act=act)
@@ -103,7 +103,7 @@ def test_observe_parts_fold_equals_k2(n, act):
 def test_fold_parts_unwritten_slot_folds_nothing():
     from vsiquantization_amd import _hip as H
     from vsiquantization_amd import fakequant as FQ
-    stride = FQ.part_slot_doubles(1 << 62)
+    stride = FQ.part_slot_doubles()
     slots = torch.zeros(2, stride, dtype=torch.float64, device=DEV)
     slots[1, 7] = 1e30   # garbage record count: ignored, never read out of range
     st = FQ.fold_parts(slots).cpu()

@@ -16,6 +16,7 @@ import sys
 # workload -> [(kernel-name fragment, bench.py kernel label, launches of it per step)];
 # a label's bytes per step = sum over its fragments of (mean per dispatch x launches)
 KERNEL_KEYS = {
+    "c1": [("k_observe_loop<", "observe", 1), ("k_fq_fwd<", "fq_fwd", 1)],
     "c2": [("k_pc_observe_fq<", "pc_observe_fq_fwd", 1), ("k_ste_bwd<", "ste_bwd", 1)],
     "c3": [("k_fq_fwd<", "fq_fwd", 1), ("k_lsq_bwd<", "lsq_bwd", 1)],
     # C4: per step 27 fused-ReLU activation launches each way + ONE multi-tensor launch

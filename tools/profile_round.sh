@@ -14,7 +14,7 @@ run() {
   return $rc
 }
 export TMPDIR=/tmp
-for W in ${WORKLOADS:-c2 c3 c4 c5}; do
+for W in ${WORKLOADS:-c1 c2 c3 c4 c5}; do
   case $W in
     c4) S=20; WU=4; SP=8; WP=2 ;;
     c5) S=16; WU=2; SP=16; WP=2 ;;

@@ -393,21 +393,42 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   return launch_rc();
 }
 
+// K2p groups per lane per step: 8 while the grid reaches 512 workgroups, else fewer so
+// that small layers still spread over >= ~512 workgroups (all CUs issuing; a 1.6M-
+// element layer at 8 per lane was 200 workgroups).  Fixed per n: deterministic.
+inline int observe_part_u(int64_t n) {
+  const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);   // lanes' worth of groups
+  return units >= 512 * 8 ? 8 : (units >= 512 * 4 ? 4 : 2);
+}
+
+// K2p grid (fixed per n), at most VSIQ_PART_MAX_RECORDS workgroups
+inline int64_t observe_part_grid(int64_t n) {
+  const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
+  const int u = observe_part_u(n);
+  // large tensors: kObsGrid workgroups striding over the tensor; small: one step each
+  int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS);
+  cap = std::min<int64_t>(cap, VSIQ_PART_MAX_RECORDS);
+  return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(units, u)));
+}
+
+template <int ACT, int U>
+void launch_observe_part_u(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
+                           hipStream_t st) {
+  if (vec && nt)
+    hipLaunchKernelGGL((k_observe_part<true, true, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+  else if (vec)
+    hipLaunchKernelGGL((k_observe_part<true, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+  else
+    hipLaunchKernelGGL((k_observe_part<false, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+}
+
 template <int ACT>
 void launch_observe_part(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
                          hipStream_t st) {
-  if (vec && nt)
-    hipLaunchKernelGGL((k_observe_part<true, true, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
-  else if (vec)
-    hipLaunchKernelGGL((k_observe_part<true, false, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
-  else
-    hipLaunchKernelGGL((k_observe_part<false, false, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
-}
-
-// K2p grid: the grid-stride rule of K2 (fixed per n)
-inline int64_t observe_part_grid(int64_t n) {
-  const int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : kObsGrid;
-  return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(cdiv(n, 4), (int64_t)kBlock * kObsU)));
+  const int u = observe_part_u(n);
+  if (u == 8) launch_observe_part_u<ACT, 8>(vec, nt, x, n, parts, grid, st);
+  else if (u == 4) launch_observe_part_u<ACT, 4>(vec, nt, x, n, parts, grid, st);
+  else launch_observe_part_u<ACT, 2>(vec, nt, x, n, parts, grid, st);
 }
 
 // CU count of the current device (cached; 256 on MI355X)

@@ -313,8 +313,11 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     return qp, st
 
 
-def part_slot_doubles(n: int) -> int:
-    """Doubles of one deferred-observer slot for n elements (K2p records x VSIQ_PART_LEN)."""
+def part_slot_doubles(n: int | None = None) -> int:
+    """Doubles of one deferred-observer slot for n elements (K2p records x VSIQ_PART_LEN);
+    n None: a slot that fits any n."""
+    if n is None:
+        return H.PART_MAX_RECORDS * H.PART_LEN
     r = int(H.lib().vsiq_observe_part_records(_i64(n)))
     H.check(r if r < 0 else 0, "vsiq_observe_part_records")
     return r * H.PART_LEN
