@@ -1,3 +1,4 @@
+# K4 fold experiments: LSQ tests, per-size K4/K2 timing, C3/C4 bench lines
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

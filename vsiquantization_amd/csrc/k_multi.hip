@@ -86,9 +86,10 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd_multi(const MBatch b, double
   if (!w0) return;   // waves 1..3 have stored their grad_x
   // flat arrival on the tensor's own counter word, records in block order: the
   // single-tensor kernel's fold for grids <= kArriveFlat, bit for bit
-  const bool last = wave_arrive<LsqFold>(ws, first, nb, (uint32_t)blk, counter + t, rec, f);
-  if (T.vec) lsq_store_block<true, NT, kMultiG>(T.gx, T.n, blk, o);
-  else lsq_store_block<false, NT, kMultiG>(T.gx, T.n, blk, o);
+  const bool last = wave_arrive<LsqFold>(ws, first, nb, (uint32_t)blk, counter + t, rec, f, [&]() {
+    if (T.vec) lsq_store_block<true, NT, kMultiG>(T.gx, T.n, blk, o);
+    else lsq_store_block<false, NT, kMultiG>(T.gx, T.n, blk, o);
+  });
   if (!last) return;
   if (threadIdx.x == 0) {
     T.gout[0] = f[0] * T.gscale;

@@ -855,22 +855,27 @@ __device__ __forceinline__ bool fold_arrivals(double *ws, uint32_t *counter, dou
 // with lane 0 (only that store is outstanding when it drains), arrives, THEN stores.
 // fold_wave / wave_arrive run in one wave (64 lanes, no __syncthreads).
 // ----------------------------------------------------------------------------
+// kWaveFold records per lane in flight: one memory round trip folds 64 x kWaveFold
+// records (each round is a dependent round trip to the coherence point)
+constexpr int kWaveFold = 8;
+constexpr uint32_t kWaveFoldDirect = kWave * kWaveFold;   // 512: one round
+
 template <typename Op>
 __device__ __forceinline__ void fold_wave(const double *ws, uint32_t first, uint32_t count, uint32_t stride,
                                           double (&a)[Op::K]) {
   constexpr int K = Op::K;
   Op::init(a);
   const uint32_t lane = threadIdx.x % kWave;
-  for (uint32_t j0 = lane; j0 < count; j0 += 4 * kWave) {
-    double r[4][K];
+  for (uint32_t j0 = lane; j0 < count; j0 += kWaveFold * kWave) {
+    double r[kWaveFold][K];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kWaveFold; ++u) {
       const uint32_t j = j0 + u * kWave < count ? j0 + u * kWave : count - 1;
 #pragma unroll
       for (int k = 0; k < K; ++k) r[u][k] = partial_load(ws + (int64_t)(first + j * stride) * kPartials + k);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kWaveFold; ++u)
       if (j0 + u * kWave < count) Op::add(a, r[u]);
   }
   Op::wave(a);
@@ -886,11 +891,16 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // in fold_arrivals.  Returns true (wave-uniform) in the block that holds, in `a`
 // (every lane), the fold of every record: flat for nb <= kArriveFlat, else arrivals
 // on counter 1 + blk % 32 then counter 0, with one direct fold of all records up to
-// kFoldDirect blocks and per-group folds above.  Fixed trees: deterministic.
-template <typename Op>
+// kWaveFoldDirect blocks (one round of loads) and per-group folds above (one round per
+// group up to 16384 blocks, then one over the 32 group records).  Fixed trees:
+// deterministic.
+// `after_arrival()` runs in wave 0 right after the block's own arrival, before any
+// fold: the caller's stores go there (issued after the record drain; their registers
+// are free again before the fold's loads).
+template <typename Op, typename F>
 __device__ __forceinline__ bool wave_arrive(double *ws, uint32_t first, uint32_t nb, uint32_t blk,
                                             uint32_t *counter, const double (&rec)[Op::K],
-                                            double (&a)[Op::K]) {
+                                            double (&a)[Op::K], F &&after_arrival) {
   constexpr int K = Op::K;
   const uint32_t lane = threadIdx.x % kWave;
   const uint32_t g = blk % kArriveGroups;
@@ -911,7 +921,7 @@ __device__ __forceinline__ bool wave_arrive(double *ws, uint32_t first, uint32_t
         role = 1;
       }
     }
-    if (role == 1 && nb <= (uint32_t)kFoldDirect) {   // straight on to counter 0
+    if (role == 1 && nb <= kWaveFoldDirect) {   // straight on to counter 0
       const uint32_t t0 = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = (t0 == (uint32_t)kArriveGroups - 1) ? 2 : 0;
     }
@@ -921,6 +931,7 @@ __device__ __forceinline__ bool wave_arrive(double *ws, uint32_t first, uint32_t
     }
   }
   role = __builtin_amdgcn_readfirstlane(role);
+  after_arrival();
   if (role == 0) return false;
   if (role == 2) {
     fold_wave<Op>(ws, first, nb, 1, a);
