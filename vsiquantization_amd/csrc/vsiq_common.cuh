@@ -35,7 +35,10 @@ constexpr int kWave = 64;
 constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // minimum partial-record slots of a workspace
 constexpr int kPartials = 8;           // doubles per partial record
-constexpr int kArriveFlat = 128;       // grids above this arrive in two levels (arrive_last)
+#ifndef VSIQ_ARRIVE_FLAT
+#define VSIQ_ARRIVE_FLAT 128
+#endif
+constexpr int kArriveFlat = VSIQ_ARRIVE_FLAT;   // grids above this arrive in two levels (arrive_last)
 constexpr int kArriveGroups = 32;      // level-1 arrival counters (counter words 1..32)
 #ifndef VSIQ_FOLD_DIRECT
 #define VSIQ_FOLD_DIRECT 2048
