@@ -86,7 +86,7 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_PC_BLOCK 5           /* K3 workgroup size 256 / 512 / 1024, 0 = auto */
 #define VSIQ_TUNE_OBS_KERNEL 7         /* K2 observer: 0 auto, 1 one-shot, 2 grid-stride */
 #define VSIQ_TUNE_OBS_GRID 8           /* K2 grid-stride workgroups, 0 = auto (512), max 2048 */
-#define VSIQ_TUNE_LSQ_GROUPS 9         /* K4 groups per lane 2 / 4 / 16, 0 = by size */
+#define VSIQ_TUNE_LSQ_GROUPS 9         /* K4 groups per lane 2 / 4 / 8 / 16, 0 = by size */
 #define VSIQ_TUNE_PC_PACKED 10         /* per-channel fq with given qparams + K6: 1 = packed short
                                           rows (default), 0 = one workgroup per row */
 #define VSIQ_TUNE_STORE_DEFER 6        /* one-round grids: hold stores back N x 512 clocks after

@@ -293,10 +293,11 @@ def test_lsq_c3_full_size(sym):
         assert float(zp.grad) == pytest.approx(gzo, rel=1e-9)
 
 
-@pytest.mark.parametrize("groups", [0, 2, 4, 16])
-@pytest.mark.parametrize("n", [1, 4099, 295_000, 525_000, 3_276_800, 13_107_200])
+@pytest.mark.parametrize("groups", [0, 2, 4, 8, 16])
+@pytest.mark.parametrize("n", [1, 4099, 295_000, 525_000, 3_276_800, 13_107_200, 21_000_003])
 def test_lsq_groups_per_lane_sizes(n, groups):
-    """K4 at 2 / 4 / 16 groups per lane (VSIQ_TUNE_LSQ_GROUPS; 0 = default 4), grids from 1
+    """K4 at 2 / 4 / 8 / 16 groups per lane (VSIQ_TUNE_LSQ_GROUPS; 0 = default: 4, 8 from
+    20M elements), grids from 1
     to >12k workgroups (flat and two-level partial folds): grad_x bitwise, f64 scale
     gradient vs the oracle's closed form."""
     x = _rand(n, n % 97, 0.5)
@@ -312,7 +313,7 @@ def test_lsq_groups_per_lane_sizes(n, groups):
 
 
 @pytest.mark.parametrize("obs_kernel", [1, 2])
-@pytest.mark.parametrize("n", [1, 4099, 525_000, 3_276_800, 13_107_200])
+@pytest.mark.parametrize("n", [1, 4099, 525_000, 3_276_800, 13_107_200, 21_000_003])
 def test_observer_kernels_sizes(n, obs_kernel):
     """K2 one-shot (flat and two-level folds) and grid-stride forms against the oracle."""
     x = _rand(n, n % 61 + 3, 0.7)

@@ -29,7 +29,7 @@ tag = os.environ.get("VSIQ_LIBRARY", "default") + os.environ.get("TUNE", "")
 for kv in os.environ.get("TUNE", "").split():
     k, v = kv.split("=")
     H.set_tuning(int(k), int(v))
-for n in (1638400, 3276800, 6553600, 13107200, 26214400):
+for n in [int(v) for v in os.environ.get('SIZES', '1638400 3276800 6553600 13107200 26214400').split()]:
     sl = max(2, min(8, (1600 << 20) // (12 * n)))
     bufs = [torch.randn(n, device=dev) for _ in range(3 * sl)]
     reps = max(10, min(200, (8 << 30) // (12 * n)))

@@ -1,0 +1,8 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest rc=$?; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -u bench.py --workload c3 > gpurun_out/b_c3.log 2>&1 || { echo bench rc=$?; tail gpurun_out/b_c3.log; exit 1; }
+tail -1 gpurun_out/b_c3.log

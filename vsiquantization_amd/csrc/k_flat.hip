@@ -359,8 +359,14 @@ void launch_observe_loop(const float *x, int64_t n, double *stats_out, float *ru
 // workgroup's 8 serial load rounds cost more than the chain: 12.5 vs 6.8 us, MI355X.)
 constexpr int64_t kObsSingle = (int64_t)kBlock * kObsU;
 
+// one-shot K2 has 2 / 4 / 16 groups-per-lane instances: K4's 8 runs as 4
+inline int obs_groups_per_lane(int64_t ng) {
+  const int p = lsq_groups_per_lane(ng);
+  return p == 8 ? 4 : p;
+}
+
 inline int64_t observe_grid(int64_t ng) {
-  if (g_tune.obs_kernel == 1) return lsq_grid(ng);
+  if (g_tune.obs_kernel == 1) return lsq_grid(ng, obs_groups_per_lane(ng));
   if (ng <= kObsSingle && g_tune.obs_grid == 0) return 1;
   const int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : kObsGrid;
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(ng, (int64_t)kBlock * kObsU)));
@@ -378,8 +384,8 @@ void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_
     else launch_observe_loop<ACT, false, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
     return;
   }
-  // one-shot: same groups-per-lane rule and grid as K4 (lsq_grid)
-  const int per_lane = lsq_groups_per_lane(ng);
+  // one-shot: K4's groups-per-lane rule (8 -> 4) and grid
+  const int per_lane = obs_groups_per_lane(ng);
 #define VSIQ_OBS(V, N)                                                                              \
   (per_lane == kLsqGroups                                                                           \
        ? launch_observe_g<ACT, V, N, kLsqGroups>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, \
@@ -499,7 +505,7 @@ int vsiq_set_tuning(int key, int value) {
       g_tune.obs_grid = value;
       return 0;
     case VSIQ_TUNE_LSQ_GROUPS:
-      if (value != 0 && value != 2 && value != 4 && value != 16) return VSIQ_E_ARG;
+      if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16) return VSIQ_E_ARG;
       g_tune.lsq_groups = value;
       return 0;
     case VSIQ_TUNE_STORE_DEFER:

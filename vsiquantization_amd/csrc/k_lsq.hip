@@ -51,6 +51,8 @@ void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const 
   const int per_lane = lsq_groups_per_lane(cdiv(n, 4));
   if (per_lane == kLsqGroups)
     launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+  else if (per_lane == 8)
+    launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
   else if (per_lane == 4)
     launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
   else

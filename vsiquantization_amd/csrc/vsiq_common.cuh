@@ -1064,9 +1064,11 @@ inline int64_t oneshot_grid(int64_t groups) {
 // (tools/exp/k4_sizes.py, fused ReLU: 105M elements 230 -> 216 us, 3.3M 19.1 -> 15.4,
 // 296K 16.4 -> 7.3); 2 per lane pays the epilogue twice as often (105M: 342 us).
 // Override: VSIQ_TUNE_LSQ_GROUPS (2 / 4 / 16).
+// From 20M elements on, 8 per lane: half the workgroups, half the arrivals
+// (C3 77M: 161.5 -> 156.1 us, 26M: 59.8 -> 58.1; at 3.3M 4 stays faster).
 inline int lsq_groups_per_lane(int64_t groups) {
-  (void)groups;
-  return g_tune.lsq_groups > 0 ? g_tune.lsq_groups : 4;
+  if (g_tune.lsq_groups > 0) return g_tune.lsq_groups;
+  return groups >= (int64_t)5 << 20 ? 8 : 4;
 }
 
 inline int64_t lsq_grid(int64_t groups, int per_lane) {
