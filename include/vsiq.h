@@ -89,6 +89,9 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_LSQ_GROUPS 9         /* K4 groups per lane 2 / 4 / 8 / 16, 0 = by size */
 #define VSIQ_TUNE_PC_PACKED 10         /* per-channel fq with given qparams + K6: 1 = packed short
                                           rows (default), 0 = one workgroup per row */
+#define VSIQ_TUNE_STORE_GATE 11        /* one-round K3 / STE grids: no stores before workgroup
+                                          start + N ticks of the 100 MHz wall clock (-1 = auto:
+                                          the grid's read time at 7.5 TB/s; 0 = off) */
 #define VSIQ_TUNE_STORE_DEFER 6        /* one-round grids: hold stores back N x 512 clocks after
                                           the loads (-1 = auto, 0 = off, max 64) */
 int vsiq_set_tuning(int key, int value);

@@ -91,7 +91,7 @@ def test_tuning_keys_match_header_and_bounds():
                             "vsiq.h")).read()
     keys = dict(re.findall(r"#define VSIQ_(TUNE_\w+) (\d+)", hdr))
     for name in ("TUNE_PC_ROWS_PER_BLOCK", "TUNE_NONTEMPORAL", "TUNE_PC_BLOCK", "TUNE_STORE_DEFER", "TUNE_OBS_KERNEL",
-                 "TUNE_OBS_GRID", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED"):
+                 "TUNE_OBS_GRID", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED", "TUNE_STORE_GATE"):
         assert int(keys[name]) == getattr(H, name), name
     assert int(re.search(r"#define VSIQ_COUNTER_WORDS (\d+)", hdr).group(1)) == H.COUNTER_WORDS
     assert int(re.search(r"#define VSIQ_ABI_VERSION (\d+)", hdr).group(1)) == H.ABI_VERSION

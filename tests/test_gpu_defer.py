@@ -1,4 +1,5 @@
-"""Deferred store phase (defer_stores, VSIQ_TUNE_STORE_DEFER) of the STE backward.
+"""Deferred store phase (defer_stores, VSIQ_TUNE_STORE_DEFER) of the STE backward, and the
+store gate (store_gate, VSIQ_TUNE_STORE_GATE) of K3 and the STE.
 
 The deferral only changes when a workgroup's stores are issued, never what they hold:
 the one-round 9-groups-per-lane path (automatic for 384..1024 workgroups) must equal
@@ -75,3 +76,37 @@ def test_flat_ste_deferred_equals_plain(act, defer_tuning):
         m = G.unpack_mask(mask.cpu().numpy(), 1, n).reshape(-1)
         G.assert_bitwise_f32(outs[-1], O.fq_backward_fixed(g.reshape(-1), m, s), "oracle")
 
+
+@pytest.fixture
+def gate_tuning():
+    yield lambda v: H.set_tuning(H.TUNE_STORE_GATE, v)
+    H.set_tuning(H.TUNE_STORE_GATE, -1)
+
+
+@pytest.mark.parametrize("shape", [(1024, 9216), (2048, 4608), (700, 9216)])
+def test_per_channel_store_gate_equals_plain_and_oracle(shape, gate_tuning):
+    """K3 with the store gate (auto: one-round grids of >= 2 rows per CU; forced short
+    and very long gates; off) and the STE with a forced gate: bit-identical outputs,
+    qparams and masks, equal to the oracle (observers/minmax.py:32-74 per row, then
+    quantizers/uniform.py:54-55,95)."""
+    rows, rowlen = shape
+    x, g = _inputs(rows, rowlen, rows + 1)
+    xd = torch.from_numpy(x).to(DEV)
+    gd = torch.from_numpy(g).to(DEV)
+    outs = {}
+    for v in (-1, 0, 300, 4000):
+        gate_tuning(v)
+        r = FQ.per_channel_observe_fq(xd, symmetric=False, qmin=0, qmax=255, want_codes=True, want_mask=True)
+        gx = FQ.ste_backward(gd, r["mask"], r["scale"], rowlen)
+        outs[v] = {k: r[k].cpu().numpy() for k in ("y", "codes", "mask", "scale", "zp")}
+        outs[v]["gx"] = gx.cpu().numpy()
+    ref = O.per_channel_observe_fq(x, False, 8, 8)
+    m = G.unpack_mask(outs[0]["mask"], rows, rowlen)
+    want_gx = O.per_channel_backward_fixed(g, ref["mask"], ref["scale"])
+    for v, o in outs.items():
+        G.assert_bitwise_f32(o["y"], ref["y"], f"y gate={v}")
+        assert np.array_equal(o["scale"], ref["scale"]) and np.array_equal(o["zp"], ref["zp"].astype(np.float64))
+        assert np.array_equal(o["codes"].astype(np.int64), ref["x_int"].astype(np.int64))
+        assert np.array_equal(o["mask"], outs[0]["mask"])
+        G.assert_bitwise_f32(o["gx"], want_gx, f"gx gate={v}")
+    assert np.array_equal(m, ref["mask"].reshape(rows, rowlen))

@@ -37,6 +37,7 @@ QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6
 TUNE_OBS_KERNEL, TUNE_OBS_GRID, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 8, 9, 10
+TUNE_STORE_GATE = 11
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 

@@ -452,6 +452,12 @@ void launch_observe_part(bool vec, bool nt, const float *x, int64_t n, double *p
 }
 
 // CU count of the current device (cached; 256 on MI355X)
+int occupancy_blocks(const void *kernel, int block) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, block, 0) != hipSuccess) return 0;
+  return n;
+}
+
 int device_cus() {
   static int cus[64] = {0};
   int dev = 0;
@@ -515,6 +521,10 @@ int vsiq_set_tuning(int key, int value) {
     case VSIQ_TUNE_PC_PACKED:
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.pc_packed = value;
+      return 0;
+    case VSIQ_TUNE_STORE_GATE:
+      if (value < -1 || value > 4000) return VSIQ_E_ARG;
+      g_tune.store_gate = value;
       return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;

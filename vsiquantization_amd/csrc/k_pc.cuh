@@ -21,6 +21,7 @@ struct PCArgs {
   float lo, hi;
   double qden, eps;
   uint32_t defer;      // deferred store phase (defer_stores units), 0 = off
+  uint32_t gate;       // store gate: no stores before workgroup start + gate ticks (10 ns), 0 = off
 };
 
 struct RowSums {
@@ -113,7 +114,8 @@ template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS>
 __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, float rmx,
                                                int64_t row, int par, float *__restrict__ y,
                                                uint8_t *__restrict__ codes,
-                                               uint64_t *__restrict__ mask, const PCArgs &a) {
+                                               uint64_t *__restrict__ mask, const PCArgs &a,
+                                               uint64_t t0 = 0) {
   const int64_t ng = cdiv(a.rowlen, 4);
   float mn = __builtin_inff(), mx = -__builtin_inff();
   uint32_t nan = 0;
@@ -141,6 +143,7 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
     if (MASK) mask_put(mlo, mhi, k, go[k].b);
   }
   if (a.defer) defer_stores(a.defer);   // after pc_row_qparams' barrier
+  if (a.gate) store_gate(t0, a.gate);
   const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -164,6 +167,7 @@ __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ 
                                                       float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
                                                       uint64_t *__restrict__ mask, PCArgs a) {
+  const uint64_t t0 = a.gate ? wall_clock64() : 0;
   const int64_t row0 = (int64_t)blockIdx.x * RPB;
   const int64_t last = a.rows - 1;
   f4 v[RPB][NV];
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ 
   }
   // RPB is 1 or 2; written out because the unroller refuses the (large) loop body
   static_assert(RPB == 1 || RPB == 2, "rows per block");
-  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a);
+  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a, t0);
   if constexpr (RPB == 2) {
     if (row0 + 1 <= last)   // uniform
       pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[RPB - 1], rmn[RPB - 1], rmx[RPB - 1],
@@ -235,17 +239,26 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
 }
 
 
+template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS, int RPB>
+void launch_pc_k(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
+  const auto kern = k_pc_observe_fq<NV, VEC, NT, STATS, MASK, CODES, BS, RPB>;
+  PCArgs b = a;
+  if (RPB == 1 && BS == kBlock && a.gate == kGateAuto) {
+    // one-round grids of >= 2 rows per CU: stores wait for the grid's read phase
+    static const int occ = occupancy_blocks(reinterpret_cast<const void *>(kern), BS);
+    b.gate = store_gate_ticks(a.rows, occ, a.rows * a.rowlen * (int64_t)sizeof(float));
+  } else if (a.gate == kGateAuto) {
+    b.gate = 0;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.rows, RPB)), dim3(BS), 0, st, x, y, c, m, b);
+}
+
 template <int NV, bool VEC, bool NT, bool STATS, int BS, int RPB>
 void launch_pc_rpb(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
-  const dim3 g((unsigned)cdiv(a.rows, RPB)), b(BS);
-  if (c && m)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, true, BS, RPB>), g, b, 0, st, x, y, c, m, a);
-  else if (c)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, true, BS, RPB>), g, b, 0, st, x, y, c, m, a);
-  else if (m)
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, true, false, BS, RPB>), g, b, 0, st, x, y, c, m, a);
-  else
-    hipLaunchKernelGGL((k_pc_observe_fq<NV, VEC, NT, STATS, false, false, BS, RPB>), g, b, 0, st, x, y, c, m, a);
+  if (c && m) launch_pc_k<NV, VEC, NT, STATS, true, true, BS, RPB>(x, y, c, m, a, st);
+  else if (c) launch_pc_k<NV, VEC, NT, STATS, false, true, BS, RPB>(x, y, c, m, a, st);
+  else if (m) launch_pc_k<NV, VEC, NT, STATS, true, false, BS, RPB>(x, y, c, m, a, st);
+  else launch_pc_k<NV, VEC, NT, STATS, false, false, BS, RPB>(x, y, c, m, a, st);
 }
 
 template <int NV, bool VEC, bool NT, bool STATS, int BS>

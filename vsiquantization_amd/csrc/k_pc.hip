@@ -35,6 +35,7 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
   if (rpb <= 0) rpb = 1;
   PCArgs b = a;
   b.defer = (bs == 256 && rpb == 1) ? store_defer_units(a.rows, false) : 0;
+  b.gate = kGateAuto;   // resolved per instantiation (launch_pc_k)
   bool ok = false;
   if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, b, rpb, st);
   else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, b, rpb, st);

@@ -19,7 +19,8 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ pre,
                                                     float *__restrict__ gx, int64_t rowlen,
                                                     uint32_t chunks, const double *__restrict__ sdev,
-                                                    double shost, uint32_t defer) {
+                                                    double shost, uint32_t defer, uint32_t gate) {
+  const uint64_t t0 = gate ? wall_clock64() : 0;
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
   const SteDiv d = make_stediv((float)(sdev ? sdev[row] : shost));
@@ -67,6 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
     __syncthreads();
     defer_stores(defer);
   }
+  if (gate) store_gate(t0, gate);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
@@ -80,15 +82,22 @@ void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *
                     int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
   const int64_t ng = cdiv(rowlen, 4);
   const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
-  const uint32_t defer = chunks9 * kBlock * 9 - ng <= ng / 8 ? store_defer_units(rows * chunks9, true) : 0;
-  if (defer) {
+  const bool fits9 = chunks9 * kBlock * 9 - ng <= ng / 8;
+  uint32_t gate = 0;
+  if (fits9 && g_tune.store_gate > 0) {   // explicit store gate (experiments)
+    static const int occ = occupancy_blocks(reinterpret_cast<const void *>(k_ste_bwd<VEC, NT, ACT, 9>), kBlock);
+    const int64_t bytes = rows * rowlen * (int64_t)(ACT ? 8 : 4) + rows * mask_words_per_row(rowlen) * 8;
+    gate = store_gate_ticks(rows * chunks9, occ, bytes);
+  }
+  const uint32_t defer = fits9 && !gate ? store_defer_units(rows * chunks9, true) : 0;
+  if (defer || gate) {
     hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock), 0, st,
-                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer);
+                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer, gate);
     return;
   }
   const int64_t chunks = oneshot_grid(ng);
   hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, kFlatU>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0,
-                     st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u);
+                     st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u, 0u);
 }
 
 template <int ACT>

@@ -65,7 +65,8 @@ struct Tuning {
   int pc_packed = 1;           // per-channel with given qparams / K6: packed short rows (0 = per-row grid)
   int obs_kernel = 0;          // K2: 0 auto (grid-stride), 1 one-shot, 2 grid-stride
   int obs_grid = 0;            // K2 grid-stride workgroups (0 = kObsGrid)
-  int lsq_groups = 0;          // K4 groups per lane 2 / 4 / 16 (0 = by size)
+  int lsq_groups = 0;          // K4 groups per lane 2 / 4 / 8 / 16 (0 = by size)
+  int store_gate = -1;         // store gate ticks (10 ns) for one-round grids (-1 = auto, 0 = off)
 };
 extern Tuning g_tune;
 
@@ -1020,6 +1021,33 @@ inline bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
 // a wave-uniform unit count (512 clocks each); a pure delay, never a correctness issue.
 __device__ __forceinline__ void defer_stores(uint32_t units) {
   for (uint32_t k = 0; k < units; ++k) __builtin_amdgcn_s_sleep(8);
+}
+
+// Store gate: hold a one-round grid's stores until `ticks` of the constant 100 MHz
+// wall clock have passed since the workgroup started, so that the grid's reads run
+// as one phase and its writes as the next (HBM read/write turnarounds) without
+// delaying the rows that finish reading after the gate (unlike defer_stores).  A
+// pure delay, wave-uniform (scalar clock), never a correctness issue.
+__device__ __forceinline__ void store_gate(uint64_t t0, uint32_t ticks) {
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+// host: store gate of a one-round grid of `grid` workgroups (`occ` resident per CU)
+// reading `read_bytes`: 1.05 x the time the reads take at 7.5 TB/s, in 10 ns ticks
+// (MI355X, tools/exp/gate_bench.py, K3 at 1.0 x: 1024 x 9216 14.4 -> 12.1 us,
+// 2048 x 4608 16.0 -> 13.7, 1280 x 9216 18.7 -> 17.5; the optimum sits at 1.0-1.1 x
+// and falls off steeply below 0.9 -- box-to-box HBM speed varies a few %, hence 1.05;
+// in bench.py's C2 step 14.3 -> 13.7 us).  Grids under 2 workgroups per CU gain nothing; grids of
+// more than one round lose (the next round waits behind the gate).
+// Override: vsiq_set_tuning(VSIQ_TUNE_STORE_GATE, ticks); 0 = off.
+constexpr uint32_t kGateAuto = 0xffffffffu;
+int device_cus();
+int occupancy_blocks(const void *kernel, int block);
+inline uint32_t store_gate_ticks(int64_t grid, int occ, int64_t read_bytes) {
+  if (g_tune.store_gate >= 0) return (uint32_t)g_tune.store_gate;
+  const int64_t cus = device_cus();
+  if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return 0;
+  return (uint32_t)std::min<int64_t>(4000, read_bytes / 71500);
 }
 
 // host: defer_stores units for a one-round grid of `grid` workgroups of 256 lanes x 9
