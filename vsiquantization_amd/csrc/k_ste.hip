@@ -8,7 +8,8 @@ namespace vsiq {
 // (division: ste_quot in vsiq_common.cuh)
 // ----------------------------------------------------------------------------
 // one-shot: workgroup b covers chunk b % chunks of row b / chunks (U groups per lane:
-// kFlatU, or 9 for a one-round grid with a deferred store phase, see defer_stores).
+// kFlatU, or 9 for a one-round grid with a store gate or deferred store phase, see
+// store_gate / defer_stores).
 // A wave's 64 groups are one 256-element mask chunk: its four mask words are
 // wave-uniform, read with scalar loads and used directly as lane masks.
 // ACT (K5): `pre` holds the pre-activation c of a fused ReLU/SiLU; the result is
@@ -84,7 +85,9 @@ void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *
   const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
   const bool fits9 = chunks9 * kBlock * 9 - ng <= ng / 8;
   uint32_t gate = 0;
-  if (fits9 && g_tune.store_gate > 0) {   // explicit store gate (experiments)
+  // one-round grids: store gate (auto; C2 STE 13.3-13.6 -> 12.9-13.0 us in bench.py on
+  // MI355X), else the deferred store phase where that was measured to pay
+  if (fits9 && g_tune.store_gate != 0) {
     static const int occ = occupancy_blocks(reinterpret_cast<const void *>(k_ste_bwd<VEC, NT, ACT, 9>), kBlock);
     const int64_t bytes = rows * rowlen * (int64_t)(ACT ? 8 : 4) + rows * mask_words_per_row(rowlen) * 8;
     gate = store_gate_ticks(rows * chunks9, occ, bytes);
