@@ -236,6 +236,34 @@ for shape, seed in (((3, 4, 8, 8), 21), ((16, 3, 16, 16), 22)):
                 rec.update(zp=0)
             cases.append(rec)
 
+# 4b. calib_grad_scale as a per-channel fp32 tensor (utils/estimate_bn.py:136 sets it on the
+#     activation quantizer): ScaleGradient's tensor-valued gradient (uniform.py:47-53,252-253)
+#     is sum-reduced onto the 0-dim scale / zero point by autograd.
+calib_idx = 0
+for sym, bits in ((True, 8), (False, 8), (True, 4)):
+    g = torch.Generator().manual_seed(40 + calib_idx)
+    x = torch.randn((6, 5, 7, 7), generator=g)
+    gg = torch.randn((6, 5, 7, 7), generator=g)
+    calib = torch.rand(5, generator=g) * 2 + 0.1
+    q = UniformQuantizer(bits, sym)
+    q.calib_grad_scale = calib
+    scale = torch.nn.Parameter(torch.tensor(np.float64(0.04 if bits == 8 else 0.3)))
+    zp = 0 if sym else torch.nn.Parameter(torch.tensor(np.float64(5.0)))
+    xr = x.clone().requires_grad_(True)
+    y = q.quantize(xr, scale, zp, True)
+    y.backward(gg)
+    key = f"lsqc{calib_idx}"
+    calib_idx += 1
+    rec = dict(kind="learnable_fq_calib", key=key, sym=sym, bits=bits, scale=float(scale.detach()),
+               scale_grad=float(scale.grad), calib=put(key + "_calib", calib),
+               x=put(key + "_x", x), g=put(key + "_g", gg), y=put(key + "_y", y),
+               grad_x=put(key + "_gx", xr.grad))
+    if not sym:
+        rec.update(zp=float(zp.detach()), zp_grad=float(zp.grad))
+    else:
+        rec.update(zp=0)
+    cases.append(rec)
+
 # asym + learnable through the manager crashes in the reference (int zp -> torch.round(int)):
 try:
     q = UniformQuantizer(8, False)

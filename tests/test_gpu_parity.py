@@ -130,6 +130,33 @@ def test_golden_learnable(case):
         assert float(zp.grad) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
 
 
+@pytest.mark.parametrize("case", G.cases("learnable_fq_calib"), ids=lambda c: c["key"])
+def test_golden_learnable_calib_grad_scale_tensor(case):
+    """calib_grad_scale as a per-channel device tensor (utils/estimate_bn.py:136): K4's
+    gradients against the reference's (fp32 sum, <= 1e-4) and the f64 closed form."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    qcls = V.UniformQuantizer if case["sym"] else V.LSQQuantizer
+    q = qcls(case["bits"], case["sym"])
+    q.calib_grad_scale = cu(G.arr(case["calib"]))
+    scale = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64, device=DEV))
+    zp = 0 if case["sym"] else torch.nn.Parameter(torch.tensor(case["zp"], dtype=torch.float64, device=DEV))
+    xg = cu(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    y.backward(cu(g))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    # gscale * calib is a float32 tensor product (uniform.py:48), then summed (sum_to)
+    gs = float((np.float32(O.grad_scale(qmax, x.size)) * G.arr(case["calib"])).astype(np.float64).sum())
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax, gs,
+                                              learn_zp=not case["sym"])
+    assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+    if not case["sym"]:
+        assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
+        assert float(zp.grad) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
+
+
 def test_asym_learnable_int_zero_point_raises_like_reference():
     q = V.UniformQuantizer(8, False)
     s = torch.nn.Parameter(torch.tensor(0.1, dtype=torch.float64, device=DEV))

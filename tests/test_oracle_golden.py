@@ -74,6 +74,23 @@ def test_learnable(case):
         assert gzp == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
 
 
+@pytest.mark.parametrize("case", G.cases("learnable_fq_calib"), ids=lambda c: c["key"])
+def test_learnable_calib_grad_scale_tensor(case):
+    """Per-channel calib_grad_scale tensor (utils/estimate_bn.py:136): the effective
+    gradient factor is (qmax*numel)^-1/2 * sum(calib) (autograd's sum_to onto the 0-dim
+    scale, uniform.py:47-53,252-253); the reference multiplies and sums in fp32."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    calib = float(G.arr(case["calib"]).astype(np.float64).sum())
+    y, gx, gsc, gzp = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                             O.grad_scale(qmax, x.size, calib), learn_zp=not case["sym"])
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+    assert gsc == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    if not case["sym"]:
+        assert gzp == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
+
+
 def test_asym_learnable_int_zp_raises_in_reference():
     (c,) = G.cases("asym_learnable_int_zp")
     assert c["raises"] == "TypeError"
