@@ -33,10 +33,11 @@ for shp in shapes:
     out = {}
     for rnd in range(ROUNDS):
         for f in fs:
-            assert lib.vsiq_set_tuning(H.TUNE_STORE_GATE, int(f * W.n * 4 / 75000)) == 0
+            # f < 0: the automatic gate (-1)
+            assert lib.vsiq_set_tuning(H.TUNE_STORE_GATE, -1 if f < 0 else int(f * W.n * 4 / 75000)) == 0
             out.setdefault(("fwd", f), []).append(t(lambda i: W.f_fwd(*W.slots[i % SL]["fwd"])))
             # STE: f = 0 -> the default (auto store defer)
-            assert lib.vsiq_set_tuning(H.TUNE_STORE_GATE, int(f * W.n * 4 / 75000) if f else -1) == 0
+            assert lib.vsiq_set_tuning(H.TUNE_STORE_GATE, int(f * W.n * 4 / 75000) if f > 0 else -1) == 0
             out.setdefault(("bwd", f), []).append(t(lambda i: W.f_bwd(*W.slots[i % SL]["bwd"])))
     for k in ("fwd", "bwd"):
         row = "  ".join(f"f{f}:{sorted(out[(k, f)])[len(out[(k, f)]) // 2]:6.2f}" for f in fs)

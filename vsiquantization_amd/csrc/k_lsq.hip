@@ -19,6 +19,10 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o);
   double rec[2], f[2];
   if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
+  if (VSIQ_EXP_K4 & 4) {   // experiment: no arrival / fold (gradient not produced)
+    lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
+    return;
+  }
   const bool last = wave_arrive<LsqFold>(ws, 0, gridDim.x, blockIdx.x, counter, rec, f, [&]() {
     lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);   // wave 0's grad_x, after its arrival
   });
