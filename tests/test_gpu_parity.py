@@ -146,11 +146,21 @@ def test_golden_learnable_calib_grad_scale_tensor(case):
     G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
     G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
     assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    # the factor is cached per tensor version: an in-place update is picked up
+    q.calib_grad_scale.mul_(2.0)
+    xg.grad = None
+    scale.grad = None
+    q.quantize(xg, scale, zp, True).backward(cu(g))
+    assert float(scale.grad) == pytest.approx(2 * case["scale_grad"], rel=1e-4, abs=1e-9)
+    q.calib_grad_scale.mul_(0.5)
+    scale.grad = None
+    if not case["sym"]:
+        zp.grad = None
+    q.quantize(xg, scale, zp, True).backward(cu(g))
     qmin, qmax = O.qrange(case["bits"], case["sym"])
-    # gscale * calib is a float32 tensor product (uniform.py:48), then summed (sum_to)
-    gs = float((np.float32(O.grad_scale(qmax, x.size)) * G.arr(case["calib"])).astype(np.float64).sum())
-    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax, gs,
-                                              learn_zp=not case["sym"])
+    calib = float(G.arr(case["calib"]).astype(np.float64).sum())   # sum_to of ScaleGradient's grad
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                              O.grad_scale(qmax, x.size, calib), learn_zp=not case["sym"])
     assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
     if not case["sym"]:
         assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)

@@ -164,3 +164,20 @@ def test_cpu_compute_is_refused():
     with pytest.raises(Exception) as ei:
         q.quantize(torch.randn(4), 0.1, 0, False)
     assert "MI355X" in str(ei.value) or "HIP" in str(ei.value)
+
+
+def test_calib_grad_scale_factor_cached_per_tensor_version():
+    """calib_grad_scale (utils/estimate_bn.py:136) may be a per-channel tensor: its sum is
+    the effective ScaleGradient factor, read once per tensor / in-place version."""
+    from vsiquantization_amd.quantizers.uniform import _calib_factor
+    q = V.UniformQuantizer(8, True)
+    assert _calib_factor(q) == 1.0
+    c = torch.tensor([0.5, 0.25, 2.0])
+    q.calib_grad_scale = c
+    assert _calib_factor(q) == 2.75
+    c.mul_(2.0)                                  # in-place: new version
+    assert _calib_factor(q) == 5.5
+    q.calib_grad_scale = torch.tensor([1.0, 1.0])
+    assert _calib_factor(q) == 2.0
+    q.calib_grad_scale = 0.5
+    assert _calib_factor(q) == 0.5

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from ..fakequant import PerChannelFQFn, PerChannelLearnFn, per_channel_fake_quant
 from ..utils.registry import register_class
-from .uniform import UniformQuantizer, _reduce_gscale
+from .uniform import UniformQuantizer, _calib_factor
 
 
 _ACTS = {"relu": F.relu, "silu": F.silu}
@@ -37,7 +37,7 @@ class PerChannelUniformQuantizer(UniformQuantizer):
             x = _ACTS[act](x)
         C = x.shape[0]
         if is_learning_scale:
-            gscale = float((self.qmax * x.numel() / C) ** -0.5) * _reduce_gscale(self.calib_grad_scale)
+            gscale = float((self.qmax * x.numel() / C) ** -0.5) * _calib_factor(self)
             learn_zp = isinstance(zero_point, torch.Tensor) and zero_point.requires_grad
             z = zero_point if isinstance(zero_point, torch.Tensor) else torch.full(
                 (C,), float(zero_point), dtype=torch.float64, device=x.device)

@@ -45,13 +45,21 @@ class RoundStraightThrough(torch.autograd.Function):
         return grad
 
 
-def _reduce_gscale(g):
-    """calib_grad_scale may be a per-channel tensor (utils/estimate_bn.py:136); the
-    reference then reduces ScaleGradient's tensor-valued gradient onto the 0-dim
-    scale (sum_to), i.e. the effective factor is the sum."""
-    if isinstance(g, torch.Tensor):
-        return float(g.detach().to(torch.float64).sum().item())
-    return float(g)
+def _calib_factor(q):
+    """Effective ``calib_grad_scale`` factor.  It may be a per-channel tensor
+    (utils/estimate_bn.py:136); the reference then reduces ScaleGradient's tensor-valued
+    gradient onto the 0-dim scale (sum_to, uniform.py:47-53,252-253), i.e. the factor is
+    the sum (here in float64; the reference's fp32 products differ by ~1e-7 relative,
+    inside the 1e-4 parity gate).  Cached per tensor and in-place version, so the host
+    reads a device tensor once after estimate_bn sets it, not on every forward."""
+    c = q.calib_grad_scale
+    if not isinstance(c, torch.Tensor):
+        return float(c)
+    cache = q.__dict__.get("_calib_cache")
+    if cache is None or cache[0] is not c or cache[1] != c._version:
+        cache = (c, c._version, float(c.detach().to(torch.float64).sum().item()))
+        q.__dict__["_calib_cache"] = cache
+    return cache[2]
 
 
 @register_class
@@ -84,7 +92,7 @@ class UniformQuantizer(BaseQuantizer):
         """(gscale, zero_point, learn_zp) of the learnable path for input x (uniform.py:47-53):
         the ScaleGradient factor, and whether the zero point is learned (rounded + clamped
         in the forward, with a gradient)."""
-        gscale = _reduce_gscale(self.calculate_grad_scale(x) * self.calib_grad_scale)
+        gscale = self.calculate_grad_scale(x) * _calib_factor(self)
         learn_zp = not self.symmetric
         if learn_zp and not isinstance(zero_point, torch.Tensor):
             zero_point = self._int_zero_point_learnable(zero_point)
