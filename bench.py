@@ -517,10 +517,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    # VSIQ_BENCH_BACKEND=gloo + ranks sharing one GPU: rehearsal of the N>1 path on a
+    # 1-GPU box only (the driver's multi-GPU runs use RCCL, one GPU per rank)
+    backend = os.environ.get("VSIQ_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local if backend == "nccl" else local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
     from vsiquantization_amd import _hip as H
     for kv in a.tune:

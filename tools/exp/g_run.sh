@@ -2,5 +2,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest rc=$?; grep -E "Error|assert|FAILED" gpurun_out/pytest_gpu.log | head -20; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
+for W in c2 c5; do
+VSIQ_BENCH_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 4 --workload $W > gpurun_out/dist2_$W.log 2>&1 || { echo "$W rc=$?"; tail -30 gpurun_out/dist2_$W.log; exit 1; }
+grep '^{' gpurun_out/dist2_$W.log | cut -c1-400
+done
