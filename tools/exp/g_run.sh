@@ -2,7 +2,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-for W in c2 c5; do
-VSIQ_BENCH_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 4 --workload $W > gpurun_out/dist2_$W.log 2>&1 || { echo "$W rc=$?"; tail -30 gpurun_out/dist2_$W.log; exit 1; }
-grep '^{' gpurun_out/dist2_$W.log | cut -c1-400
+for i in 1 2 3; do
+timeout -k 10 300 python3 -u tools/exp/host_overhead.py > gpurun_out/host_ovh.log 2>&1 || { echo "rc=$?"; tail -20 gpurun_out/host_ovh.log; exit 1; }
+grep -E "learnable fwd\+bwd|trivial" gpurun_out/host_ovh.log
 done

@@ -167,7 +167,17 @@ def ptr(t):
     return None if t is None else c_p(t.data_ptr())
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(device) -> c_p:
+    """torch's current HIP stream on `device` (the raw handle; ~0.3 us instead of the ~2 us
+    of building a torch.cuda.Stream object per launch)."""
+    if _RAW_STREAM is not None:
+        idx = device.index if isinstance(device, torch.device) else device
+        if idx is None:
+            idx = torch.cuda.current_device()
+        return c_p(_RAW_STREAM(idx))
     return c_p(torch.cuda.current_stream(device).cuda_stream)
 
 

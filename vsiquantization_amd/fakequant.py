@@ -376,10 +376,10 @@ def per_channel_observe_fq(x: torch.Tensor, *, symmetric: bool, qmin: int, qmax:
     dev = x.device
     C = x.shape[0] if x.dim() > 0 else 1
     rowlen = x.numel() // max(C, 1)
-    if run_min is None:
-        run_min = torch.zeros(C, dtype=torch.float32, device=dev)
-    if run_max is None:
-        run_max = torch.zeros(C, dtype=torch.float32, device=dev)
+    if run_min is None or run_max is None:   # fresh observer state 0/0 (minmax.py:28-29), one fill
+        state = torch.zeros(2, C, dtype=torch.float32, device=dev)
+        run_min = state[0] if run_min is None else run_min
+        run_max = state[1] if run_max is None else run_max
     if run_min.numel() != C or run_max.numel() != C:
         raise ValueError(f"running state has {run_min.numel()} channels, tensor has {C}")
     y = torch.empty_like(x) if quantize else None

@@ -45,8 +45,8 @@ class PerChannelMinMaxObserver(BaseObserver):
     def _state(self, x):
         C = x.shape[0] if x.dim() > 0 else 1
         if self.run_min is None or self.run_min.numel() != C or self.run_min.device != x.device:
-            self.run_min = torch.zeros(C, dtype=torch.float32, device=x.device)
-            self.run_max = torch.zeros(C, dtype=torch.float32, device=x.device)
+            state = torch.zeros(2, C, dtype=torch.float32, device=x.device)   # one fill
+            self.run_min, self.run_max = state[0], state[1]
         return self.run_min, self.run_max
 
     def reset(self):
