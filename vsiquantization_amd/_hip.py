@@ -209,7 +209,7 @@ def workspace(device, n: int = 0) -> _Workspace:
     (Growing it while a previous launch still reads the old buffer is safe: the caching
     allocator only recycles the old block after work queued on this stream.)"""
     dev = torch.device(device)
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    key = (dev.index, stream_of(dev).value)
     w = _WS.get(key)
     if w is None:
         w = _WS[key] = _Workspace(dev, n)
