@@ -112,3 +112,29 @@ def test_per_channel_store_gate_equals_plain_and_oracle(shape, gate_tuning):
         assert np.array_equal(o["mask"], outs[0]["mask"])
         G.assert_bitwise_f32(o["gx"], want_gx, f"gx gate={v}")
     assert np.array_equal(m, ref["mask"].reshape(rows, rowlen))
+
+
+@pytest.mark.parametrize("n,act", [(6_553_600, None), (6_553_600, "relu"), (13_107_200 + 4, "relu"),
+                                   (4_800_000 + 3, None)])
+def test_per_tensor_fq_store_gate_equals_plain_and_oracle(n, act, gate_tuning):
+    """K1 / K5 forward on one-round 9-groups-per-lane grids with the store gate (auto, forced
+    long) against the plain kFlatU grid (gate off): bit-identical y, codes and 1-bit masks,
+    and y / codes / mask equal to the oracle (quantizers/uniform.py:54-55,95 after
+    modules/fused.py:133's activation)."""
+    rng = np.random.default_rng(n % 1000)
+    c = (rng.standard_normal(n) * 0.3).astype(np.float32)
+    c[::7919] = np.nan
+    cd = torch.from_numpy(c).to(DEV)
+    outs = {}
+    for v in (0, -1, 4000):
+        gate_tuning(v)
+        y, mask, codes = FQ.fake_quant(cd, 0.021, 0, -8, 7, want_mask=True, want_codes=True, act=act)
+        outs[v] = (y.cpu().numpy(), mask.cpu().numpy(), codes.cpu().numpy())
+    for v in (-1, 4000):
+        G.assert_bitwise_f32(outs[v][0], outs[0][0], f"y gate={v}")
+        assert np.array_equal(outs[v][1], outs[0][1]) and np.array_equal(outs[v][2], outs[0][2])
+    yo, qo, mo = O.fq_forward(O.act_forward(c, act), 0.021, 0, -8, 7)
+    G.assert_bitwise_f32(outs[-1][0], yo, "y vs oracle")
+    ok = ~np.isnan(qo)
+    assert np.array_equal(outs[-1][2][ok].astype(np.int64), qo[ok].astype(np.int64))
+    assert np.array_equal(G.unpack_mask(outs[-1][1], 1, n).reshape(-1), mo)

@@ -10,30 +10,34 @@ namespace vsiq {
 // ----------------------------------------------------------------------------
 // K1: y = fq(act(x)), one-shot (kFlatU groups per lane, no loop: exact vmcnt)
 // ----------------------------------------------------------------------------
-template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+// U groups per lane: kFlatU, or 9 for a one-round grid whose stores wait behind the
+// store gate (t0: the workgroup's start on the wall clock; gate 0 = no gate).
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U = kFlatU>
 __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float *__restrict__ y,
                                              uint8_t *__restrict__ codes, uint64_t *__restrict__ mask,
-                                             int64_t n, const QP &p, int64_t blk) {
+                                             int64_t n, const QP &p, int64_t blk, uint64_t t0 = 0,
+                                             uint32_t gate = 0) {
   const int64_t ng = cdiv(n, 4);
-  const int64_t base = blk * kBlock * kFlatU + threadIdx.x;   // lanes chunk-aligned
-  f4 v[kFlatU];
+  const int64_t base = blk * kBlock * U + threadIdx.x;   // lanes chunk-aligned
+  f4 v[U];
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
-  GroupOut go[kFlatU];
+  for (int u = 0; u < U; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+  GroupOut go[U];
   uint32_t mlo = 0, mhi = 0;
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4<ACT>(v[u]), p, base + u * kBlock, n);
     if (MASK) mask_put(mlo, mhi, u, go[u].b);
   }
+  if (gate) store_gate(t0, gate);
   const int lane = threadIdx.x % kWave;
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
     if (i - lane >= ng) break;   // whole wave past the end (uniform)
     fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[u]);
   }
-  if (MASK && lane < 4 * kFlatU) {   // lane 4u+j: word j of slot u's chunk
+  if (MASK && lane < 4 * U) {   // lane 4u+j: word j of slot u's chunk
     const int64_t first = base - lane + (lane >> 2) * kBlock;
     if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
   }

@@ -5,27 +5,44 @@
 namespace vsiq {
 
 // K1 kernel: one tensor, block body in k_body.cuh
-template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U>
 __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                    uint8_t *__restrict__ codes,
                                                    uint64_t *__restrict__ mask, int64_t n,
-                                                   QPSrc src) {
+                                                   QPSrc src, uint32_t gate) {
+  const uint64_t t0 = gate ? wall_clock64() : 0;
   const QP p = load_qp(src);
-  fq_fwd_block<VEC, NT, CODES, MASK, ACT>(x, y, codes, mask, n, p, blockIdx.x);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, t0, gate);
+}
+
+// One-round grids of 9 groups per lane with the store gate where that applies
+// (store_gate_ticks: >= 2 workgroups per CU, all resident), else kFlatU groups per lane.
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+void launch_fq_k(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
+                 const QPSrc &src, hipStream_t st) {
+  const int64_t ng = cdiv(n, 4);
+  const int64_t grid9 = cdiv(ng, (int64_t)kBlock * 9);
+  uint32_t gate = 0;
+  if (g_tune.store_gate != 0 && grid9 * kBlock * 9 - ng <= ng / 8) {
+    static const int occ =
+        occupancy_blocks(reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), kBlock);
+    gate = store_gate_ticks(grid9, occ, 4 * n);
+  }
+  if (gate)
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), dim3((unsigned)grid9), dim3(kBlock), 0, st,
+                       x, y, codes, mask, n, src, gate);
+  else
+    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>), dim3((unsigned)oneshot_grid(ng)),
+                       dim3(kBlock), 0, st, x, y, codes, mask, n, src, 0u);
 }
 
 template <int ACT, bool VEC, bool NT>
 void launch_fq_act(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
                    const QPSrc &src, hipStream_t st) {
-  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4))), block(kBlock);
-  if (codes && mask)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, true, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
-  else if (codes)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, true, false, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
-  else if (mask)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, true, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
-  else
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, false, false, ACT>), grid, block, 0, st, x, y, codes, mask, n, src);
+  if (codes && mask) launch_fq_k<VEC, NT, true, true, ACT>(x, y, codes, mask, n, src, st);
+  else if (codes) launch_fq_k<VEC, NT, true, false, ACT>(x, y, codes, mask, n, src, st);
+  else if (mask) launch_fq_k<VEC, NT, false, true, ACT>(x, y, codes, mask, n, src, st);
+  else launch_fq_k<VEC, NT, false, false, ACT>(x, y, codes, mask, n, src, st);
 }
 
 template <int ACT>
