@@ -458,6 +458,18 @@ int occupancy_blocks(const void *kernel, int block) {
   return n;
 }
 
+int device_wall_clock_khz() {
+  static int khz[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 100000;
+  if (!khz[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) != hipSuccess || v <= 0) v = 100000;
+    khz[dev] = v;
+  }
+  return khz[dev];
+}
+
 int device_cus() {
   static int cus[64] = {0};
   int dev = 0;

@@ -1023,11 +1023,12 @@ __device__ __forceinline__ void defer_stores(uint32_t units) {
   for (uint32_t k = 0; k < units; ++k) __builtin_amdgcn_s_sleep(8);
 }
 
-// Store gate: hold a one-round grid's stores until `ticks` of the constant 100 MHz
-// wall clock have passed since the workgroup started, so that the grid's reads run
-// as one phase and its writes as the next (HBM read/write turnarounds) without
-// delaying the rows that finish reading after the gate (unlike defer_stores).  A
-// pure delay, wave-uniform (scalar clock), never a correctness issue.
+// Store gate: hold a one-round grid's stores until `ticks` of the constant wall
+// clock (s_memrealtime, 100 MHz on MI355X) have passed since the workgroup started,
+// so that the grid's reads run as one phase and its writes as the next (HBM
+// read/write turnarounds) without delaying the rows that finish reading after the
+// gate (unlike defer_stores).  A pure delay, wave-uniform (scalar clock), never a
+// correctness issue.
 __device__ __forceinline__ void store_gate(uint64_t t0, uint32_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
@@ -1043,11 +1044,14 @@ __device__ __forceinline__ void store_gate(uint64_t t0, uint32_t ticks) {
 constexpr uint32_t kGateAuto = 0xffffffffu;
 int device_cus();
 int occupancy_blocks(const void *kernel, int block);
+int device_wall_clock_khz();
 inline uint32_t store_gate_ticks(int64_t grid, int occ, int64_t read_bytes) {
   if (g_tune.store_gate >= 0) return (uint32_t)g_tune.store_gate;
   const int64_t cus = device_cus();
   if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return 0;
-  return (uint32_t)std::min<int64_t>(4000, read_bytes / 71500);
+  // 1.05 x read_bytes / 7.5 TB/s in wall-clock ticks (100 MHz on MI355X: bytes / 71500)
+  const double ticks = 1.05 * (double)read_bytes / 7.5e12 * 1e3 * (double)device_wall_clock_khz();
+  return (uint32_t)std::min(40.0 * device_wall_clock_khz() / 1e3, ticks);   // <= 40 us
 }
 
 // host: defer_stores units for a one-round grid of `grid` workgroups of 256 lanes x 9
