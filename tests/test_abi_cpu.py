@@ -37,6 +37,10 @@ def test_abi_version_and_errors():
     assert lib.vsiq_error_string(0) == b"success"
     assert b"invalid" in lib.vsiq_error_string(-1)
     assert lib.vsiq_workspace_doubles(1 << 30) >= 8
+    # room for the largest reducing grid of any kernel / tuning: 2 groups per lane
+    for n in (1, 4099, 21_000_003, 77_070_336):
+        grid = max(2048, -(-(-(-n // 4)) // (256 * 2)))
+        assert lib.vsiq_workspace_doubles(n) >= (grid + 32) * 8, n
 
 
 def test_argument_validation_without_gpu():

@@ -356,7 +356,11 @@ def test_observer_kernels_sizes(n, obs_kernel):
     x = _rand(n, n % 61 + 3, 0.7)
     H.set_tuning(H.TUNE_OBS_KERNEL, obs_kernel)
     try:
-        qp, st = FQ.observe_tensor(cu(x), symmetric=False)
+        side = torch.cuda.Stream()   # a fresh (device, stream) workspace sized for this n only
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            qp, st = FQ.observe_tensor(cu(x), symmetric=False)
+        torch.cuda.current_stream().wait_stream(side)
     finally:
         H.set_tuning(H.TUNE_OBS_KERNEL, 0)
     mn, mx = O.observe_minmax(x)

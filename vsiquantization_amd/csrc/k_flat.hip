@@ -151,11 +151,18 @@ __device__ __forceinline__ void observe_stride(const float *__restrict__ x, int6
     f4 v[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
+    if (b + (int64_t)kBlock * U <= nfull) {
+      // every group of this step is whole (block-uniform): straight-line, no per-group
+      // exec-mask branches (they were ~1/3 of the K2p instruction stream)
 #pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int64_t i = b + threadIdx.x + k * kBlock;
-      if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
-      else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int64_t i = b + threadIdx.x + k * kBlock;
+        if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+        else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+      }
     }
   }
 }
@@ -416,7 +423,14 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
 // K2p groups per lane per step: 8 while the grid reaches 512 workgroups, else fewer so
 // that small layers still spread over >= ~512 workgroups (all CUs issuing; a 1.6M-
 // element layer at 8 per lane was 200 workgroups).  Fixed per n: deterministic.
+#ifndef VSIQ_EXP_PART_U
+#define VSIQ_EXP_PART_U 0          // experiments: force K2p groups per lane
+#endif
+#ifndef VSIQ_EXP_PART_CAP
+#define VSIQ_EXP_PART_CAP VSIQ_PART_MAX_RECORDS   // experiments: K2p grid cap
+#endif
 inline int observe_part_u(int64_t n) {
+  if (VSIQ_EXP_PART_U) return VSIQ_EXP_PART_U;
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);   // lanes' worth of groups
   return units >= 512 * 8 ? 8 : (units >= 512 * 4 ? 4 : 2);
 }
@@ -427,7 +441,7 @@ inline int64_t observe_part_grid(int64_t n) {
   const int u = observe_part_u(n);
   // large tensors: kObsGrid workgroups striding over the tensor; small: one step each
   int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS);
-  cap = std::min<int64_t>(cap, VSIQ_PART_MAX_RECORDS);
+  cap = std::min<int64_t>(cap, VSIQ_EXP_PART_CAP);
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(units, u)));
 }
 
@@ -501,7 +515,9 @@ const char *vsiq_error_string(int code) {
 }
 
 int64_t vsiq_workspace_doubles(int64_t n) {
-  const int64_t g = std::max<int64_t>(kMaxReduceGrid, lsq_grid(cdiv(std::max<int64_t>(n, 0), 4)));
+  // the largest reducing grid any kernel / tuning can use for n: 2 groups per lane (K4
+  // and the one-shot K2 at VSIQ_TUNE_LSQ_GROUPS 2; the one-shot K2 runs K4's 8 as 4)
+  const int64_t g = std::max<int64_t>(kMaxReduceGrid, lsq_grid(cdiv(std::max<int64_t>(n, 0), 4), 2));
   return (g + kArriveGroups) * kPartials;
 }
 
