@@ -1,10 +1,9 @@
 """Worker of tests/test_gpu_dist_calib.py: one rank of a batch-sharded calibration run
 (launched by torch.distributed.run, 2 ranks, gloo, all ranks on cuda:0).
 
-Every rank builds the same 3-layer ConvBnReLU model (seeded), takes its half of every
-calibration batch, runs calibrate_qat_model with the activation observers' dist_group
-set (per-call all-reduce, or deferred records + one sync_calibration), and rank 0
-writes the observer state as JSON to argv[1]."""
+Every rank observes its half of every batch through QuantizationManager.quantize with
+the managers' dist_group set -- per-call all-reduce, or deferred K2p records + one
+sync_calibration -- and rank 0 writes the observer state as JSON to argv[1]."""
 import json
 import os
 import sys
@@ -14,8 +13,8 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from tests.dist_calib_common import DEV, loader, model, state  # noqa: E402
-from vsiquantization_amd.utils.quantize_manager import calibrate_qat_model, data_calib  # noqa: E402
+from tests.dist_calib_common import activations, managers, observe, state  # noqa: E402
+from vsiquantization_amd.distributed import sync_calibration  # noqa: E402
 
 
 def main():
@@ -23,14 +22,19 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
+    acts = activations()
     res = {}
     for mode in ("per_call", "deferred"):
-        m = model()
-        for layer in m:
-            layer.activation_quantizer.dist_group = dist.group.WORLD
-        shard = [(imgs.chunk(world)[rank], t) for imgs, t in loader()]
-        calibrate_qat_model(m, shard, data_calib, DEV, defer_observers=(mode == "deferred"))
-        res[mode] = state(m)
+        mgrs = managers()
+        for qm in mgrs:
+            qm.dist_group = dist.group.WORLD
+            qm.dist_defer = mode == "deferred"
+        observe(mgrs, acts, shard=(rank, world))
+        if mode == "deferred":
+            sync_calibration(torch.nn.ModuleList(mgrs))
+            for qm in mgrs:
+                qm.dist_defer = False
+        res[mode] = state(mgrs)
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)
