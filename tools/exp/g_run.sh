@@ -2,5 +2,5 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_dist_calib.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest rc=$?; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 200 python3 -u tools/exp/codes_bench.py > gpurun_out/codes.log 2>&1 || { echo "rc=$?"; tail gpurun_out/codes.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/codes.log
