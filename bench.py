@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5"], default="c2")
     p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
+    p.add_argument("--bits-w", type=int, default=2, help="C4 weight bits (YAML default 2; SURVEY also w8)")
+    p.add_argument("--bits-a", type=int, default=4, help="C4 activation bits (YAML default 4; SURVEY also a8)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -430,7 +432,7 @@ class C5Calibration:
 
 
 # --------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(workload, seconds):
+def cpu_baseline(workload, seconds, bits=(2, 4)):
     """The reference's eager-torch op sequence (oracle/eager_torch.py) on the host cores."""
     from oracle import eager_torch as E
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -476,10 +478,10 @@ def cpu_baseline(workload, seconds):
 
         def fn():
             for w, gw, c, g in tens:
-                E.lsq_step(w, gw, scale=0.05, bits=2)
-                E.lsq_step(c, g, scale=0.5, bits=4, act="relu")
+                E.lsq_step(w, gw, scale=0.05, bits=bits[0])
+                E.lsq_step(c, g, scale=0.5, bits=bits[1], act="relu")
         n = sum(t[0].numel() + t[2].numel() for t in tens)
-        sample = f"{imgs} of 256 images through all 27 backbone layers (+ weights), fwd+bwd"
+        sample = f"{imgs} of 256 images through all 27 backbone layers (+ weights), w{bits[0]}/a{bits[1]}, fwd+bwd"
     else:
         x = torch.randn(64, 3, 224, 224, generator=gen)
         g = torch.randn(64, 3, 224, 224, generator=gen)
@@ -534,7 +536,7 @@ def main():
         H.set_tuning(int(k), int(v))
 
     if a.workload == "c4":
-        W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch)
+        W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch, bits_w=a.bits_w, bits_a=a.bits_a)
     elif a.workload == "c5":
         W = C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=max(a.steps, a.warmup))
     else:
@@ -620,7 +622,7 @@ def main():
     if a.tune:
         out["config"]["tuning"] = a.tune
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds, bits=(a.bits_w, a.bits_a))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
