@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 5
+#define VSIQ_ABI_VERSION 6
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -178,7 +178,8 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
  * float64 summation order.
  */
 #define VSIQ_PART_LEN 8
-#define VSIQ_PART_MAX_RECORDS 1024   /* vsiq_observe_part_records(n) <= this for every n */
+#define VSIQ_PART_MAX_RECORDS 4096   /* vsiq_observe_part_records(n) <= this for every n
+                                        (one record per wave: at most 1024 workgroups x 4) */
 int64_t vsiq_observe_part_records(int64_t n);
 int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
                               void *stream);

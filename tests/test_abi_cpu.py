@@ -63,12 +63,12 @@ def test_argument_validation_without_gpu():
                                 null, 0, null, null) == -1
     # deferred observer (K2p): record count from n, slot size checked, no-op fold of 0 calls
     assert lib.vsiq_observe_part_records(0) == -1
-    assert lib.vsiq_observe_part_records(1) == 1
-    assert lib.vsiq_observe_part_records(1 << 40) == 512
+    assert lib.vsiq_observe_part_records(1) == 4                    # one record per wave
+    assert lib.vsiq_observe_part_records(1 << 40) == 512 * 4
     assert max(lib.vsiq_observe_part_records(n) for n in range(1, 1 << 24, 4099)) <= H.PART_MAX_RECORDS
-    assert lib.vsiq_observe_part_records(1638400) == 800            # small layers: 2 groups / lane
+    assert lib.vsiq_observe_part_records(1638400) == 800 * 4        # small layers: 2 groups / lane
     assert lib.vsiq_act_observe_part_f32(null, 16, 0, null, 0, null) == -1
-    assert lib.vsiq_act_observe_part_f32(1, 16, 0, 1, H.PART_LEN - 1, null) == -3   # slot too small
+    assert lib.vsiq_act_observe_part_f32(1, 16, 0, 1, 4 * H.PART_LEN - 1, null) == -3   # slot too small
     assert lib.vsiq_act_observe_part_f32(1, 16, 3, 1, 64, null) == -1               # bad activation
     assert lib.vsiq_observe_fold_parts(null, 0, 8, null, null) == 0
     assert lib.vsiq_observe_fold_parts(null, 1, 8, null, null) == -1

@@ -25,14 +25,14 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
 ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)
 ST_LEN = 10
 PART_LEN = 8   # VSIQ_PART_LEN: doubles per K2p partial record
-PART_MAX_RECORDS = 1024   # VSIQ_PART_MAX_RECORDS
+PART_MAX_RECORDS = 4096   # VSIQ_PART_MAX_RECORDS
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6

@@ -212,8 +212,8 @@ __global__ __launch_bounds__(kBlock) void k_observe_loop(const float *__restrict
 }
 
 // K2p: the grid-stride pass of k_observe_loop WITHOUT the cross-workgroup fold.  Each
-// workgroup stores its block record {min, max, nan count, sum|x|, sum x, sum x^2, n,
-// grid} (VSIQ_PART_LEN doubles, plain stores) and exits: no arrival atomics, no
+// wave stores its record {min, max, nan count, sum|x|, sum x, sum x^2, n, records}
+// (VSIQ_PART_LEN doubles, plain stores) and exits: no arrival atomics, no
 // last-block fold, no running update.  For calibration, where nothing consumes an
 // observer's result before the calibration ends: k_observe_fold_parts folds every
 // call's records at once (deferred sync), and the running min/max is replayed there.
@@ -222,11 +222,18 @@ __global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict
                                                           double *__restrict__ parts) {
   ObsAcc a;
   observe_stride<VEC, NT, ACT, U>(x, n, a);
-  obs_block_reduce(a);
-  if (threadIdx.x == 0) {
-    double *r = parts + (int64_t)blockIdx.x * VSIQ_PART_LEN;
+  // one record per WAVE (DPP reductions only): no LDS round trip and no barrier in the
+  // tail of the grid (C5 observe phase 263 -> 253-258 us on MI355X, tools/exp/floor_bench.py)
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  if (threadIdx.x % kWave == 0) {
+    double *r = parts + ((int64_t)blockIdx.x * kWaves + threadIdx.x / kWave) * VSIQ_PART_LEN;
     r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan; r[3] = a.sa;
-    r[4] = a.s1; r[5] = a.s2; r[6] = (double)n; r[7] = (double)gridDim.x;
+    r[4] = a.s1; r[5] = a.s2; r[6] = (double)n; r[7] = (double)gridDim.x * kWaves;
   }
 }
 
@@ -427,7 +434,7 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
 #define VSIQ_EXP_PART_U 0          // experiments: force K2p groups per lane
 #endif
 #ifndef VSIQ_EXP_PART_CAP
-#define VSIQ_EXP_PART_CAP VSIQ_PART_MAX_RECORDS   // experiments: K2p grid cap
+#define VSIQ_EXP_PART_CAP (VSIQ_PART_MAX_RECORDS / kWaves)   // experiments: K2p grid cap
 #endif
 inline int observe_part_u(int64_t n) {
   if (VSIQ_EXP_PART_U) return VSIQ_EXP_PART_U;
@@ -435,12 +442,12 @@ inline int observe_part_u(int64_t n) {
   return units >= 512 * 8 ? 8 : (units >= 512 * 4 ? 4 : 2);
 }
 
-// K2p grid (fixed per n), at most VSIQ_PART_MAX_RECORDS workgroups
+// K2p grid (fixed per n), at most VSIQ_PART_MAX_RECORDS / kWaves workgroups (a record per wave)
 inline int64_t observe_part_grid(int64_t n) {
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
   const int u = observe_part_u(n);
   // large tensors: kObsGrid workgroups striding over the tensor; small: one step each
-  int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS);
+  int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS / kWaves);
   cap = std::min<int64_t>(cap, VSIQ_EXP_PART_CAP);
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(units, u)));
 }
@@ -599,14 +606,14 @@ int vsiq_act_observe_f32(const float *c, int64_t n, int act, double *stats_out, 
 
 int64_t vsiq_observe_part_records(int64_t n) {
   if (n <= 0) return VSIQ_E_ARG;
-  return observe_part_grid(n);
+  return observe_part_grid(n) * kWaves;
 }
 
 int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
                               void *stream) {
   if (n <= 0 || !c || !parts || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
   const int64_t grid = observe_part_grid(n);
-  if (parts_len < grid * VSIQ_PART_LEN) return VSIQ_E_WS;
+  if (parts_len < grid * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
   const bool vec = aligned16(c) && n % 4 == 0;
   VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, (hipStream_t)stream);
   return launch_rc();

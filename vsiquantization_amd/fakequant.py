@@ -324,7 +324,7 @@ def part_slot_doubles(n: int | None = None) -> int:
 
 
 def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) -> torch.Tensor:
-    """Deferred observer pass (K2p): the per-workgroup partial records of act(x) into
+    """Deferred observer pass (K2p): the per-wave partial records of act(x) into
     ``out`` (f64, >= part_slot_doubles(numel) entries; allocated when None), no fold,
     no running update.  Fold with ``fold_parts``."""
     x = H.require_device_f32(x)
