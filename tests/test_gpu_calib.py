@@ -43,8 +43,8 @@ def _state(model):
 def test_async_observers_equal_sync():
     a = _model()
     b = copy.deepcopy(a)
-    calibrate_qat_model(a, _loader(), data_calib, DEV, async_observers=True)
-    calibrate_qat_model(b, _loader(), data_calib, DEV, async_observers=False)
+    calibrate_qat_model(a, _loader(), data_calib, DEV, async_observers=True, defer_observers=False)
+    calibrate_qat_model(b, _loader(), data_calib, DEV, async_observers=False, defer_observers=False)
     sa, sb = _state(a), _state(b)
     assert sa == sb
     assert all(len(s[2]) == 6 for s in sa)
@@ -58,8 +58,8 @@ def test_deferred_calibration_equals_sync():
     reference's running min/max and qparams exactly, and its mean|x| / mean / std lists."""
     a = _model()
     b = copy.deepcopy(a)
-    calibrate_qat_model(a, _loader(), data_calib, DEV, defer_observers=True)
-    calibrate_qat_model(b, _loader(), data_calib, DEV)
+    calibrate_qat_model(a, _loader(), data_calib, DEV)   # default: deferred
+    calibrate_qat_model(b, _loader(), data_calib, DEV, defer_observers=False)
     sa, sb = _state(a), _state(b)
     for x, y in zip(sa, sb):
         assert (x[0], x[1]) == (y[0], y[1])
