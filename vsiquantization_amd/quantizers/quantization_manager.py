@@ -141,6 +141,8 @@ class QuantizationManager(nn.Module):
         (qm.py:55-71)."""
         if self.is_learning_scale or not self.is_observer_qparam:
             return
+        if isinstance(x, torch.Tensor):
+            self._x_device = x.device   # where this layer's tensors live (_home_device)
         if act is not None and not self._act_fusable(x):
             x, act = _ACTS[act](x), None
         if (self.async_observer and not self.is_quantize and self._device_observer(x)
@@ -255,17 +257,37 @@ class QuantizationManager(nn.Module):
         return x
 
     # ------------------------------------------------------------------ learnable qparams
+    def _home_device(self):
+        """Device of the tensors this manager observed (or of its observer state), if any."""
+        dev = self.__dict__.get("_x_device")
+        if dev is not None:
+            return dev
+        st = getattr(self.observer, "_state", None)
+        if isinstance(st, torch.Tensor):
+            return st.device
+        for t in (self.scale, self.zero_point):
+            if isinstance(t, torch.Tensor):
+                return t.device
+        return None
+
     def make_learn_qparameter(self):
-        """scale -> nn.Parameter (qm.py:92-103); float64 when it came from the learn init."""
+        """scale -> nn.Parameter (qm.py:92-103); float64 when it came from the learn init.
+
+        The reference creates it on the CPU and relies on a later ``model.to(device)``; here
+        it is created where the observer state lives, so a model that is not moved again
+        does not read its scale back to the host on every call (and stays graph-capturable)."""
         self._join()
+        dev = self._home_device()
         s = self.scale
         s = s.detach().clone() if isinstance(s, torch.Tensor) else torch.tensor(s)
-        self.scale = nn.Parameter(s, requires_grad=True)
+        self.scale = nn.Parameter(s.to(dev) if dev is not None else s, requires_grad=True)
         learn_zp = (not self.is_symmetric) or getattr(self.quantizer, "learns_zero_point", False)
         if learn_zp:
             z = self.zero_point
             z = (z.detach().to(torch.float64).clone() if isinstance(z, torch.Tensor)
                  else torch.tensor(float(z), dtype=torch.float64))
+            if dev is not None:
+                z = z.to(dev)
             self.zero_point = nn.Parameter(z + 1e-9, requires_grad=True)
         else:
             self.zero_point = 0
