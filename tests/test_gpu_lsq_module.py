@@ -132,3 +132,38 @@ def test_lsq_fake_quantize_axis_mismatch_raises_like_reference():
     fq.disable_observer()
     with pytest.raises(RuntimeError):
         fq(torch.randn(6, 5, 4, 4, device=DEV))    # weights with C_out != C_in
+
+
+@pytest.mark.parametrize("shape,zpl", [((1024, 1024, 3, 3), True), ((256, 128, 3, 3), False),
+                                       ((64, 32, 5, 5), True), ((300, 4000), False), ((40, 1030), True)])
+def test_pc_lsq_axis0_row_resident_equals_two_stage_and_oracle(shape, zpl):
+    """Axis-0 K6 with whole rows in registers (one launch, grad_scale/grad_zp per row
+    written directly, store gate on one-round grids) vs the two-stage records + fold form
+    (VSIQ_TUNE_PC_PACKED 0): grad_x bit for bit, per-channel gradients to float64
+    reordering; both against the oracle (lsq_module.py:134-166 per channel)."""
+    from vsiquantization_amd import _hip as H
+    rng = np.random.default_rng(shape[0] + shape[1])
+    x = (rng.standard_normal(shape) * 0.05).astype(np.float32)
+    g = rng.standard_normal(shape).astype(np.float32)
+    C = shape[0]
+    s = rng.uniform(0.0005, 0.002, C)
+    z = np.rint(rng.uniform(100, 150, C)) + 0.2 if zpl else np.zeros(C)
+    gscale = (255 * x.size / C) ** -0.5
+    sd = torch.tensor(s, dtype=torch.float64, device=DEV)
+    zd = torch.tensor(z, dtype=torch.float64, device=DEV)
+    out = {}
+    try:
+        for mode in (1, 0):
+            H.set_tuning(H.TUNE_PC_PACKED, mode)
+            gx, gs, gz = FQ.pc_lsq_backward(cu(g), cu(x), sd, zd, 0, 255, gscale, zpl, 0)
+            out[mode] = [npy(t) for t in (gx, gs, gz)]
+    finally:
+        H.set_tuning(H.TUNE_PC_PACKED, 1)
+    G.assert_bitwise_f32(out[1][0], out[0][0], "grad_x")
+    np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(out[1][2], out[0][2], rtol=1e-12, atol=1e-15)
+    _, gxo, gso, gzo = O.pc_lsq_forward_backward(x, g, s, z, 0, 255, gscale, axis=0, learn_zp=zpl)
+    G.assert_bitwise_f32(out[1][0], gxo, "grad_x vs oracle")
+    np.testing.assert_allclose(out[1][1], gso, rtol=1e-9, atol=1e-12)
+    if zpl:
+        np.testing.assert_allclose(out[1][2], gzo, rtol=1e-9, atol=1e-12)

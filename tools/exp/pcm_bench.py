@@ -7,6 +7,10 @@ import vsiquantization_amd  # noqa
 from vsiquantization_amd import fakequant as FQ
 
 dev = torch.device("cuda:0")
+from vsiquantization_amd import _hip as H  # noqa: E402
+for kv in os.environ.get("TUNE", "").split():   # e.g. TUNE="11=0 10=0"
+    k, v = kv.split("=")
+    H.set_tuning(int(k), int(v))
 
 
 def t(fn, reps):

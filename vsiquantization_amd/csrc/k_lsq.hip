@@ -228,6 +228,91 @@ __global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict_
   }
 }
 
+// K6 for axis 0 with whole rows in registers (rows == channels, 256 <= groups per row
+// <= 9 x 256): workgroup c holds row c, so the row's {sum t, sum z} is the channel's
+// total -- grad_scale[c] / grad_zp[c] are written directly (no records, no fold
+// launch), and one-round grids store behind the store gate.  Same per-element code
+// (lsq_group_out) as the two-stage form; the f64 sums differ only in order.
+template <bool VEC, bool NT, bool ZPL, int NV>
+__global__ __launch_bounds__(kBlock) void k_pcr_lsq_bwd(const float *__restrict__ g,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ gx, int64_t rowlen,
+                                                        const double *__restrict__ scale,
+                                                        const double *__restrict__ zp, float lo, float hi,
+                                                        double gscale, double *__restrict__ gs_out,
+                                                        double *__restrict__ gz_out, uint32_t gate) {
+  const uint64_t t0 = gate ? wall_clock64() : 0;
+  const int64_t row = blockIdx.x;
+  const QP p = load_qp(QPSrc{nullptr, scale + row, zp ? zp + row : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
+  const int64_t ng = cdiv(rowlen, 4);
+  const float *xr = x + row * rowlen, *gr = g + row * rowlen;
+  float *gxr = gx + row * rowlen;
+  f4 xv[NV], gv[NV], o[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    xv[k] = load_group_c<VEC, NT>(xr, threadIdx.x + k * kBlock, ng, rowlen);
+    gv[k] = load_group_c<VEC, NT>(gr, threadIdx.x + k * kBlock, ng, rowlen);
+  }
+  LsqAcc acc{0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    o[k] = lsq_group_out<ZPL, kActNone>(threadIdx.x + k * kBlock, ng, rowlen, xv[k], gv[k], p, acc);
+  lsq_block_reduce(acc);
+  if (threadIdx.x == 0) {
+    gs_out[row] = acc.t * gscale;
+    if (gz_out) {   // ClampBackward of the rounded zero point (lsq_module.py:339-343)
+      double gz = 0.0;
+      if (ZPL) {
+        const double zr = __builtin_rint(zp ? zp[row] : 0.0);
+        gz = (zr >= (double)lo && zr <= (double)hi) ? acc.z * gscale : 0.0;
+      }
+      gz_out[row] = gz;
+    }
+  }
+  if (gate) store_gate(t0, gate);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t i = threadIdx.x + k * kBlock;
+    if (i < ng) store_group<VEC, NT>(gxr, i, rowlen, o[k]);
+  }
+}
+
+template <bool VEC, bool NT, bool ZPL, int NV>
+void launch_pcr_nv(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                   const double *scale, const double *zp, float lo, float hi, double gscale,
+                   double *gs, double *gz, hipStream_t st) {
+  uint32_t gate = 0;
+  if (g_tune.store_gate != 0) {
+    static const int occ =
+        occupancy_blocks(reinterpret_cast<const void *>(k_pcr_lsq_bwd<VEC, NT, ZPL, NV>), kBlock);
+    gate = store_gate_ticks(rows, occ, 8 * rows * rowlen);
+  }
+  hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV>), dim3((unsigned)rows), dim3(kBlock), 0, st, g, x, gx,
+                     rowlen, scale, zp, lo, hi, gscale, gs, gz, gate);
+}
+
+// rows == channels and whole rows fit 9 groups per lane with >= 1 per lane
+inline bool pcr_fits(int64_t rows, int64_t rowlen, int64_t channels) {
+  const int64_t ng = cdiv(rowlen, 4);
+  return rows == channels && ng >= kBlock && ng <= 9 * kBlock;
+}
+
+template <bool VEC, bool NT>
+void launch_pcr_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                    const double *scale, const double *zp, int zp_learn, float lo, float hi,
+                    double gscale, double *gs, double *gz, hipStream_t st) {
+  const int64_t per_lane = cdiv(cdiv(rowlen, 4), (int64_t)kBlock);
+#define VSIQ_PCR(ZPL)                                                                               \
+  (per_lane <= 1   ? launch_pcr_nv<VEC, NT, ZPL, 1>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st) \
+   : per_lane <= 2 ? launch_pcr_nv<VEC, NT, ZPL, 2>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st) \
+   : per_lane <= 3 ? launch_pcr_nv<VEC, NT, ZPL, 3>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st) \
+   : per_lane <= 5 ? launch_pcr_nv<VEC, NT, ZPL, 5>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st) \
+                   : launch_pcr_nv<VEC, NT, ZPL, 9>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st))
+  if (zp_learn) VSIQ_PCR(true);
+  else VSIQ_PCR(false);
+#undef VSIQ_PCR
+}
+
 template <bool VEC, bool NT>
 void launch_pcp_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                     int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
@@ -298,6 +383,11 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
   hipStream_t st = (hipStream_t)stream;
   const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
   const bool nt = g_tune.nontemporal != 0;
+  if (pcr_fits(rows, rowlen, channels) && g_tune.pc_packed != 0) {   // axis 0, rows in registers
+    VSIQ_B2(launch_pcr_lsq, vec, nt, g, x, gx, rows, rowlen, scale, zp, zp_learn, (float)qmin, (float)qmax,
+            gscale, grad_scale_out, grad_zp_out, st);
+    return launch_rc();
+  }
   if (pc_packed(rowlen) && g_tune.pc_packed != 0)   // one chunk per row: same record layout
     VSIQ_B2(launch_pcp_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
             (float)qmax, ws, st);
