@@ -138,3 +138,31 @@ def test_per_tensor_fq_store_gate_equals_plain_and_oracle(n, act, gate_tuning):
     ok = ~np.isnan(qo)
     assert np.array_equal(outs[-1][2][ok].astype(np.int64), qo[ok].astype(np.int64))
     assert np.array_equal(G.unpack_mask(outs[-1][1], 1, n).reshape(-1), mo)
+
+
+@pytest.mark.parametrize("shape", [(1024, 9216), (700, 4608), (1024, 8000)])
+def test_per_channel_fixed_fq_store_gate_equals_plain_and_oracle(shape, gate_tuning):
+    """Per-channel fake quant with given qparams (PerChannelUniformQuantizer / the
+    learnable per-channel forward) on one-round 9-groups-per-lane grids behind the store
+    gate vs the plain (rows, kFlatU chunks) grid: y, codes and masks bit for bit, and equal
+    to the oracle (quantizers/uniform.py:54-55,95 per row)."""
+    rows, rowlen = shape
+    x, _ = _inputs(rows, rowlen, rows + 3)
+    scales = np.linspace(2e-4, 3e-3, rows)
+    zps = np.rint(np.linspace(100, 150, rows))
+    xd = torch.from_numpy(x).to(DEV)
+    sd = torch.from_numpy(scales).to(DEV)
+    zd = torch.from_numpy(zps).to(DEV)
+    outs = {}
+    for v in (0, -1, 4000):
+        gate_tuning(v)
+        y, mask, codes = FQ.per_channel_fake_quant(xd, sd, zd, 0, 255, want_mask=True, want_codes=True)
+        outs[v] = (y.cpu().numpy(), mask.cpu().numpy(), codes.cpu().numpy())
+    for v in (-1, 4000):
+        G.assert_bitwise_f32(outs[v][0], outs[0][0], f"y gate={v}")
+        assert np.array_equal(outs[v][1], outs[0][1]) and np.array_equal(outs[v][2], outs[0][2])
+    for r in (0, rows // 2, rows - 1):
+        yo, qo, mo = O.fq_forward(x[r], float(scales[r]), float(zps[r]), 0, 255)
+        G.assert_bitwise_f32(outs[-1][0][r], yo, f"y row {r}")
+        assert np.array_equal(outs[-1][2][r].astype(np.int64), qo.astype(np.int64))
+        assert np.array_equal(G.unpack_mask(outs[-1][1], rows, rowlen)[r], mo)

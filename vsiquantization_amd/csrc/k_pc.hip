@@ -66,37 +66,41 @@ __device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
   return load_qp(s);
 }
 
-template <bool VEC, bool NT, bool CODES, bool MASK>
+// U groups per lane: kFlatU, or 9 for a one-round grid behind the store gate
+// (gate 0 = none; t0 = the workgroup's start on the wall clock)
+template <bool VEC, bool NT, bool CODES, bool MASK, int U>
 __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
                                                       uint64_t *__restrict__ mask, uint32_t chunks,
-                                                      PCFixed a) {
+                                                      PCFixed a, uint32_t gate) {
+  const uint64_t t0 = gate ? wall_clock64() : 0;
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
   const QP p = pc_fixed_qp(a, row);
   const int64_t ng = cdiv(a.rowlen, 4);
   const float *xr = x + row * a.rowlen;
   float *yr = y + row * a.rowlen;
-  const int64_t base = chunk * kBlock * kFlatU + threadIdx.x;
-  f4 v[kFlatU];
+  const int64_t base = chunk * kBlock * U + threadIdx.x;
+  f4 v[U];
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) v[u] = load_group_c<VEC, NT>(xr, base + u * kBlock, ng, a.rowlen);
-  GroupOut go[kFlatU];
+  for (int u = 0; u < U; ++u) v[u] = load_group_c<VEC, NT>(xr, base + u * kBlock, ng, a.rowlen);
+  GroupOut go[U];
   uint32_t mlo = 0, mhi = 0;
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     go[u] = fq_out_flat<VEC, CODES, MASK>(v[u], p, base + u * kBlock, a.rowlen);
     if (MASK) mask_put(mlo, mhi, u, go[u].b);
   }
+  if (gate) store_gate(t0, gate);
   uint8_t *cr = CODES ? codes + row * a.rowlen : nullptr;
   const int lane = threadIdx.x % kWave;
 #pragma unroll
-  for (int u = 0; u < kFlatU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
     if (i - lane >= ng) break;
     fq_store_out<VEC, NT, CODES>(yr, cr, i, ng, a.rowlen, go[u]);
   }
-  if (MASK && lane < 4 * kFlatU) {
+  if (MASK && lane < 4 * U) {
     const int64_t first = base - lane + (lane >> 2) * kBlock;
     if (first < ng)
       mask[row * mask_words_per_row(a.rowlen) + 4 * (first / kWave) + (lane & 3)] =
@@ -104,17 +108,36 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
   }
 }
 
+// one-round grids of 9 groups per lane behind the store gate where that applies (as K1,
+// k_fq.hip), else (rows, kFlatU chunks)
+template <bool VEC, bool NT, bool CODES, bool MASK>
+void launch_pc_fixed_k(const float *x, float *y, uint8_t *c, uint64_t *m, const PCFixed &a, int64_t rows,
+                       hipStream_t st) {
+  const int64_t ng = cdiv(a.rowlen, 4);
+  const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
+  uint32_t gate = 0;
+  if (g_tune.store_gate != 0 && chunks9 * kBlock * 9 - ng <= ng / 8) {
+    static const int occ =
+        occupancy_blocks(reinterpret_cast<const void *>(k_pc_fq_fwd<VEC, NT, CODES, MASK, 9>), kBlock);
+    gate = store_gate_ticks(rows * chunks9, occ, 4 * rows * a.rowlen);
+  }
+  if (gate) {
+    hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, CODES, MASK, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock),
+                       0, st, x, y, c, m, (uint32_t)chunks9, a, gate);
+    return;
+  }
+  const int64_t chunks = oneshot_grid(ng);
+  hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, CODES, MASK, kFlatU>), dim3((unsigned)(rows * chunks)),
+                     dim3(kBlock), 0, st, x, y, c, m, (uint32_t)chunks, a, 0u);
+}
 
 template <bool VEC, bool NT>
 void launch_pc_fixed(const float *x, float *y, uint8_t *c, uint64_t *m, const PCFixed &a, int64_t rows,
                      hipStream_t st) {
-  const int64_t chunks = oneshot_grid(cdiv(a.rowlen, 4));
-  const dim3 grid((unsigned)(rows * chunks)), block(kBlock);
-  const uint32_t ch = (uint32_t)chunks;
-  if (c && m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, true>), grid, block, 0, st, x, y, c, m, ch, a);
-  else if (c) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, true, false>), grid, block, 0, st, x, y, c, m, ch, a);
-  else if (m) hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, true>), grid, block, 0, st, x, y, c, m, ch, a);
-  else hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, false, false>), grid, block, 0, st, x, y, c, m, ch, a);
+  if (c && m) launch_pc_fixed_k<VEC, NT, true, true>(x, y, c, m, a, rows, st);
+  else if (c) launch_pc_fixed_k<VEC, NT, true, false>(x, y, c, m, a, rows, st);
+  else if (m) launch_pc_fixed_k<VEC, NT, false, true>(x, y, c, m, a, rows, st);
+  else launch_pc_fixed_k<VEC, NT, false, false>(x, y, c, m, a, rows, st);
 }
 
 // ----------------------------------------------------------------------------
