@@ -1,23 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X fake-quant hot path (BASELINE.json metric).
 
-Default workload (config C2, the north-star kernel): per-channel asymmetric int8
+Headline workload (config C2, the north-star kernel): per-channel asymmetric int8
 MinMax observe + fake-quant FORWARD followed by the straight-through BACKWARD on
 a 1024x1024x3x3 fp32 OIHW conv weight, one weight per step:
 
-    fwd  vsiq_pc_observe_fq_f32   read W (4 B) + write Y (4 B) + write mask (1 B)   9 B/elem
-    bwd  vsiq_ste_bwd_f32         read G (4 B) + read mask (1 B) + write dW (4 B)   9 B/elem
+    fwd  vsiq_pc_observe_fq_f32   read W (4 B) + write Y (4 B) + write mask (1 bit)
+    bwd  vsiq_ste_bwd_f32         read G (4 B) + read mask (1 bit) + write dW (4 B)
 
 8 distinct (W, G, Y, mask, dW) slots (8 x 160 MB) rotate so no step is served from
 the 256 MB Infinity Cache.  Launches go straight through the C ABI (the same entry
 points the Python quantizers call), with precomputed arguments, on torch's current
-stream.  HIP events bracket every kernel inside the timed region: their mean gives
+stream.  HIP events bracket the kernels inside the timed region: their mean gives
 each kernel's duration -> roofline.achieved.
 
-  python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3]
+The same JSON line carries, under "configs", the other BASELINE configs measured in
+the same run (C1 per-tensor, C3 LSQ, C4 YOLOv8n backbone, C5 calibration) and
+"batched_act_quant" (north_star's batched activation quant: per-call observe with the
+RCCL exchange + fake quant over a 1024-image batch split across the ranks), plus
+"api_us_per_step" (the C2 step through the public Python API).
 
-For N>1 (torchrun, one process per GPU) every rank processes its own weights (weak
-scaling, no collective on this path); value = elements of all ranks / max time.
+  python bench.py [--gpus N --steps K --warmup W] [--workload c1..c5] [--extras LIST]
+
+--gpus N > 1 without a torchrun environment: this process (which never touches the
+GPU) starts `torch.distributed.run` with N ranks, one GPU each, RCCL, and exits with
+its return code.  Under torchrun, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
@@ -25,6 +32,9 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
+import sys
 import time
 
 import torch
@@ -32,30 +42,63 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ACT_BATCH = 1024        # batched activation quant: images over all ranks
+EXTRA_STEPS = {"c1": (200, 20), "c3": (20, 4), "c4": (8, 2), "c5": (16, 2), "act": (6, 2)}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5"], default="c2")
+    p.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "act"], default="c2")
+    p.add_argument("--extras", default=None,
+                   help="comma list of extra configs in the same line (c1,c3,c4,c5,act; 'none'); "
+                        "default: all of them for the c2 headline, none otherwise")
     p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
     p.add_argument("--bits-w", type=int, default=2, help="C4 weight bits (YAML default 2; SURVEY also w8)")
     p.add_argument("--bits-a", type=int, default=4, help="C4 activation bits (YAML default 4; SURVEY also a8)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-api", action="store_true", help="skip the public-API C2 timing")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU timing budget per config and thread count")
+    p.add_argument("--master-port", type=int, default=0)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher rehearsal without a GPU: ranks join a gloo group and report")
     p.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                    help="experiments: vsiq_set_tuning(KEY, VALUE) before the workload is built "
                         "(keys: include/vsiq.h VSIQ_TUNE_*)")
-    return p.parse_args()
+    a = p.parse_args(argv)
+    if a.extras is None:
+        a.extras = "c1,c3,c4,c5,act" if a.workload == "c2" else ""
+    a.extras = [e for e in a.extras.split(",") if e and e != "none"]
+    bad = [e for e in a.extras if e not in EXTRA_STEPS]
+    if bad:
+        p.error(f"unknown --extras {bad}")
+    return a
+
+
+# --------------------------------------------------------------------------- launcher
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv) -> int:
+    """N ranks under torch.distributed.run as a CHILD process (this process has not
+    touched the GPU, and is not replaced: it waits and returns the child's code)."""
+    port = a.master_port or free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
 
 
 # --------------------------------------------------------------------------- workloads
 class C2PerChannel:
     """Per-channel asym int8 observe+fq fwd + STE bwd on a 1024x1024x3x3 weight."""
 
+    key = "c2"
     name = "C2 per-channel asym int8 MinMax observe+fake-quant fwd + STE bwd"
     shape = (1024, 1024, 3, 3)
     qmin, qmax, sym = 0, 255, False
@@ -65,10 +108,10 @@ class C2PerChannel:
         from vsiquantization_amd.fakequant import qden
         self.H = H
         C = self.shape[0]
-        self.n = n = 1
+        n = 1
         for d in self.shape:
-            self.n *= d
-        n = self.n
+            n *= d
+        self.n = n
         self.rowlen = n // C
         self.slots = []
         lib = H.lib()
@@ -96,6 +139,8 @@ class C2PerChannel:
         # writes dW (per-row qparams/state: 1024 x 24 B, negligible and not counted)
         self.kernels = {"pc_observe_fq_fwd": 8 * n + mbytes, "ste_bwd": 8 * n + mbytes}
 
+    group = property(lambda self: len(self.slots))
+
     def launch(self, i):
         s = self.slots[i % len(self.slots)]
         return self.f_fwd(*s["fwd"]) | self.f_bwd(*s["bwd"])
@@ -115,22 +160,38 @@ class C2PerChannel:
         return rc
 
     def check(self):
-        """Cheap self-check of slot 0 against the observer-free closed form (no oracle import)."""
+        """Slot 0, 64 rows spread over the tensor, against the reference's formulas restated
+        in torch on the host (minmax.py:49-74 in float64, uniform.py:55,95 with IEEE fp32
+        x / s, the STE gradient (g*s)/s): scale, zero point, y and dW bit-exact."""
         s = self.slots[0]
-        x = s["x"].reshape(self.shape[0], -1)
-        mn = torch.clamp(x.min(1).values, max=0.0).double().cpu()
-        mx = torch.clamp(x.max(1).values, min=0.0).double().cpu()
-        scale = (mx - mn) / (255 + 1e-8)   # host f64 division (torch-GPU would use a reciprocal)
-        return bool(torch.equal(scale, s["scale"].cpu()))
+        C = self.shape[0]
+        rows = torch.linspace(0, C - 1, 64).long()
+        x = s["x"].reshape(C, -1)[rows].cpu()
+        g = s["g"].reshape(C, -1)[rows].cpu()
+        mn = torch.clamp(x.min(1).values, max=0.0).double()
+        mx = torch.clamp(x.max(1).values, min=0.0).double()
+        scale = (mx - mn) / (255 + 1e-8)
+        zp = torch.round(-mn / (scale + 1e-8))
+        s32, z32 = scale.float()[:, None], zp.float()[:, None]
+        r = torch.round(x / s32 + z32)
+        q = torch.clamp(r, 0, 255)
+        y = (q - z32) * s32
+        m = (r >= 0) & (r <= 255)
+        gx = torch.where(m, (g * s32) / s32, torch.zeros_like(g))
+        got = lambda k: s[k].reshape(C, -1)[rows].cpu()   # noqa: E731
+        return bool(torch.equal(scale, s["scale"][rows].cpu()) and torch.equal(zp, s["zp"][rows].cpu())
+                    and torch.equal(y.view(torch.int32), got("y").view(torch.int32))
+                    and torch.equal(gx.view(torch.int32), got("gx").view(torch.int32)))
 
 
-class C1PerTensor:
+class C1PerTensor(C2PerChannel):
     """C1: the reference's minimal config -- MinMaxObserver + UniformQuantizer, per-tensor
     symmetric int8, on a 256x256 fp32 weight (observers/minmax.py:76-88 then
     quantizers/uniform.py:34-56): per step one K2 observe (running min/max + f64 qparams
     on the device) and one K1 fake quant reading those qparams by pointer.  65,536
     elements: latency-bound (launch + reduction chain), the GB/s are not the point."""
 
+    key = "c1"
     name = "C1 per-tensor sym int8 MinMax observe + fake-quant fwd, 256x256"
     shape = (256, 256)
 
@@ -158,8 +219,6 @@ class C1PerTensor:
         self.f_bwd = lib.vsiq_fq_fwd_f32
         self.kernels = {"observe": 4 * n, "fq_fwd": 8 * n}
 
-    launch = None   # set below (same group structure as C2: all observes, then all fake quants)
-
     def check(self):
         """Slot 0 against the reference's formulas in torch on the host (IEEE fp32 x / s)."""
         s = self.slots[0]
@@ -170,11 +229,13 @@ class C1PerTensor:
         return bool(torch.equal(s["y"].cpu().view(torch.int32), want.view(torch.int32)))
 
 
-class C3Lsq:
+class C3Lsq(C2PerChannel):
     """LSQ learnable symmetric int8 fwd + STE bwd on a 512x3x224x224 activation."""
 
+    key = "c3"
     name = "C3 LSQ learnable-scale sym int8 fwd + STE/scale-grad bwd"
     shape = (512, 3, 224, 224)
+    scale0 = 0.03
 
     def __init__(self, dev, slots, seed_base):
         from vsiquantization_amd import _hip as H
@@ -188,34 +249,49 @@ class C3Lsq:
         w = H.workspace(dev, n)
         self.ws = w
         self.slots = []
+        self.gscale = (127 * n) ** -0.5
         for i in range(min(slots, 2)):   # 2 slots x 1.2 GB already defeat the MALL
             gen = torch.Generator(device=dev).manual_seed(seed_base + 2 * i)
             x = torch.randn(self.shape, device=dev, generator=gen)
             gen.manual_seed(seed_base + 2 * i + 1)
             g = torch.randn(self.shape, device=dev, generator=gen)
             s = dict(x=x, g=g, y=torch.empty_like(x), gx=torch.empty_like(x),
-                     scale=torch.tensor(0.03, dtype=torch.float64, device=dev),
+                     scale=torch.tensor(self.scale0, dtype=torch.float64, device=dev),
                      grads=torch.empty(2, dtype=torch.float64, device=dev))
             P = {k: H.ptr(v) for k, v in s.items()}
-            gscale = (127 * n) ** -0.5
             s["fwd"] = (P["x"], P["y"], None, None, H.c_i64(n), None, P["scale"], 0.0, None, 0.0, 0, 0,
                         -128, 127, st)
             s["bwd"] = (P["g"], P["x"], P["gx"], H.c_i64(n), P["scale"], 0.0, None, 0.0, 0, -128, 127,
-                        gscale, P["grads"], H.ptr(w.ws), H.c_i64(w.ws_len), H.ptr(w.counter), st)
+                        self.gscale, P["grads"], H.ptr(w.ws), H.c_i64(w.ws_len), H.ptr(w.counter), st)
             self.slots.append(s)
         self.f_fwd = lib.vsiq_fq_fwd_f32
         self.f_bwd = lib.vsiq_lsq_bwd_f32
         self.kernels = {"fq_fwd": 8 * n, "lsq_bwd": 12 * n}
 
-    launch = C2PerChannel.launch
-    launch_group = C2PerChannel.launch_group
-
     def check(self):
-        return True
-
-
-C1PerTensor.launch = C2PerChannel.launch
-C1PerTensor.launch_group = C2PerChannel.launch_group
+        """Slot 0: y and grad_x bit-exact against the reference's formulas in torch on the
+        host over the first 2M elements (uniform.py:55,95, IEEE fp32 x / s; STE (g*s)/s);
+        the scale gradient within 1e-9 of the float64 sums of the reference's fp32
+        autograd terms over the whole tensor (MulBackward g*(q - zp), DivBackward
+        -(mask*g*s)*((x/s)/s), times gscale: SURVEY §8d's closed form)."""
+        s = self.slots[0]
+        k = 1 << 21
+        s32 = torch.tensor(self.scale0, dtype=torch.float64).float()
+        acc, ok = 0.0, True
+        for i0 in range(0, self.n, 1 << 23):
+            x = s["x"].reshape(-1)[i0:i0 + (1 << 23)].cpu()
+            g = s["g"].reshape(-1)[i0:i0 + (1 << 23)].cpu()
+            r = torch.round(x / s32)
+            q = torch.clamp(r, -128, 127)
+            m = (r >= -128) & (r <= 127)
+            gm = torch.where(m, g * s32, torch.zeros_like(g))
+            acc += float((g * q).double().sum()) + float(((-gm) * ((x / s32) / s32)).double().sum())
+            if i0 == 0:
+                y, gx = q * s32, gm / s32
+                ok = (torch.equal(y[:k].view(torch.int32), s["y"].reshape(-1)[:k].cpu().view(torch.int32))
+                      and torch.equal(gx[:k].view(torch.int32), s["gx"].reshape(-1)[:k].cpu().view(torch.int32)))
+        want = acc * self.gscale
+        return bool(ok and abs(float(s["grads"][0]) - want) <= 1e-9 * abs(want))
 
 
 def yolov8n_backbone(img=320, width=(3, 16, 32, 64, 128, 256), depth=(1, 2, 2)):
@@ -244,6 +320,12 @@ def yolov8n_backbone(img=320, width=(3, 16, 32, 64, 128, 256), depth=(1, 2, 2)):
     return layers
 
 
+def _act_ref(c, s32, qmin, qmax):
+    """relu then the reference's fake quant (uniform.py:55,95), torch on the host."""
+    a = torch.relu(c)
+    return torch.clamp(torch.round(a / s32), qmin, qmax) * s32
+
+
 class C4Backbone:
     """C4: the YOLOv8n backbone's 27 ConvBnReLU quantizers at 320x320, batch 256, in the
     learning phase: the 27 learnable weight fake quants as one multi-tensor launch each way
@@ -251,7 +333,9 @@ class C4Backbone:
     learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd).  The conv itself is
     MIOpen and out of scope: synthetic conv outputs of the right shapes stand in for it."""
 
+    key = "c4"
     name = "C4 YOLOv8n backbone ConvBnReLU fake-quant (weights + fused ReLU/act), learnable"
+    group = 4
 
     def __init__(self, dev, slots, seed_base, batch=256, bits_w=2, bits_a=4):
         from vsiquantization_amd import _hip as H
@@ -262,6 +346,7 @@ class C4Backbone:
         self.shape = (batch, 3, 320, 320)
         qw = (-(2 ** (bits_w - 1)), 2 ** (bits_w - 1) - 1)
         qa = (-(2 ** (bits_a - 1)), 2 ** (bits_a - 1) - 1)
+        self.qa = qa
         self.bits = (bits_w, bits_a)
         gen = torch.Generator(device=dev).manual_seed(seed_base)
         self.fwd, self.bwd, self.keep = [], [], []
@@ -339,11 +424,19 @@ class C4Backbone:
         return rc
 
     def check(self):
-        """grad scale of the first activation quantizer is finite and the fused ReLU zeroed
-        the gradient wherever the conv output is negative."""
+        """Layer 0 (the largest activation): the fused ReLU + act fake quant y bit-exact
+        against torch on the host over the first 2M elements; grad zero where the conv
+        output is negative (ReLU backward); every gradient record finite."""
         t = self.keep[0]
+        k = 1 << 21
+        c = t["c"].reshape(-1)[:k].cpu()
+        s32 = t["sa"].cpu().float()
+        y = _act_ref(c, s32, *self.qa)
+        ok = torch.equal(y.view(torch.int32), t["y"].reshape(-1)[:k].cpu().view(torch.int32))
         neg = t["c"] < 0
-        return bool(torch.isfinite(t["grads_a"]).all()) and bool((t["gc"][neg] == 0).all())
+        return bool(ok and (t["gc"][neg] == 0).all()
+                    and all(bool(torch.isfinite(x["grads_a"]).all() and torch.isfinite(x["grads_w"]).all())
+                            for x in self.keep))
 
 
 class C5Calibration:
@@ -359,11 +452,12 @@ class C5Calibration:
     is measured).  min/max are bit-identical to a 1-GPU run (tests/test_dist_gloo.py).
     Synthetic conv outputs stand in for the conv (MIOpen, out of scope)."""
 
+    key = "c5"
     name = "C5 YOLOv8n backbone calibration: fused-ReLU MinMax observers, deferred RCCL sync"
+    group = 16
 
     def __init__(self, dev, slots, seed_base, batch=128, steps=16):
         from vsiquantization_amd import _hip as H
-        from vsiquantization_amd.fakequant import qden
         self.H = H
         lib = H.lib()
         self.st = H.stream_of(dev)
@@ -393,7 +487,11 @@ class C5Calibration:
         return rc
 
     def launch(self, i):
-        return self._observe(i)
+        """One (untimed, warmup) calibration batch, followed by the deferred sync over the
+        batches so far, so that the timed region finds the fold / replay path warm too."""
+        rc = self._observe(i)
+        self._sync(min(self.steps, i + 1))
+        return rc
 
     def _sync(self, k):
         """The deferred sync over the first k batches: one fold launch over every slot,
@@ -406,6 +504,7 @@ class C5Calibration:
         if self.world > 1:
             allreduce_stats(recs)
         self.minmax = replay_minmax_tensor(0.0, 0.0, recs)         # stays on the device
+        self.recs = recs
 
     def launch_group(self, i0, cnt, ev):
         rc = 0
@@ -418,8 +517,8 @@ class C5Calibration:
         return rc
 
     def check(self):
-        """Running min/max after the sync identical on every rank; equal to a direct
-        reduction of the (synthetic) relu(conv output) on one GPU."""
+        """Running min/max after the sync identical on every rank; on one GPU equal to a
+        direct reduction of relu(conv output), and mean|x| within 1e-6 of torch's."""
         self._sync(1)
         mm = torch.stack(self.minmax, dim=-1)
         if self.world > 1:
@@ -428,15 +527,134 @@ class C5Calibration:
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
             return bool(torch.equal(hi, lo))
         ref = [(min(0.0, float(torch.relu(a).min())), max(0.0, float(torch.relu(a).max()))) for a in self.acts]
-        return [tuple(r) for r in mm.tolist()] == ref
+        from vsiquantization_amd import _hip as H
+        ma = [float(torch.relu(a).double().abs().mean()) for a in self.acts]
+        got = self.recs[:, 0, H.ST_SUMABS] / self.recs[:, 0, H.ST_N]
+        close = all(abs(float(v) - w) <= 1e-6 * w for v, w in zip(got, ma))
+        return [tuple(r) for r in mm.tolist()] == ref and close
 
 
-# --------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(workload, seconds, bits=(2, 4)):
-    """The reference's eager-torch op sequence (oracle/eager_torch.py) on the host cores."""
+class ActQuant:
+    """north_star's batched activation quant: the YOLOv8n backbone's 27 activation
+    quantizers in observe + quantize mode (calibrate, then
+    activate_quantizer without learnable qparams) over a batch of 1024 images split
+    across the ranks (1024/N per GPU: strong scaling).  Per layer and call: K2 observe
+    of relu(conv output) (4 B/elem) -> with N > 1 the RCCL all-reduce of the stats record
+    (MAX over [-min, max], SUM over the sums) + vsiq_observe_finalize (running update, f64
+    qparams; QuantizationManager.dist_group, distributed.py) -> K1 fused-ReLU fake quant
+    reading those qparams by pointer (8 B/elem).  Symmetric, observer 8-bit, quantizer
+    4-bit (the YAML default a4 and the observer quirk)."""
+
+    key = "act"
+    name = "batched activation quant: YOLOv8n backbone, per-call MinMax observe (+RCCL) + fake quant, fused ReLU"
+    group = 2
+
+    def __init__(self, dev, world, rank, total_batch=ACT_BATCH, bits=4):
+        from vsiquantization_amd import _hip as H
+        from vsiquantization_amd.fakequant import qden
+        if total_batch % world:
+            raise ValueError(f"batch {total_batch} does not split over {world} ranks")
+        self.H = H
+        lib = H.lib()
+        st = H.stream_of(dev)
+        self.world = world
+        self.batch = total_batch // world
+        self.layers = yolov8n_backbone()
+        self.shape = (self.batch, 3, 320, 320)
+        self.qmin, self.qmax = -(2 ** (bits - 1)), 2 ** (bits - 1) - 1
+        gen = torch.Generator(device=dev).manual_seed(7000 + rank)
+        qd = qden(True, 8, 1e-8)
+        self.L = []
+        for _, co, _, _, h in self.layers:
+            x = torch.randn(self.batch, co, h, h, device=dev, generator=gen)
+            t = dict(x=x, y=torch.empty_like(x), rmm=torch.zeros(2, device=dev),
+                     st=torch.empty(H.ST_LEN, dtype=torch.float64, device=dev),
+                     qp=torch.empty(H.QP_LEN, dtype=torch.float64, device=dev))
+            t["ws"] = torch.empty(lib.vsiq_workspace_doubles(x.numel()), dtype=torch.float64, device=dev)
+            t["cnt"] = torch.zeros(H.COUNTER_WORDS, dtype=torch.int32, device=dev)
+            P = {k: H.ptr(v) for k, v in t.items()}
+            n = H.c_i64(x.numel())
+            loc = world == 1   # one GPU: the observer pass updates the state and writes qparams itself
+            t["obs"] = (P["x"], n, H.ACT_RELU, P["st"], P["rmm"] if loc else None, P["qp"] if loc else None,
+                        1, qd, 1e-8, P["ws"], H.c_i64(t["ws"].numel()), P["cnt"], st)
+            t["fin"] = (P["st"], P["rmm"], P["qp"], 1, qd, 1e-8, st)
+            t["fq"] = (P["x"], P["y"], None, None, n, H.ACT_RELU, P["qp"], None, 0.0, None, 0.0, 0, 0,
+                       self.qmin, self.qmax, st)
+            self.L.append(t)
+        self.f_obs, self.f_fin, self.f_fq = lib.vsiq_act_observe_f32, lib.vsiq_observe_finalize, lib.vsiq_act_fq_fwd_f32
+        self.n = sum(t["x"].numel() for t in self.L)
+        self.slots = [None]
+        self.kernels = {"observe_quant_all_layers": 12 * self.n}
+
+    def launch(self, i):
+        from vsiquantization_amd.distributed import allreduce_stats
+        rc = 0
+        for t in self.L:
+            rc |= self.f_obs(*t["obs"])
+            if self.world > 1:
+                allreduce_stats(t["st"])
+                rc |= self.f_fin(*t["fin"])
+            rc |= self.f_fq(*t["fq"])
+        return rc
+
+    def launch_group(self, i0, cnt, ev):
+        rc = 0
+        ev[0].record()
+        for j in range(cnt):
+            rc |= self.launch(i0 + j)
+        ev[1].record()
+        return rc
+
+    def check(self):
+        """qparams identical on every rank; layer 0's y bit-exact (first 2M elements)
+        against torch on the host with the scale from the global max of relu(x)."""
+        qp = torch.stack([t["qp"] for t in self.L])
+        if self.world > 1:
+            hi, lo = qp.clone(), qp.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            same = bool(torch.equal(hi, lo))
+        else:
+            same = True
+        t = self.L[0]
+        mx = t["x"].max().clamp_min(0.0).reshape(1)
+        if self.world > 1:
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        s32 = torch.tensor(float(mx) / (127 + 1e-8)).float()
+        k = 1 << 21
+        y = _act_ref(t["x"].reshape(-1)[:k].cpu(), s32, self.qmin, self.qmax)
+        return same and bool(torch.equal(y.view(torch.int32), t["y"].reshape(-1)[:k].cpu().view(torch.int32)))
+
+
+# --------------------------------------------------------------------------- CPU baseline (§8d)
+def cpu_thread_counts():
+    """[os.cpu_count(), the CPUs this process may actually use (affinity and cgroup
+    quota), OMP_NUM_THREADS] without duplicates: SURVEY §8d asks for os.cpu_count();
+    on a shared GPU box the usable share can be far smaller, so both are timed."""
+    total = os.cpu_count() or 1
+    usable = total
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    out = [total]
+    for c in (usable, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)):
+        if c and c not in out:
+            out.append(c)
+    return out, total, usable
+
+
+def cpu_workload(workload, bits=(2, 4), frac=1):
+    """(fn, elements, description): the workload as the reference's eager op sequence
+    (oracle/eager_torch.py) on the host -- the WHOLE workload at frac=1, 1/frac of its
+    out-channels / images for the thread-count probe."""
     from oracle import eager_torch as E
-    threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     gen = torch.Generator().manual_seed(0)
     if workload == "c1":
         from oracle.fakequant_np import minmax_qparams
@@ -446,18 +664,21 @@ def cpu_baseline(workload, seconds, bits=(2, 4)):
             mn, mx = E.observe(x)
             s, z = minmax_qparams(mn, mx, True, 8)
             return E.fake_quant(x, s, z, -128, 127)
-        n = x.numel()
-        sample = "the whole 256x256 workload (observe + fake quant per call)"
-    elif workload == "c2":
-        rows = 64   # bounded sample: 64 of the 1024 out-channels (same row length 9216)
+        return fn, x.numel(), "the whole 256x256 workload (observe + fake quant per call)"
+    if workload == "c2":
+        rows = 1024 // frac
         w = torch.randn(rows, 1024, 3, 3, generator=gen) * 0.05
         g = torch.randn(rows, 1024, 3, 3, generator=gen)
-        fn = lambda: E.per_channel_step(w, g, symmetric=False, bits=8)  # noqa: E731
-        n = w.numel()
-        sample = f"{rows} of 1024 out-channels of the 1024x1024x3x3 weight (9216 elem/row), fwd+bwd"
-    elif workload == "c5":
-        imgs = 4   # bounded sample: 4 of the 128 images per GPU, all 27 layers
-
+        return ((lambda: E.per_channel_step(w, g, symmetric=False, bits=8)), w.numel(),
+                f"{rows} of the 1024 out-channels of the 1024x1024x3x3 weight, reference classes looped "
+                "over the out-channels, fwd+bwd")
+    if workload == "c3":
+        imgs = 512 // frac
+        x = torch.randn(imgs, 3, 224, 224, generator=gen)
+        g = torch.randn(imgs, 3, 224, 224, generator=gen)
+        return (lambda: E.lsq_step(x, g)), x.numel(), f"{imgs} of the 512 images of the 512x3x224x224 activation, fwd+bwd"
+    if workload == "c5":
+        imgs = 128 // frac
         acts = [torch.randn(imgs, co, h, h, generator=gen) for _, co, _, _, h in yolov8n_backbone()]
 
         def fn():   # reference calibration per layer: relu, observer (2 .item()), 3 stats
@@ -465,10 +686,10 @@ def cpu_baseline(workload, seconds, bits=(2, 4)):
                 a = torch.relu(c)
                 E.observe(a)
                 a.abs().mean().item(), a.mean().item(), a.std().item()
-        n = sum(t.numel() for t in acts)
-        sample = f"{imgs} of 128 images per GPU through all 27 backbone observers (relu + MinMax + stats)"
-    elif workload == "c4":
-        imgs = 4   # bounded sample: 4 of the 256 images, all 27 layers + their weights
+        return (fn, sum(t.numel() for t in acts),
+                f"{imgs} of the 128 images per GPU of one calibration batch through all 27 observers")
+    if workload == "c4":
+        imgs = 256 // frac
         tens = []
         for cin, cout, k, _, h in yolov8n_backbone():
             tens.append((torch.randn(cout, cin, k, k, generator=gen) * (2.0 / (cin * k * k)) ** 0.5,
@@ -480,31 +701,89 @@ def cpu_baseline(workload, seconds, bits=(2, 4)):
             for w, gw, c, g in tens:
                 E.lsq_step(w, gw, scale=0.05, bits=bits[0])
                 E.lsq_step(c, g, scale=0.5, bits=bits[1], act="relu")
-        n = sum(t[0].numel() + t[2].numel() for t in tens)
-        sample = f"{imgs} of 256 images through all 27 backbone layers (+ weights), w{bits[0]}/a{bits[1]}, fwd+bwd"
-    else:
-        x = torch.randn(64, 3, 224, 224, generator=gen)
-        g = torch.randn(64, 3, 224, 224, generator=gen)
-        fn = lambda: E.lsq_step(x, g)  # noqa: E731
-        n = x.numel()
-        sample = "64 of 512 images of the 512x3x224x224 activation, fwd+bwd"
+        return (fn, sum(t[0].numel() + t[2].numel() for t in tens),
+                f"{imgs} of the 256 images through all 27 backbone layers (+ weights), w{bits[0]}/a{bits[1]}, fwd+bwd")
+    raise ValueError(workload)
+
+
+def _best_time(fn, seconds, max_runs=50):
+    """min wall time of fn over >= 1 timed runs after one warm-up run, within ~seconds."""
+    t0 = time.perf_counter()
     fn()
-    best, t_end, iters = float("inf"), time.perf_counter() + seconds, 0
-    while time.perf_counter() < t_end or iters < 2:
+    t_end = time.perf_counter() + max(seconds - (time.perf_counter() - t0), 0.0)
+    best, iters = float("inf"), 0
+    while iters < 1 or (time.perf_counter() < t_end and iters < max_runs):
         t0 = time.perf_counter()
         fn()
         best = min(best, time.perf_counter() - t0)
         iters += 1
+    return best, iters
+
+
+_THREAD_PLAN = None
+
+
+def thread_plan(seconds=2.0):
+    """Thread counts worth timing the whole workloads at: every count of
+    cpu_thread_counts() (os.cpu_count() first) is probed once on the C1 op sequence
+    (256x256 observe + fake quant: ~10 OpenMP regions); counts whose probe rate is below
+    half of the best are not used for the whole workloads (on a GPU box whose usable CPU
+    share is a fraction of os.cpu_count(), oversubscribed OpenMP regions run ~1000x
+    slower and one whole workload would take minutes).  Returns (counts kept, probe
+    rates Melem/s by count, os.cpu_count(), usable CPUs)."""
+    global _THREAD_PLAN
+    if _THREAD_PLAN is None:
+        counts, total, usable = cpu_thread_counts()
+        fn, n, _ = cpu_workload("c1")
+        prev = torch.get_num_threads()
+        probe = {}
+        for th in counts:
+            progress(f"cpu baseline: thread probe at {th} threads")
+            torch.set_num_threads(th)
+            probe[th] = n / _best_time(fn, seconds, max_runs=20)[0] / 1e6
+        torch.set_num_threads(prev)
+        best = max(probe.values())
+        _THREAD_PLAN = ([th for th in counts if 2 * probe[th] >= best], probe, total, usable)
+    return _THREAD_PLAN
+
+
+def cpu_baseline(workload, seconds, bits=(2, 4)):
+    """The reference's eager-torch op sequence on the host cores: the WHOLE
+    workload, min of N wall times after a warm-up run (within `seconds`, at least one
+    timed run), at each thread count thread_plan() keeps (os.cpu_count() and the usable
+    CPU count are both probed and recorded); value = the best whole-workload rate."""
+    counts, probe, total, usable = thread_plan()
+    fn, n, desc = cpu_workload(workload, bits)
+    prev = torch.get_num_threads()
+    tried, runs = {}, {}
+    for th in counts:
+        progress(f"cpu baseline {workload}: whole workload at {th} threads")
+        torch.set_num_threads(th)
+        t, runs[th] = _best_time(fn, seconds)
+        tried[th] = n / t / 1e6
+    torch.set_num_threads(prev)
+    th = max(tried, key=tried.get)
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:  # noqa: BLE001
         model = platform.processor()
-    return {"value": n / best / 1e6, "unit": "Melem/s", "cores": threads, "kind": "port",
-            "sample": f"{sample}; min of {iters} runs; torch {torch.__version__} CPU, {model}, "
-                      f"os.cpu_count()={os.cpu_count()}"}
+    return {"value": tried[th], "unit": "Melem/s", "cores": int(th), "kind": "port",
+            "sample": f"{desc}; min of {runs[th]} runs at {th} threads; torch {torch.__version__} CPU, {model}",
+            "threads_whole": {str(k): v for k, v in tried.items()},
+            "thread_probe_c1": {str(k): v for k, v in probe.items()},
+            "os_cpu_count": total, "usable_cpus": usable, "cpu_model": model}
 
 
-# --------------------------------------------------------------------------- main
+# --------------------------------------------------------------------------- measurement
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """One line per phase on stderr (long runs must not look hung)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def load_pmc_traffic(workload, kernel):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -514,42 +793,16 @@ def load_pmc_traffic(workload, kernel):
         return None
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # VSIQ_BENCH_BACKEND=gloo + ranks sharing one GPU: rehearsal of the N>1 path on a
-    # 1-GPU box only (the driver's multi-GPU runs use RCCL, one GPU per rank)
-    backend = os.environ.get("VSIQ_BENCH_BACKEND", "nccl")
-    dev = torch.device("cuda", local if backend == "nccl" else local % torch.cuda.device_count())
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
-    from vsiquantization_amd import _hip as H
-    for kv in a.tune:
-        k, v = kv.split("=")
-        H.set_tuning(int(k), int(v))
-
-    if a.workload == "c4":
-        W = C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch, bits_w=a.bits_w, bits_a=a.bits_a)
-    elif a.workload == "c5":
-        W = C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=max(a.steps, a.warmup))
-    else:
-        W = {"c1": C1PerTensor, "c2": C2PerChannel, "c3": C3Lsq}[a.workload](dev, a.slots, 1000 * rank)
-    for i in range(a.warmup):
+def measure(W, steps, warmup, world):
+    """W untimed warmup steps, self-check, then exactly `steps` timed steps between
+    barrier + synchronize on both sides; the max over ranks of the wall time; per-phase
+    HIP-event durations (rank-local) -> roofline of the dominant phase."""
+    for i in range(warmup):
         assert W.launch(i) == 0
-    torch.cuda.synchronize()
-    ok = W.check()
-
-    ns = len(W.slots) if a.workload not in ("c4", "c5") else (4 if a.workload == "c4" else 16)
-    # C4: events around 4 steps' phases; C5: 16 calibration batches, then the deferred sync
-    groups = [(g0, min(ns, a.steps - g0)) for g0 in range(0, a.steps, ns)]
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in groups]
+    names = list(W.kernels)
+    ns = W.group
+    groups = [(g0, min(ns, steps - g0)) for g0 in range(0, steps, ns)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in groups]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -563,71 +816,218 @@ def main():
     dt = time.perf_counter() - t0
     assert rc == 0, f"kernel launch failed rc={rc}"
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
-
-    names = list(W.kernels)
-    dur = {names[0]: sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps * 1e-3,
-           names[1]: sum(e[1].elapsed_time(e[2]) for e in evs) / a.steps * 1e-3}
-    dom = max(dur, key=dur.get)
+    # self-check AFTER the timed region, on the outputs of the timed launches (host work
+    # between warmup and timing would leave the GPU idle right before the timed steps)
+    ok = bool(W.check())
+    if world > 1:
+        t = torch.tensor([int(ok)], device=torch.cuda.current_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    dur = {k: sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps * 1e-3 for i, k in enumerate(names)}
+    dom = max((k for k in names if W.kernels[k] > 0), key=dur.get)
     achieved = W.kernels[dom] / dur[dom] / 1e9
-    traffic = load_pmc_traffic(a.workload, dom)
     per_kernel = {k: {"avg_us": dur[k] * 1e6, "alg_bytes": W.kernels[k],
                       "GBps": W.kernels[k] / dur[k] / 1e9 if dur[k] > 0 else 0.0,
                       "frac": W.kernels[k] / dur[k] / 1e9 / HBM_PEAK_GBS if dur[k] > 0 else 0.0}
                   for k in names}
+    total = W.n * steps * world   # W.n: elements per rank per step (act: its 1/world of the batch)
+    return {"value": total / dt / 1e6, "ms_per_step": dt / steps * 1e3, "self_check": ok,
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": load_pmc_traffic(W.key, dom)},
+            "kernels": per_kernel}
 
-    total_elems = W.n * a.steps * world
-    metrics = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + achieved HBM GB/s vs roofline",
-               "c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
-               "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
-               "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
-                     "HBM GB/s vs roofline",
-               "c5": "Melements/s calibration observer pass (fused ReLU, 27 layers, deferred RCCL "
-                     "sync) + achieved HBM GB/s vs roofline"}
+
+def api_us_per_step(dev, steps=100, warmup=10):
+    """The C2 step through the PUBLIC Python API (what a QAT user runs):
+    PerChannelMinMaxObserver.observe_quantize(W, PerChannelUniformQuantizer(8, False))
+    + backward, fresh gradient per step, host + GPU time per step (µs)."""
+    import vsiquantization_amd as V
+    shape = C2PerChannel.shape
+    gen = torch.Generator(device=dev).manual_seed(11)
+    xs = [(torch.randn(shape, device=dev, generator=gen) * 0.05).requires_grad_(True) for _ in range(4)]
+    g = torch.randn(shape, device=dev, generator=gen)
+    obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+
+    def step(i):
+        x = xs[i % len(xs)]
+        x.grad = None
+        y, _ = obs.observe_quantize(x, q)
+        y.backward(g)
+
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e6
+
+
+METRICS = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + achieved HBM GB/s vs roofline",
+           "c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
+           "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
+           "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
+                 "HBM GB/s vs roofline",
+           "c5": "Melements/s calibration observer pass (fused ReLU, 27 layers, deferred RCCL "
+                 "sync) + achieved HBM GB/s vs roofline",
+           "act": "Melements/s batched activation observe + fake quant (per-call RCCL exchange) + "
+                  "achieved HBM GB/s vs roofline"}
+
+
+def build_workload(key, a, dev, rank, world):
+    if key == "c4":
+        return C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch, bits_w=a.bits_w, bits_a=a.bits_a)
+    if key == "c5":
+        return C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=16)
+    if key == "act":
+        return ActQuant(dev, world, rank)
+    return {"c1": C1PerTensor, "c2": C2PerChannel, "c3": C3Lsq}[key](dev, a.slots, 1000 * rank)
+
+
+def describe(W, key, a, world):
+    cfg = {"workload": W.name, "shape": list(W.shape), "elements_per_step": W.n}
+    if key in ("c1", "c2", "c3"):
+        cfg.update(slots=len(W.slots), parallelism=f"replicas x{world} (independent tensors per rank, "
+                                                   "no collective on this path)")
+    if key == "c4":
+        cfg.update(layers=len(W.layers), bits_w=W.bits[0], bits_a=W.bits[1],
+                   act_elements_per_step=W.n_act, weight_elements_per_step=W.n_w,
+                   parallelism=f"dp x{world} (batch {a.batch} per GPU; quantizer path has no "
+                               "collective, scale grads ride DDP's all-reduce)",
+                   note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
+    if key == "c5":
+        cfg.update(layers=len(W.layers), images_per_gpu_per_batch=128, batches=16,
+                   act_elements_per_batch=W.n,
+                   parallelism=f"dp x{world} (128 images per GPU per batch; deferred observer sync: "
+                               "2 all-reduces per calibration run)",
+                   note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
+    if key == "act":
+        cfg.update(layers=len(W.layers), total_batch=ACT_BATCH, images_per_gpu=W.batch,
+                   elements_per_gpu_per_step=W.n, bits_a=4, observer_bits=8,
+                   parallelism=f"dp x{world} (batch {ACT_BATCH} split over the ranks; per layer one "
+                               "RCCL exchange of the observer stats)" if world > 1 else "1 GPU, no exchange",
+                   note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
+    return cfg
+
+
+def dry_run(a, world, rank):
+    """Launcher rehearsal on the CPU: every rank joins a gloo group and contributes 1."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        ranks = int(t.item())
+        dist.destroy_process_group()
+    else:
+        ranks = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested_gpus": a.gpus, "ranks_joined": ranks}),
+              flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return launch_ranks(a, argv)
+    world = int(env_world or 1)
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch with --nproc-per-node={a.gpus} "
+              "or without torchrun", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        dry_run(a, world, rank)
+        return 0
+    # VSIQ_BENCH_BACKEND=gloo + ranks sharing one GPU: rehearsal of the N>1 path on a
+    # 1-GPU box only (the driver's multi-GPU runs use RCCL, one GPU per rank)
+    backend = os.environ.get("VSIQ_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local if backend == "nccl" else local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+        world = dist.get_world_size()
+    import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
+    from vsiquantization_amd import _hip as H
+    for kv in a.tune:
+        k, v = kv.split("=")
+        H.set_tuning(int(k), int(v))
+    cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
+    bits = (a.bits_w, a.bits_a)
+
+    progress(f"{a.workload}: build")
+    W = build_workload(a.workload, a, dev, rank, world)
+    progress(f"{a.workload}: measure")
+    r = measure(W, a.steps, a.warmup, world)
+    cfg = describe(W, a.workload, a, world)
+    cfg["self_check"] = r["self_check"]
     out = {
-        "metric": metrics[a.workload],
-        "value": total_elems / dt / 1e6,
+        "metric": METRICS[a.workload],
+        "value": r["value"],
         "unit": "Melem/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3,
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.workload == "act" else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (torch.randn, seeded per rank/slot)",
-        "config": {"workload": W.name, "shape": list(W.shape), "elements_per_step": W.n,
-                   "slots": len(W.slots), "parallelism": f"replicas x{world} (independent weights, "
-                                                         "no collective on this path)",
-                   "self_check": ok},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
-        "kernels": per_kernel,
+        "config": cfg,
+        "roofline": r["roofline"],
+        "kernels": r["kernels"],
     }
-    if a.workload == "c4":
-        out["config"].update(layers=len(W.layers), bits_w=W.bits[0], bits_a=W.bits[1],
-                             act_elements_per_step=W.n_act, weight_elements_per_step=W.n_w,
-                             parallelism=f"dp x{world} (batch {a.batch} per GPU; quantizer path has no "
-                                         "collective, scale grads ride DDP's all-reduce)",
-                             note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
-    if a.workload == "c5":
-        out["config"].update(layers=len(W.layers), images_per_gpu_per_batch=128,
-                             batches=a.steps, act_elements_per_batch=W.n,
-                             parallelism=f"dp x{world} (128 images per GPU per batch; deferred "
-                                         "observer sync: 2 all-reduces per calibration run)",
-                             note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
     if a.tune:
         out["config"]["tuning"] = a.tune
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds, bits=(a.bits_w, a.bits_a))
+    del W
+    torch.cuda.empty_cache()
+    if a.workload == "c2" and not a.no_api:
+        progress("c2: public API timing")
+        out["api_us_per_step"] = api_us_per_step(dev)
+        torch.cuda.empty_cache()
+
+    extras = {}
+    for key in a.extras:
+        if key == a.workload:
+            continue
+        steps, warm = EXTRA_STEPS[key]
+        progress(f"{key}: build + measure")
+        Wx = build_workload(key, a, dev, rank, world)
+        rx = measure(Wx, steps, warm, world)
+        extras[key] = {"metric": METRICS[key], "value": rx["value"], "unit": "Melem/s",
+                       "ms_per_step": rx["ms_per_step"], "steps": steps, "warmup": warm,
+                       "scaling": "strong" if key == "act" else "weak",
+                       "config": dict(describe(Wx, key, a, world), self_check=rx["self_check"]),
+                       "roofline": rx["roofline"], "kernels": rx["kernels"]}
+        del Wx
+        torch.cuda.empty_cache()
+    if cpu:
+        # CPU legs after every GPU measurement (host threads do not disturb the timed regions)
+        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds, bits)
+        for key, e in extras.items():
+            if key != "act":
+                e["cpu_baseline"] = cpu_baseline(key, a.cpu_seconds, bits)
+    if "act" in extras:
+        out["batched_act_quant"] = extras.pop("act")
+    if extras:
+        out["configs"] = extras
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -43,10 +43,12 @@ def per_channel_step(w, g, symmetric=False, bits=8):
     qmin, qmax = qrange(bits, symmetric)
     w = w.detach().requires_grad_(True)
     ys = []
-    for c in range(w.shape[0]):
-        mn, mx = observe(w[c].detach())
+    # unbind (not w[c]): its backward stacks the row gradients once, where 1024 SelectBackward
+    # nodes would each scatter into a full-size zero gradient (quadratic in the channel count)
+    for row in w.unbind(0):
+        mn, mx = observe(row.detach())
         s, z = minmax_qparams(mn, mx, symmetric, 8)
-        ys.append(fake_quant(w[c], s, z, qmin, qmax))
+        ys.append(fake_quant(row, s, z, qmin, qmax))
     torch.stack(ys).backward(g)
     return w.grad
 

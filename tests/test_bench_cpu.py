@@ -1,5 +1,13 @@
-"""bench.py host logic (no GPU): workload shapes match SURVEY.md §8 configs."""
+"""bench.py host logic (no GPU): workload shapes match SURVEY.md §8 configs, the N-rank
+launcher, the CPU-baseline thread plan."""
+import json
+import os
+import subprocess
+import sys
+
 import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_yolov8n_backbone_matches_survey_c4():
@@ -8,3 +16,43 @@ def test_yolov8n_backbone_matches_survey_c4():
     assert sum(co * h * h for _, co, _, _, h in layers) == 2_137_600      # act elem / image
     assert sum(ci * co * k * k for ci, co, k, _, _ in layers) == 1_267_632   # weight elems
     assert layers[0] == (3, 16, 3, 2, 160) and layers[-1] == (512, 256, 1, 1, 10)
+
+
+def test_parse_extras_defaults():
+    assert bench.parse([]).extras == ["c1", "c3", "c4", "c5", "act"]          # headline C2: all configs
+    assert bench.parse(["--workload", "c3"]).extras == []
+    assert bench.parse(["--extras", "none"]).extras == []
+    assert bench.parse(["--extras", "c4,act"]).extras == ["c4", "act"]
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_gpus_2_spawns_two_ranks():
+    """--gpus 2 without torchrun: the launcher starts torch.distributed.run with 2 ranks
+    (gloo rehearsal of the rendezvous, no GPU) and rank 0 reports the world size."""
+    p = _run(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out == {"dry_run": True, "n_gpus": 2, "requested_gpus": 2, "ranks_joined": 2}
+
+
+def test_world_size_mismatch_is_an_error():
+    p = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_cpu_thread_counts_start_with_os_cpu_count():
+    counts, total, usable = bench.cpu_thread_counts()
+    assert counts[0] == total == os.cpu_count()
+    assert 1 <= usable <= total and len(set(counts)) == len(counts)
+
+
+def test_cpu_baseline_c1_reports_threads():
+    r = bench.cpu_baseline("c1", 0.2)
+    assert r["kind"] == "port" and r["value"] > 0 and r["unit"] == "Melem/s"
+    assert str(os.cpu_count()) in r["thread_probe_c1"] and str(r["cores"]) in r["threads_whole"]
