@@ -124,3 +124,12 @@ def test_gfx950_code_object_present():
     """The fat binary embeds an amdgcn gfx950 code object."""
     data = open(_build.OUT, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_torch_extension_loads_on_cpu():
+    """_vsiq_torch.so (the C++ autograd nodes) imports without a GPU and is linked to the
+    same ABI as the HIP library."""
+    from vsiquantization_amd import _hip as H
+    ext = H.torch_ext()
+    assert ext.abi_version() == H.ABI_VERSION
+    assert all(hasattr(ext, f) for f in ("pc_observe_fq", "fq_fixed", "fq_learn"))

@@ -1,0 +1,152 @@
+"""The C++ autograd nodes of _vsiq_torch.so (csrc/torch_ops.cpp) against the Python
+autograd.Functions over ctypes (VSIQ_TORCH_EXT=0): same kernels, so every output and
+gradient must be bit-identical.  The rest of the -m gpu suite runs the public API on the
+C++ nodes (the default) against the oracle and the reference goldens."""
+import numpy as np
+import pytest
+import torch
+
+import vsiquantization_amd as V
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd.quantizers.lsq_module import LSQFakeQuantize
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _bits(t):
+    """bit pattern (NaN-safe equality)"""
+    t = t.detach().cpu().contiguous()
+    return t.view({torch.float32: torch.int32, torch.float64: torch.int64}.get(t.dtype, t.dtype))
+
+
+def both(fn, monkeypatch):
+    """fn() under the C++ nodes, then under the Python Functions."""
+    out = []
+    for ext in (True, False):
+        monkeypatch.setattr(H, "torch_ext_enabled", lambda e=ext: e)
+        out.append(fn())
+    monkeypatch.undo()
+    return out
+
+
+def test_extension_loads():
+    ext = H.torch_ext()
+    assert ext.abi_version() == H.ABI_VERSION
+
+
+@pytest.mark.parametrize("shape,sym", [((64, 32, 3, 3), False), ((48, 27), True), ((5, 1000), False),
+                                       ((1024, 1024, 3, 3), False)])
+def test_pc_observe_quantize_ext_equals_python(shape, sym, monkeypatch):
+    g0 = torch.Generator(device=DEV).manual_seed(1)
+    w = torch.randn(shape, device=DEV, generator=g0) * 0.05
+    w[1, 0] = float("nan") if shape[0] > 2 else w[1, 0]
+    g = torch.randn(shape, device=DEV, generator=g0)
+
+    def run():
+        x = w.clone().requires_grad_(True)
+        obs = V.PerChannelMinMaxObserver(sym)
+        y, rs = obs.observe_quantize(x, V.PerChannelUniformQuantizer(8, sym), want_row_stats=True)
+        y.backward(g)
+        return y, x.grad, obs.scale, obs.zero_point, rs, obs.run_min, obs.run_max
+
+    a, b = both(run, monkeypatch)
+    for u, v in zip(a, b):
+        assert torch.equal(_bits(u), _bits(v))
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+@pytest.mark.parametrize("kind", ["float", "cuda", "cpu", "qp"])
+def test_fixed_ext_equals_python(kind, act, monkeypatch):
+    g0 = torch.Generator(device=DEV).manual_seed(2)
+    c = torch.randn(3, 8, 33, 17, device=DEV, generator=g0)
+    g = torch.randn(c.shape, device=DEV, generator=g0)
+    q = V.UniformQuantizer(4, False)
+    scale, zp = 0.071, 5
+    qp = torch.tensor([scale, zp, 0.0, 0.0], dtype=torch.float64, device=DEV)
+
+    def run():
+        x = c.clone().requires_grad_(True)
+        if kind == "qp":
+            y = V.fakequant.fake_quant_fixed(x, None, None, q.qmin, q.qmax, qp=qp, act=act)
+        else:
+            s = {"float": scale, "cuda": torch.tensor(scale, dtype=torch.float64, device=DEV),
+                 "cpu": torch.tensor(scale, dtype=torch.float64)}[kind]
+            y = q.quantize(x, s, zp, False, act=act)
+        y.backward(g)
+        return y, x.grad
+
+    a, b = both(run, monkeypatch)
+    for u, v in zip(a, b):
+        assert torch.equal(_bits(u), _bits(v))
+
+
+@pytest.mark.parametrize("act", [None, "relu"])
+@pytest.mark.parametrize("where", ["cuda", "cpu"])
+@pytest.mark.parametrize("asym", [False, True])
+def test_learnable_ext_equals_python(asym, where, act, monkeypatch):
+    g0 = torch.Generator(device=DEV).manual_seed(3)
+    c = torch.randn(4, 16, 40, 40, device=DEV, generator=g0)
+    g = torch.randn(c.shape, device=DEV, generator=g0)
+    q = V.LSQQuantizer(8, False) if asym else V.UniformQuantizer(8, True)
+
+    def run():
+        x = c.clone().requires_grad_(True)
+        s = torch.nn.Parameter(torch.tensor(0.03, dtype=torch.float64, device=where))
+        z = torch.nn.Parameter(torch.tensor(3.4, dtype=torch.float64, device=where)) if asym else 0
+        y = q.quantize(x, s, z, True, act=act)
+        y.backward(g)
+        out = [y, x.grad, s.grad]
+        if asym:
+            out.append(z.grad)
+        return out
+
+    a, b = both(run, monkeypatch)
+    for u, v in zip(a, b):
+        assert u.device == v.device and u.dtype == v.dtype and u.shape == v.shape
+        assert torch.equal(_bits(u), _bits(v))
+
+
+def test_lsq_fake_quantize_per_tensor_ext_equals_python(monkeypatch):
+    g0 = torch.Generator(device=DEV).manual_seed(4)
+    X = torch.randn(8, 16, 12, 12, device=DEV, generator=g0)
+    g = torch.randn(X.shape, device=DEV, generator=g0)
+
+    def run():
+        torch.manual_seed(0)
+        m = LSQFakeQuantize(learn_scale=True, config_act=True, observer=torch.ao.quantization.MinMaxObserver,
+                            quant_min=0, quant_max=255).to(DEV)
+        x = X.clone().requires_grad_(True)
+        m(x.detach())            # observe -> scale / zp -> scale_param / zero_point_param_float
+        m.disable_observer()
+        y = m(x)
+        y.backward(g)
+        return [y, x.grad] + [p.grad for p in m.parameters() if p.grad is not None]
+
+    a, b = both(run, monkeypatch)
+    assert len(a) == len(b)
+    for u, v in zip(a, b):
+        assert torch.equal(_bits(u), _bits(v))
+
+
+def test_public_api_host_cost_is_low():
+    """The C2 step through the public API on the C++ nodes: one fwd+bwd per weight;
+    reported for information (bench.py's api_us_per_step is the measured figure)."""
+    import time
+    w = (torch.randn(1024, 1024, 3, 3, device=DEV) * 0.05).requires_grad_(True)
+    g = torch.randn_like(w)
+    obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+    for _ in range(10):
+        w.grad = None
+        y, _ = obs.observe_quantize(w, q)
+        y.backward(g)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(100):
+        w.grad = None
+        y, _ = obs.observe_quantize(w, q)
+        y.backward(g)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t) / 100 * 1e6
+    print(f"public API C2 fwd+bwd: {us:.1f} us/step")
+    assert np.isfinite(us)

@@ -24,6 +24,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJDIR = os.path.join(ROOT, "build", "vsiq")
 OUT = os.path.join(HERE, "_vsiq_hip.so")
+TORCH_EXT_SRC = os.path.join(CSRC, "torch_ops.cpp")
+TORCH_EXT_OUT = os.path.join(HERE, "_vsiq_torch.so")
 ARCH = os.environ.get("VSIQ_OFFLOAD_ARCH", "gfx950")
 
 FLAGS = [
@@ -93,5 +95,40 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
     return OUT
 
 
+def needs_torch_ext_build() -> bool:
+    if not os.path.exists(TORCH_EXT_OUT):
+        return True
+    t = os.path.getmtime(TORCH_EXT_OUT)
+    deps = [TORCH_EXT_SRC, OUT, os.path.join(ROOT, "include", "vsiq.h"), os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_torch_ext(force: bool = False, verbose: bool = True) -> str:
+    """`_vsiq_torch.so`: the C++ autograd nodes of csrc/torch_ops.cpp (pybind11 module
+    against torch's headers, host code only), linked to `_vsiq_hip.so` ($ORIGIN rpath)
+    and to torch's own libraries (so the HIP runtime is torch's)."""
+    if not force and not needs_torch_ext_build():
+        return TORCH_EXT_OUT
+    import sysconfig
+
+    import torch
+    import torch.utils.cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda") + [sysconfig.get_paths()["include"],
+                                                   os.path.join(ROOT, "include")]
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    cmd = [hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           "-DTORCH_EXTENSION_NAME=_vsiq_torch", "-Wno-unused-result", "-Wno-deprecated-declarations",
+           *[f"-I{i}" for i in inc], TORCH_EXT_SRC, "-o", TORCH_EXT_OUT + ".tmp",
+           f"-L{tlib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+           f"-L{HERE}", "-l:_vsiq_hip.so", f"-Wl,-rpath,{tlib}", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print("[vsiq build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(TORCH_EXT_OUT + ".tmp", TORCH_EXT_OUT)
+    return TORCH_EXT_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_torch_ext(force="--force" in sys.argv)

@@ -134,6 +134,32 @@ def lib():
     return _LIB
 
 
+_EXT = None
+
+
+def torch_ext_enabled() -> bool:
+    """VSIQ_TORCH_EXT=0 routes the per-call autograd paths through the Python
+    autograd.Functions over ctypes instead (same kernels; tests compare the two)."""
+    return os.environ.get("VSIQ_TORCH_EXT", "1") != "0"
+
+
+def torch_ext():
+    """The C++ autograd nodes (`_vsiq_torch.so`, csrc/torch_ops.cpp); raise if absent."""
+    global _EXT
+    if _EXT is None:
+        lib()   # the HIP library first (ABI check), then the module linked to it
+        try:
+            from . import _vsiq_torch
+        except ImportError as e:
+            raise VsiqError(
+                f"vsiquantization_amd torch extension _vsiq_torch.so missing or not loadable ({e}); "
+                "build it with `python -c 'import __graft_entry__ as g; g.build()'`") from None
+        if _vsiq_torch.abi_version() != ABI_VERSION:
+            raise VsiqError("_vsiq_torch.so was linked against another vsiq ABI; rebuild")
+        _EXT = _vsiq_torch
+    return _EXT
+
+
 def check(rc: int, what: str):
     if rc != 0:
         msg = lib().vsiq_error_string(rc)

@@ -140,10 +140,42 @@ class FakeQuantFixedFn(torch.autograd.Function):
         return gx, None, None, None, None, None, None
 
 
+def _qarg(v):
+    """A scale / zero-point argument as (tensor | None, host float) for the C++ nodes:
+    tensors go through as tensors (the node reads a CUDA one by pointer and keeps the
+    autograd edge of a learnable one), numbers as host floats."""
+    if isinstance(v, torch.Tensor):
+        return v, 0.0
+    if isinstance(v, (numbers.Real, np.floating, np.integer)):
+        return None, float(v)
+    raise TypeError(f"unsupported qparam type {type(v).__name__}")
+
+
 def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None, act=None):
+    """Fixed-qparam fake quant; with a gradient-requiring x, the STE backward is attached
+    (C++ node of _vsiq_torch.so, or FakeQuantFixedFn with VSIQ_TORCH_EXT=0)."""
     if x.requires_grad and torch.is_grad_enabled():
+        if H.torch_ext_enabled():
+            x = H.require_device_f32(x)
+            st, sh = _qarg(scale) if qp is None else (None, 0.0)
+            zt, zh = _qarg(zero_point) if qp is None else (None, 0.0)
+            return H.torch_ext().fq_fixed(x, st, sh, zt, zh, int(qmin), int(qmax), qp, H.act_code(act))
         return FakeQuantFixedFn.apply(x, scale, zero_point, qmin, qmax, qp, act)
     return fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, act=act)[0]
+
+
+def fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
+    """Learnable fake quant (uniform.py:47-56): K1/K5 forward, K4 backward with the
+    ScaleGradient factor ``gscale`` (C++ node of _vsiq_torch.so, or FakeQuantLearnFn
+    with VSIQ_TORCH_EXT=0)."""
+    if H.torch_ext_enabled():
+        x = H.require_device_f32(x)
+        st, sh = _qarg(scale)
+        zt, zh = _qarg(zero_point)
+        w = H.workspace(x.device, x.numel())
+        return H.torch_ext().fq_learn(x, st, sh, zt, zh, int(qmin), int(qmax), float(gscale), bool(learn_zp),
+                                      H.act_code(act), w.ws, w.counter)
+    return FakeQuantLearnFn.apply(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
 
 
 # --------------------------------------------------------------------------- learnable (K4)

@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 
 from .. import _hip as H
-from ..fakequant import PerChannelObserveFQFn, per_channel_observe_fq
+from ..fakequant import PerChannelObserveFQFn, per_channel_observe_fq, qden
 from ..utils.registry import register_class
 from .base import BaseObserver
 
@@ -79,8 +79,14 @@ class PerChannelMinMaxObserver(BaseObserver):
         x = H.require_device_f32(x)
         mn, mx = self._state(x)
         if x.requires_grad and torch.is_grad_enabled():
-            y, s, z, rs = PerChannelObserveFQFn.apply(x, self.symmetric, quantizer.qmin, quantizer.qmax,
-                                                      self.num_bits, self.eps, mn, mx, want_row_stats)
+            if H.torch_ext_enabled():   # C++ autograd node (_vsiq_torch.so)
+                y, s, z, rs = H.torch_ext().pc_observe_fq(x, mn, mx, bool(self.symmetric), int(quantizer.qmin),
+                                                          int(quantizer.qmax),
+                                                          qden(self.symmetric, self.num_bits, self.eps),
+                                                          float(self.eps), bool(want_row_stats))
+            else:
+                y, s, z, rs = PerChannelObserveFQFn.apply(x, self.symmetric, quantizer.qmin, quantizer.qmax,
+                                                          self.num_bits, self.eps, mn, mx, want_row_stats)
             rs = rs if want_row_stats else None
         else:
             r = per_channel_observe_fq(x, symmetric=self.symmetric, qmin=quantizer.qmin,

@@ -25,7 +25,7 @@ from __future__ import annotations
 import torch
 from torch.ao.quantization import FakeQuantize, MovingAverageMinMaxObserver
 
-from ..fakequant import (FakeQuantFixedFn, FakeQuantLearnFn, PerChannelFQFn, PerChannelLearnFn)
+from ..fakequant import PerChannelFQFn, PerChannelLearnFn, fake_quant_fixed, fake_quant_learn
 
 
 class ScaleGradient(torch.autograd.Function):
@@ -124,7 +124,7 @@ class LSQFakeQuantize(FakeQuantize):
             if self.is_per_channel:
                 self._check_channels(X, scale)
                 return PerChannelFQFn.apply(X, scale, zero_point, qmin, qmax, 1)
-            return FakeQuantFixedFn.apply(X, scale, zero_point, qmin, qmax, None, None)
+            return fake_quant_fixed(X, scale, zero_point, qmin, qmax)
         return X
 
     def _check_channels(self, X, param):
@@ -138,7 +138,7 @@ class LSQFakeQuantize(FakeQuantize):
         if self.is_per_channel:
             self._check_channels(X, s)
             return PerChannelLearnFn.apply(X, s, z, qmin, qmax, float(grad_scale), True, 1)
-        return FakeQuantLearnFn.apply(X, s, z, qmin, qmax, float(grad_scale), True, None)
+        return fake_quant_learn(X, s, z, qmin, qmax, float(grad_scale), True)
 
     # ------------------------------------------------------------------ reference pieces
     def calculate_grad_scale(self, quant_tensor):

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import torch
 
-from ..fakequant import FakeQuantLearnFn, fake_quant, fake_quant_fixed
+from ..fakequant import fake_quant, fake_quant_fixed, fake_quant_learn
 from ..utils.registry import register_class
 from .base import BaseQuantizer
 
@@ -86,7 +86,7 @@ class UniformQuantizer(BaseQuantizer):
         if not is_learning_scale:
             return fake_quant_fixed(x, scale, zero_point, self.qmin, self.qmax, act=act)
         gscale, zero_point, learn_zp = self.learn_args(x, zero_point)
-        return FakeQuantLearnFn.apply(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp, act)
+        return fake_quant_learn(x, scale, zero_point, self.qmin, self.qmax, gscale, learn_zp, act)
 
     def learn_args(self, x, zero_point):
         """(gscale, zero_point, learn_zp) of the learnable path for input x (uniform.py:47-53):
