@@ -1,5 +1,6 @@
 """Worker of tests/test_gpu_dist_calib.py: one rank of a batch-sharded calibration run
-(launched by torch.distributed.run, 2 ranks, gloo, all ranks on cuda:0).
+(launched by torch.distributed.run, 2 ranks, gloo, all ranks on cuda:0);
+argv: output path, configuration ("small" / "c5", tests/dist_calib_common.py).
 
 Every rank observes its half of every batch through QuantizationManager.quantize with
 the managers' dist_group set -- per-call all-reduce, or deferred K2p records + one
@@ -13,23 +14,24 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from tests.dist_calib_common import activations, managers, observe, state  # noqa: E402
+from tests.dist_calib_common import Config, activations, managers, observe, state  # noqa: E402
 from vsiquantization_amd.distributed import sync_calibration  # noqa: E402
 
 
 def main():
     out_path = sys.argv[1]
+    cfg = Config(sys.argv[2] if len(sys.argv) > 2 else "small")
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
-    acts = activations()
+    acts = activations(cfg)
     res = {}
     for mode in ("per_call", "deferred"):
-        mgrs = managers()
+        mgrs = managers(cfg)
         for qm in mgrs:
             qm.dist_group = dist.group.WORLD
             qm.dist_defer = mode == "deferred"
-        observe(mgrs, acts, shard=(rank, world))
+        observe(cfg, mgrs, acts, shard=(rank, world))
         if mode == "deferred":
             sync_calibration(torch.nn.ModuleList(mgrs))
             for qm in mgrs:
