@@ -15,6 +15,8 @@ Reference call sites exercised (file:line under /root/reference):
   * quantizers/quantization_manager.py:55-114  collect / quantize / learn-init sequence
   * modules/fused.py:32-134 + modules/fuse.py:45-149  (toy fused model, host structure)
   * modules/fused.py:133 + quantizers/fake_quantize.py:49-50  (F.relu / F.silu, then quantize_out)
+  * modules/fused.py:32-412 (BN fold, fused forward/backward) + modules/fuse.py:45-149 /
+    fuse_config.py:57-149 (fuse_modules_unified structure, child-name config lookup)
 
 Per-channel has no reference class: it is defined as the
 reference classes applied independently to each out-channel slice W[c].
@@ -405,6 +407,231 @@ for per_channel, config_act in ((True, False), (True, True), (False, False), (Fa
                       zp=put(key + "_zp", fq.zero_point_param_float.detach()),
                       scale_grad=put(key + "_sgrad", fq.scale_param.grad),
                       zp_grad=put(key + "_zgrad", fq.zero_point_param_float.grad)))
+
+# ---------------------------------------------------------------------------
+# 8. Fused QAT layers (modules/fused.py:32-412): the BN fold at construction
+#    (fused.py:100-108, 294-300) and one forward + backward through FakeQuantize.forward
+#    (quantizers/fake_quantize.py:43-51) in the observe + quantize mode,
+#    then -- symmetric layers -- the learnable mode after init_scaling_factor_for_learning
+#    + make_learn_qparameter (qm.py:92-114).  The conv / linear itself is the host's
+#    (MIOpen / hipBLASLt on the GPU box: not bitwise), so the intermediates around it
+#    are recorded too: the fake-quantized weight and its gradient, the pre-activation
+#    (the input of F.relu / F.silu, captured in modules.fused's namespace) and its
+#    gradient.  Layers run in eval() (an unfolded BN uses its running statistics).
+# ---------------------------------------------------------------------------
+import copy  # noqa: E402
+
+import torch.nn as nn  # noqa: E402
+import modules.fused as RF  # noqa: E402
+
+
+class _CaptureF:
+    """Stand-in for modules.fused.F recording the pre-activation of F.relu / F.silu."""
+
+    def __init__(self, real):
+        self.real, self.seen = real, []
+
+    def __getattr__(self, k):
+        return getattr(self.real, k)
+
+    def _cap(self, x):
+        x.retain_grad()
+        self.seen.append(x)
+
+    def relu(self, x, *a, **k):
+        self._cap(x)
+        return self.real.relu(x, *a, **k)
+
+    def silu(self, x, *a, **k):
+        self._cap(x)
+        return self.real.silu(x, *a, **k)
+
+
+def _run_fused(m, x, g):
+    """One forward + backward of a reference fused layer; returns the recorded tensors."""
+    cap = _CaptureF(F)
+    wq_seen, a_in = [], []
+    orig_qw, orig_qa = m.quantize_weights, m.quantize_activation
+
+    def qw(w):
+        out = orig_qw(w)
+        out.retain_grad()
+        wq_seen.append(out)
+        return out
+
+    def qa(a):
+        if a.requires_grad:
+            a.retain_grad()
+        a_in.append(a)
+        return orig_qa(a)
+
+    m.quantize_weights, m.quantize_activation = qw, qa
+    RF.F = cap
+    try:
+        xr = x.clone().requires_grad_(True)
+        y = m(xr)
+        y.backward(g)
+    finally:
+        RF.F = F
+        del m.quantize_weights, m.quantize_activation
+    pre = cap.seen[0] if cap.seen else a_in[0]
+    core = m.conv_fuse if hasattr(m, "conv_fuse") else m.linear_fuse
+    out = dict(x=x, y=y, g=g, wq=wq_seen[0], grad_wq=wq_seen[0].grad, pre=pre, grad_pre=pre.grad,
+               grad_x=xr.grad, grad_w=core.weight.grad)
+    if core.bias is not None:
+        out["grad_b"] = core.bias.grad
+    core.weight.grad = None
+    if core.bias is not None:
+        core.bias.grad = None
+    return out
+
+
+def _qstate(qm):
+    s, z = qm.scale, qm.zero_point
+    return dict(scale=float(s.detach()) if isinstance(s, torch.Tensor) else float(s),
+                zp=float(z.detach()) if isinstance(z, torch.Tensor) else float(z))
+
+
+FUSED = [  # (class, conv?, bias, act, is_fuse_bn, w_sym, a_sym, bits_w, bits_a)
+    ("ConvBnReLU", True, False, "relu", True, True, True, 4, 4),
+    ("ConvBnReLU", True, True, "silu", True, True, True, 8, 8),
+    ("ConvBnReLU", True, False, "relu", False, True, True, 2, 4),
+    ("ConvBnReLU", True, True, "relu", True, False, False, 8, 8),
+    ("ConvBn", True, True, None, True, True, True, 8, 4),
+    ("ConvBn", True, False, None, False, True, True, 4, 8),
+    ("ConvReLU", True, True, "relu", None, True, True, 4, 4),
+    ("Conv", True, False, None, None, True, True, 8, 8),
+    ("LinearBnReLU", False, True, "relu", True, True, True, 4, 4),
+    ("LinearBnReLU", False, True, "silu", False, True, True, 8, 8),
+    ("LinearBn", False, True, None, True, True, True, 2, 8),
+]
+fz_idx = 0
+for cls_name, is_conv, bias, act, fuse_bn, w_sym, a_sym, bits_w, bits_a in FUSED:
+    key = f"fz{fz_idx}"
+    torch.manual_seed(800 + fz_idx)
+    if is_conv:
+        core = nn.Conv2d(6, 8, 3, padding=1, bias=bias)
+        bn = nn.BatchNorm2d(8, eps=1e-3)
+        xshape = (2, 6, 9, 9)
+    else:
+        core = nn.Linear(40, 24, bias=bias)
+        bn = nn.BatchNorm1d(24)
+        xshape = (5, 40)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.3, 0.3)
+        bn.running_var.uniform_(0.2, 3.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    act_mod = {"relu": nn.ReLU(), "silu": nn.SiLU(), None: None}[act]
+    names = ("MinMaxObserver", "UniformQuantizer", "MinMaxObserver", "UniformQuantizer")
+    cls = getattr(RF, cls_name)
+    c0, b0 = copy.deepcopy(core), copy.deepcopy(bn)
+    if cls_name in ("ConvBnReLU", "LinearBnReLU"):
+        m = cls(c0, b0, act_mod, *names, w_sym, a_sym, fuse_bn, bits_w, bits_a)
+    elif cls_name in ("ConvBn", "LinearBn"):
+        m = cls(c0, b0, *names, w_sym, a_sym, fuse_bn, bits_w, bits_a)
+    elif cls_name == "ConvReLU":
+        m = cls(c0, act_mod, *names, w_sym, a_sym, bits_w, bits_a)
+    else:
+        m = cls(c0, *names, w_sym, a_sym, bits_w, bits_a)
+    m.eval()
+    lin = m.conv_fuse if is_conv else m.linear_fuse
+    rec = dict(kind="fused_layer", key=key, cls=cls_name, conv=is_conv, bias=bias, act=act,
+               is_fuse_bn=fuse_bn, w_sym=w_sym, a_sym=a_sym, bits_w=bits_w, bits_a=bits_a,
+               bn_eps=float(bn.eps), core_w=put(key + "_cw", core.weight), bn_w=put(key + "_bnw", bn.weight),
+               bn_b=put(key + "_bnb", bn.bias), bn_mean=put(key + "_bnm", bn.running_mean),
+               bn_var=put(key + "_bnv", bn.running_var), fold_w=put(key + "_fw", lin.weight))
+    if bias:
+        rec["core_b"] = put(key + "_cb", core.bias)
+    if lin.bias is not None:
+        rec["fold_b"] = put(key + "_fb", lin.bias)
+    gen = torch.Generator().manual_seed(900 + fz_idx)
+    x = torch.randn(xshape, generator=gen)
+    # observe + quantize mode (qm.py:65-90 with is_learning_scale False)
+    for qm in (m.weight_quantizer, m.activation_quantizer):
+        qm.is_learning_scale = False
+    with torch.no_grad():
+        yshape = m(x).shape
+    for qm in (m.weight_quantizer, m.activation_quantizer):   # forget the shape probe
+        qm.observer.min_val, qm.observer.max_val = 0, 0
+        qm.mean_abs_x, qm.mean_x, qm.std = [], [], []
+    g = torch.randn(yshape, generator=gen)
+    r = _run_fused(m, x, g)
+    rec["observe"] = dict({k: put(f"{key}_o_{k}", v) for k, v in r.items()},
+                          wq_qp=_qstate(m.weight_quantizer), act_qp=_qstate(m.activation_quantizer))
+    # learnable mode (symmetric layers; asymmetric + learnable raises in the reference, §0.5)
+    if w_sym and a_sym:
+        for qm in (m.weight_quantizer, m.activation_quantizer):
+            qm.is_learning_scale = True
+            qm.init_scaling_factor_for_learning()
+            qm.make_learn_qparameter()
+        inits = dict(w=float(m.weight_quantizer.scale.detach()), a=float(m.activation_quantizer.scale.detach()))
+        x2 = torch.randn(xshape, generator=gen)
+        g2 = torch.randn(yshape, generator=gen)
+        r = _run_fused(m, x2, g2)
+        rec["learn"] = dict({k: put(f"{key}_l_{k}", v) for k, v in r.items()}, init_scale_w=inits["w"],
+                            init_scale_a=inits["a"],
+                            scale_grad_w=float(m.weight_quantizer.scale.grad),
+                            scale_grad_a=float(m.activation_quantizer.scale.grad))
+    cases.append(rec)
+    fz_idx += 1
+
+# ---------------------------------------------------------------------------
+# 9. fuse_modules_unified (modules/fuse.py:45-149, 254-277) on a toy model with a
+#    FuseConfigManager (modules/fuse_config.py:57-149): which children fuse into which
+#    class, with which quantizer settings.  The config lookup uses the CHILD name of the
+#    first fused module (fuse.py:113-114), not its path: the pattern "stem" below
+#    never matches, the pattern "^conv$" does.
+# ---------------------------------------------------------------------------
+from collections import OrderedDict  # noqa: E402
+
+from modules.fuse import fuse_modules_unified  # noqa: E402
+from modules.fuse_config import FuseConfig, FuseConfigManager  # noqa: E402
+
+
+def toy_model():
+    torch.manual_seed(1234)
+    return nn.Sequential(OrderedDict(
+        stem=nn.Sequential(OrderedDict(conv=nn.Conv2d(3, 8, 3, padding=1, bias=False),
+                                       bn=nn.BatchNorm2d(8), act=nn.ReLU())),
+        block=nn.Sequential(OrderedDict(conv1=nn.Conv2d(8, 8, 1), relu1=nn.SiLU(),
+                                        conv2=nn.Conv2d(8, 16, 3, padding=1, bias=False),
+                                        bn2=nn.BatchNorm2d(16))),
+        tail=nn.Sequential(nn.Conv2d(16, 16, 3, padding=1), nn.ReLU(), nn.Conv2d(16, 4, 1)),
+        head=nn.Sequential(OrderedDict(pool=nn.Flatten(), fc=nn.Linear(4 * 8 * 8, 10),
+                                       bn=nn.BatchNorm1d(10), act=nn.ReLU())),
+    ))
+
+
+cm = FuseConfigManager(FuseConfig(bits_w=2, bits_a=4))
+cm.add_layer_config("stem", FuseConfig(bits_w=8, bits_a=8))                    # path: never matches
+cm.add_layer_config("^conv$", FuseConfig(bits_w=4, bits_a=4, w_symmetric=False))
+cm.add_layer_config("conv2", FuseConfig(bits_w=6, bits_a=5, is_fuse_bn=False))
+cm.add_layer_config("^0$", FuseConfig(bits_w=3, bits_a=3))
+cm.add_layer_config("fc", FuseConfig(bits_w=8, bits_a=6, a_symmetric=False))
+model = toy_model()
+toy_sd = {k: v.clone() for k, v in model.state_dict().items()}
+patterns = [["conv", "bn", "relu"], ["conv", "bn"], ["conv", "relu"], ["linear", "bn", "relu"],
+            ["linear", "bn"], ["conv"], ["linear"]]
+fused_model = fuse_modules_unified(model, patterns, is_trace=False, config_manager=cm)
+struct = []
+for name, mod in fused_model.named_modules():
+    ent = dict(name=name, type=type(mod).__name__)
+    if hasattr(mod, "weight_quantizer"):
+        ent.update(bits_w=mod.bits_w, bits_a=mod.bits_a,
+                   w_sym=mod.weight_quantizer.quantizer.symmetric,
+                   a_sym=mod.activation_quantizer.quantizer.symmetric,
+                   qw=type(mod.weight_quantizer.quantizer).__name__,
+                   ow=type(mod.weight_quantizer.observer).__name__,
+                   is_fuse_bn=getattr(mod, "is_fuse_bn", None), has_bn=hasattr(mod, "bn"),
+                   is_relu=getattr(mod, "is_relu", None))
+    struct.append(ent)
+cases.append(dict(kind="fuse_structure", patterns=patterns, structure=struct,
+                  configs={"default": dict(bits_w=2, bits_a=4), "stem": dict(bits_w=8, bits_a=8),
+                           "^conv$": dict(bits_w=4, bits_a=4, w_symmetric=False),
+                           "conv2": dict(bits_w=6, bits_a=5, is_fuse_bn=False),
+                           "^0$": dict(bits_w=3, bits_a=3), "fc": dict(bits_w=8, bits_a=6, a_symmetric=False)},
+                  state_dict={k: put("toy_" + k, v) for k, v in toy_sd.items()}))
 
 np.savez_compressed(os.path.join(OUT, "fakequant_goldens.npz"), **arrays)
 with open(os.path.join(OUT, "cases.json"), "w") as f:
