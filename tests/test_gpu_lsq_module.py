@@ -167,3 +167,40 @@ def test_pc_lsq_axis0_row_resident_equals_two_stage_and_oracle(shape, zpl):
     np.testing.assert_allclose(out[1][1], gso, rtol=1e-9, atol=1e-12)
     if zpl:
         np.testing.assert_allclose(out[1][2], gzo, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_manager_asym_per_channel_learnable_keeps_observer_zp(bits):
+    """Asymmetric PerChannelUniformQuantizer through QuantizationManager: calibrate with
+    PerChannelMinMaxObserver, activate learning -> the [C] scale becomes an f64 Parameter
+    and the observer's per-channel zero points stay as fixed [C] tensors (not 0, which
+    would clamp every negative weight at qmin = 0).  y / grad_w bitwise and the scale
+    gradient <= 1e-9 vs the oracle with those zero points (learn_zp False)."""
+    rng = np.random.default_rng(11 + bits)
+    w = (rng.standard_normal((48, 16, 3, 3)) * 0.05).astype(np.float32)
+    g = rng.standard_normal(w.shape).astype(np.float32)
+    qm = V.QuantizationManager("PerChannelUniformQuantizer", "PerChannelMinMaxObserver", bits, False,
+                               is_learning_scale=False).to(DEV)
+    qm.is_quantize = False
+    qm.quantize(cu(w))                                    # calibration: observe only
+    s0 = npy(qm.scale).astype(np.float64)
+    z0 = npy(qm.zero_point).astype(np.float64)
+    assert z0.shape == (48,) and np.any(z0 > 0)
+    qm.is_quantize = True
+    qm.is_learning_scale = True
+    qm.make_learn_qparameter()
+    assert isinstance(qm.scale, torch.nn.Parameter) and qm.scale.dtype == torch.float64
+    assert isinstance(qm.zero_point, torch.Tensor) and not qm.zero_point.requires_grad
+    np.testing.assert_array_equal(npy(qm.zero_point), z0)
+    wg = cu(w, grad=True)
+    y = qm.quantize(wg)
+    y.backward(cu(g))
+    q = qm.quantizer
+    gscale = (q.qmax * w.size / 48) ** -0.5
+    yo, gxo, gso, _ = O.pc_lsq_forward_backward(w, g, s0, z0, q.qmin, q.qmax, gscale, axis=0,
+                                                learn_zp=False)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(wg.grad), gxo, "grad_w")
+    np.testing.assert_allclose(npy(qm.scale.grad), gso, rtol=1e-9, atol=1e-12)
+    if bits == 8:
+        assert npy(y).min() < 0, "negative weights must survive the asymmetric grid"

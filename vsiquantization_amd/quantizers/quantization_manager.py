@@ -289,6 +289,14 @@ class QuantizationManager(nn.Module):
             if dev is not None:
                 z = z.to(dev)
             self.zero_point = nn.Parameter(z + 1e-9, requires_grad=True)
+        elif (isinstance(self.quantizer, PerChannelUniformQuantizer) and not self.quantizer.symmetric
+              and isinstance(self.zero_point, torch.Tensor) and self.zero_point.dim() == 1):
+            # asymmetric per-channel (build-defined, no reference counterpart): the
+            # reference's hard-coded is_symmetric (qm.py:50) would reset zp to 0 and clamp
+            # every negative weight at qmin = 0; keep the observer's per-channel zero
+            # points as fixed [C] f64 tensors instead (learn them with learns_zero_point)
+            z = self.zero_point.detach().to(torch.float64).clone()
+            self.zero_point = z.to(dev) if dev is not None else z
         else:
             self.zero_point = 0
 
