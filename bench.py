@@ -793,12 +793,37 @@ def load_pmc_traffic(workload, kernel):
         return None
 
 
+def settle_gates(W, cap=4000):
+    """Untimed steps until the store-gate tuner (csrc/gate_tune.hip) has chosen the gate
+    of every one-round launch site this workload uses: each site's first ~100 launches
+    time candidate gates.  A choice of delay only -- results are identical for every gate.
+    Returns (steps run, one dict per tuned site)."""
+    from vsiquantization_amd import _hip as H
+    n = 0
+    while n < cap:   # at least one round, so that every launch site exists
+        for _ in range(8):
+            assert W.launch(n) == 0
+            n += 1
+        torch.cuda.synchronize()
+        if H.gate_tuning_pending() == 0:
+            break
+    sites = []
+    for line in H.gate_report().splitlines():
+        f = line.split()
+        kv = dict(x.split("=") for x in f[1:] if "=" in x)
+        sites.append({"site": f[0], "grid": int(kv["grid"]), "read_bytes": int(kv["bytes"]),
+                      "est_ticks": int(float(kv["est"])), "gate_ticks": int(kv["best"]),
+                      "tuned": kv["done"] == "1"})
+    return n, sites
+
+
 def measure(W, steps, warmup, world):
     """W untimed warmup steps, self-check, then exactly `steps` timed steps between
     barrier + synchronize on both sides; the max over ranks of the wall time; per-phase
     HIP-event durations (rank-local) -> roofline of the dominant phase."""
     for i in range(warmup):
         assert W.launch(i) == 0
+    settle, gate_sites = settle_gates(W)
     names = list(W.kernels)
     ns = W.group
     groups = [(g0, min(ns, steps - g0)) for g0 in range(0, steps, ns)]
@@ -838,7 +863,8 @@ def measure(W, steps, warmup, world):
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": load_pmc_traffic(W.key, dom)},
-            "kernels": per_kernel}
+            "kernels": per_kernel,
+            "store_gate": {"settle_steps": settle, "sites": gate_sites}}
 
 
 def api_us_per_step(dev, steps=300, warmup=30):
@@ -991,6 +1017,7 @@ def main(argv=None):
         "config": cfg,
         "roofline": r["roofline"],
         "kernels": r["kernels"],
+        "store_gate": r["store_gate"],
     }
     if a.tune:
         out["config"]["tuning"] = a.tune

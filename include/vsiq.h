@@ -90,11 +90,31 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_PC_PACKED 10         /* per-channel fq with given qparams + K6: 1 = packed short
                                           rows (default), 0 = one workgroup per row */
 #define VSIQ_TUNE_STORE_GATE 11        /* one-round K3 / STE grids: no stores before workgroup
-                                          start + N ticks of the 100 MHz wall clock (-1 = auto:
-                                          the grid's read time at 7.5 TB/s; 0 = off) */
+                                          start + N ticks of the 100 MHz wall clock (-1 = auto,
+                                          see VSIQ_TUNE_GATE_AUTOTUNE; 0 = off) */
 #define VSIQ_TUNE_STORE_DEFER 6        /* one-round grids: hold stores back N x 512 clocks after
                                           the loads (-1 = auto, 0 = off, max 64) */
+#define VSIQ_TUNE_GATE_AUTOTUNE 12     /* 1 (default): the automatic store gate is tuned online
+                                          per launch site (kernel, grid, bytes, device) from
+                                          event-timed launches; 0: fixed 1.05 x the read time
+                                          at 7.5 TB/s */
 int vsiq_set_tuning(int key, int value);
+
+/*
+ * Store-gate tuner (VSIQ_TUNE_GATE_AUTOTUNE).  The only state the library keeps
+ * between calls besides the knobs: per launch site, a handful of HIP event pairs and
+ * the timings they returned (host memory; no device memory, no host sync).
+ *   vsiq_gate_tuning_pending: sites still tuning after harvesting finished timings
+ *     (a caller that wants steady-state launches runs warm-up calls until it is 0);
+ *   vsiq_gate_report: one text line per site (label, grid, bytes, chosen ticks, median
+ *     launch time per candidate in us) into buf (NUL-terminated, truncated to len);
+ *     returns the full length;
+ *   vsiq_gate_reset: forget every site (returns 1 and keeps them while timings are
+ *     still in flight).
+ */
+int vsiq_gate_tuning_pending(void);
+int64_t vsiq_gate_report(char *buf, int64_t len);
+int vsiq_gate_reset(void);
 
 /*
  * Self-test of the kernels' correctly rounded division x / s (reciprocal +

@@ -1,0 +1,91 @@
+"""Store-gate tuner (csrc/gate_tune.hip, VSIQ_TUNE_GATE_AUTOTUNE): the first launches of
+a one-round launch site run candidate gates, timed by event pairs; the gate is a pure
+delay, so every candidate must give the same bits.  C2-shaped K3 forward and STE
+backward run through tuning and are compared with the oracle (bitwise) at every launch;
+the tuner must settle and report the sites."""
+import numpy as np
+import pytest
+import torch
+
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import fakequant as FQ
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _reset():
+    torch.cuda.synchronize()
+    assert H.lib().vsiq_gate_reset() == 0
+
+
+@pytest.mark.parametrize("shape", [(1024, 1024, 3, 3), (768, 512, 3, 3)])
+def test_tuned_gate_bits_identical_to_oracle(shape):
+    rng = np.random.default_rng(5)
+    w = (rng.standard_normal(shape) * 0.05).astype(np.float32)
+    g = rng.standard_normal(shape).astype(np.float32)
+    ref = O.per_channel_observe_fq(w, False, 8)
+    gxo = O.per_channel_backward_fixed(g, ref["mask"], ref["scale"])
+    x, gd = torch.from_numpy(w).to(DEV), torch.from_numpy(g).to(DEV)
+    rowlen = w.size // shape[0]
+    _reset()
+    ys, gxs = [], []
+    for i in range(140):   # > 12 candidates x 8 samples per site
+        r = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255, want_mask=True)
+        gx = FQ.ste_backward(gd, r["mask"], r["scale"], rowlen)
+        if i % 7 == 0:
+            ys.append(r["y"].clone())
+            gxs.append(gx.clone())
+        if i % 16 == 15:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for y, gx in zip(ys, gxs):
+        G.assert_bitwise_f32(y.cpu().numpy(), ref["y"], "y")
+        G.assert_bitwise_f32(gx.cpu().numpy(), gxo, "grad_x")
+    assert H.gate_tuning_pending() == 0
+    rep = H.gate_report()
+    lines = {l.split()[0]: l for l in rep.splitlines()}
+    sites = ("k3_pc_observe_fq", "ste_bwd") if shape[1] * shape[2] * shape[3] == 9216 else ("k3_pc_observe_fq",)
+    for k in sites:   # the STE grid of 4608-element rows is not a one-round 9-group grid
+        assert k in lines, rep
+        assert " done=1 " in lines[k], rep
+        assert f"grid={shape[0]} " in lines[k], rep
+
+
+def test_forced_gate_and_autotune_off():
+    """VSIQ_TUNE_STORE_GATE forces ticks (no tuning); GATE_AUTOTUNE 0 keeps the fixed
+    estimate and creates no site."""
+    x = torch.randn(1024, 9216, device=DEV) * 0.05
+    _reset()
+    try:
+        H.set_tuning(H.TUNE_GATE_AUTOTUNE, 0)
+        y0 = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"]
+        H.set_tuning(H.TUNE_STORE_GATE, 700)
+        y1 = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"]
+        torch.cuda.synchronize()
+        assert H.gate_report() == ""
+        assert torch.equal(y0.view(torch.int32), y1.view(torch.int32))
+    finally:
+        H.set_tuning(H.TUNE_GATE_AUTOTUNE, 1)
+        H.set_tuning(H.TUNE_STORE_GATE, -1)
+
+
+def test_capture_uses_current_gate_and_matches_eager():
+    """A launch under HIP-graph capture is never timed; replay == eager bit for bit."""
+    x = torch.randn(1024, 9216, device=DEV) * 0.05
+    _reset()
+    eager = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"].clone()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"]
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), eager.view(torch.int32))

@@ -38,6 +38,7 @@ QP_LEN = 4
 TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6
 TUNE_OBS_KERNEL, TUNE_OBS_GRID, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 8, 9, 10
 TUNE_STORE_GATE = 11
+TUNE_GATE_AUTOTUNE = 12
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
@@ -57,6 +58,9 @@ _SIGS = {
     "vsiq_workspace_doubles": ([c_i64], c_i64),
     "vsiq_mask_words": ([c_i64, c_i64], c_i64),
     "vsiq_set_tuning": ([c_int, c_int], c_int),
+    "vsiq_gate_tuning_pending": ([], c_int),
+    "vsiq_gate_report": ([ctypes.c_char_p, c_i64], c_i64),
+    "vsiq_gate_reset": ([], c_int),
     "vsiq_selftest_div": ([c_p, c_int, c_p, c_p], c_int),
     "vsiq_selftest_fq": ([c_int, c_p, c_p, c_int, ctypes.c_float, ctypes.c_float, c_p, c_p], c_int),
     "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
@@ -187,6 +191,19 @@ def mask_buffer(rows: int, rowlen: int, device) -> torch.Tensor:
 
 def set_tuning(key: int, value: int):
     check(lib().vsiq_set_tuning(int(key), int(value)), "vsiq_set_tuning")
+
+
+def gate_tuning_pending() -> int:
+    """Store-gate launch sites still tuning (vsiq_gate_tuning_pending)."""
+    return int(lib().vsiq_gate_tuning_pending())
+
+
+def gate_report() -> str:
+    """One line per tuned store-gate launch site (vsiq_gate_report)."""
+    n = int(lib().vsiq_gate_report(None, 0))
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().vsiq_gate_report(buf, n + 1)
+    return buf.value.decode()
 
 
 def ptr(t):

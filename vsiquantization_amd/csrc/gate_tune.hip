@@ -1,0 +1,258 @@
+// gate_tune.hip — online tuner of the one-round store gate (store_gate_select in
+// vsiq_common.cuh).  Host code only.
+//
+// A launch site is (kernel, grid, read bytes, device).  Its first launches cycle
+// through candidate gates f x (read bytes at 7.5 TB/s), and no gate, each bracketed by
+// a pair of HIP events on the launch stream; later calls harvest finished pairs
+// (hipEventQuery, never a host sync), and once every candidate has kSamples times the
+// smallest median wins and is used from then on.  All state is behind one mutex
+// (autograd's backward thread launches too); launches under HIP-graph capture take the
+// current choice and are never timed.
+#include "vsiq_common.cuh"
+
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+namespace vsiq {
+namespace {
+
+constexpr double kFactors[] = {0.0, 0.90, 0.95, 0.975, 1.0, 1.025, 1.05, 1.075, 1.10, 1.15, 1.20, 1.30};
+constexpr int kCand = sizeof(kFactors) / sizeof(kFactors[0]);
+constexpr int kSamples = 8;        // timed launches per candidate
+constexpr double kDefault = 1.05;  // before (or without) tuning
+constexpr double kCapUs = 40.0;
+
+struct Site {
+  std::string label;
+  int64_t grid = 0, bytes = 0;
+  int dev = 0;
+  double est = 0.0;                 // ticks of read bytes at 7.5 TB/s
+  uint32_t ticks[kCand] = {};
+  std::vector<float> ms[kCand];
+  int issued[kCand] = {};
+  int rr = 0;
+  bool done = false;
+  uint32_t best = 0;
+};
+
+struct Sample {
+  hipEvent_t a = nullptr, b = nullptr;
+  Site *site = nullptr;
+  int cand = 0;
+  int dev = 0;
+};
+
+using Key = std::tuple<const void *, int64_t, int64_t, int>;
+
+std::mutex g_mu;
+std::map<Key, Site> g_sites;
+std::vector<Sample *> g_pending;
+std::map<int, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_pool;
+
+uint32_t clamp_ticks(double t, int khz) {
+  const double cap = kCapUs * khz / 1e3;
+  return (uint32_t)std::max(0.0, std::min(cap, t));
+}
+
+float median(std::vector<float> v) {
+  std::sort(v.begin(), v.end());
+  const size_t n = v.size();
+  return n % 2 ? v[n / 2] : 0.5f * (v[n / 2 - 1] + v[n / 2]);
+}
+
+void finish_if_complete(Site &s) {
+  if (s.done) return;
+  for (int c = 0; c < kCand; ++c)
+    if ((int)s.ms[c].size() < kSamples) return;
+  int bc = 0;
+  float bm = median(s.ms[0]);
+  for (int c = 1; c < kCand; ++c) {
+    const float m = median(s.ms[c]);
+    if (m < bm) { bm = m; bc = c; }
+  }
+  s.best = s.ticks[bc];
+  s.done = true;
+}
+
+// caller holds g_mu
+void harvest_locked() {
+  size_t keep = 0;
+  for (size_t i = 0; i < g_pending.size(); ++i) {
+    Sample *p = g_pending[i];
+    const hipError_t q = hipEventQuery(p->b);
+    if (q == hipErrorNotReady) {
+      g_pending[keep++] = p;
+      continue;
+    }
+    float ms = 0.0f;
+    if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f) {
+      p->site->ms[p->cand].push_back(ms);
+      finish_if_complete(*p->site);
+      g_pool[p->dev].emplace_back(p->a, p->b);
+    } else {
+      p->site->issued[p->cand]--;   // lost sample: issue again
+      (void)hipGetLastError();
+    }
+    delete p;
+  }
+  g_pending.resize(keep);
+}
+
+}  // namespace
+
+GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, int occ, int64_t read_bytes,
+                          hipStream_t st) {
+  GateSel sel;
+  const int forced = g_tune.store_gate;
+  if (forced >= 0) {
+    sel.gate = (uint32_t)forced;
+    return sel;
+  }
+  const int64_t cus = device_cus();
+  if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return sel;
+  const int khz = device_wall_clock_khz();
+  const double est = (double)read_bytes / 7.5e12 * 1e3 * (double)khz;
+  if (!g_tune.gate_autotune) {
+    sel.gate = clamp_ticks(kDefault * est, khz);
+    return sel;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    sel.gate = clamp_ticks(kDefault * est, khz);
+    return sel;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  Site &s = g_sites[Key{kernel, grid, read_bytes, dev}];
+  if (s.grid == 0) {
+    s.label = label;
+    s.grid = grid;
+    s.bytes = read_bytes;
+    s.dev = dev;
+    s.est = est;
+    for (int c = 0; c < kCand; ++c) s.ticks[c] = clamp_ticks(kFactors[c] * est, khz);
+  }
+  if (s.done) {
+    sel.gate = s.best;
+    return sel;
+  }
+  sel.gate = clamp_ticks(kDefault * est, khz);
+  // under capture: no event work at all (queries are not allowed in global capture mode)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return sel;
+  }
+  if (!g_pending.empty()) harvest_locked();
+  if (s.done) {
+    sel.gate = s.best;
+    return sel;
+  }
+  int c = -1;
+  for (int k = 0; k < kCand; ++k) {
+    const int j = (s.rr + k) % kCand;
+    if (s.issued[j] < kSamples) { c = j; break; }
+  }
+  if (c < 0) return sel;   // every sample issued, results still in flight
+  s.rr = (c + 1) % kCand;
+  auto &pool = g_pool[dev];
+  std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+  if (!pool.empty()) {
+    ev = pool.back();
+    pool.pop_back();
+  } else if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) {
+    (void)hipGetLastError();
+    return sel;
+  }
+  if (hipEventRecord(ev.first, st) != hipSuccess) {
+    (void)hipGetLastError();
+    pool.push_back(ev);
+    return sel;
+  }
+  Sample *p = new Sample;
+  p->a = ev.first;
+  p->b = ev.second;
+  p->site = &s;
+  p->cand = c;
+  p->dev = dev;
+  s.issued[c]++;
+  sel.gate = s.ticks[c];
+  sel.timing = p;
+  return sel;
+}
+
+void store_gate_launched(GateSel &sel, hipStream_t st) {
+  if (!sel.timing) return;
+  Sample *p = static_cast<Sample *>(sel.timing);
+  sel.timing = nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (hipEventRecord(p->b, st) != hipSuccess) {
+    (void)hipGetLastError();
+    p->site->issued[p->cand]--;
+    g_pool[p->dev].emplace_back(p->a, p->b);
+    delete p;
+    return;
+  }
+  g_pending.push_back(p);
+}
+
+int gate_sites_tuning() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  harvest_locked();
+  int n = 0;
+  for (auto &kv : g_sites)
+    if (!kv.second.done) ++n;
+  return n;
+}
+
+int64_t gate_report(char *buf, int64_t len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  harvest_locked();
+  std::string out;
+  char line[512];
+  for (auto &kv : g_sites) {
+    const Site &s = kv.second;
+    std::snprintf(line, sizeof line, "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u",
+                  s.label.c_str(), s.dev, (long long)s.grid, (long long)s.bytes, s.est, s.done ? 1 : 0,
+                  s.best);
+    out += line;
+    for (int c = 0; c < kCand; ++c) {
+      if (s.ms[c].empty()) continue;
+      std::snprintf(line, sizeof line, " %u:%.2f", s.ticks[c], 1e3 * median(s.ms[c]));
+      out += line;
+    }
+    out += "\n";
+  }
+  if (buf && len > 0) {
+    const int64_t n = std::min<int64_t>(len - 1, (int64_t)out.size());
+    std::copy(out.begin(), out.begin() + n, buf);
+    buf[n] = '\0';
+  }
+  return (int64_t)out.size();
+}
+
+int gate_reset() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  harvest_locked();
+  if (!g_pending.empty()) return 1;   // samples in flight keep their sites alive
+  g_sites.clear();
+  return 0;
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int vsiq_gate_tuning_pending(void) { return gate_sites_tuning(); }
+
+int64_t vsiq_gate_report(char *buf, int64_t len) { return gate_report(buf, len); }
+
+int vsiq_gate_reset(void) { return gate_reset(); }
+
+}  // extern "C"

@@ -11,11 +11,11 @@ namespace vsiq {
 // K1: y = fq(act(x)), one-shot (kFlatU groups per lane, no loop: exact vmcnt)
 // ----------------------------------------------------------------------------
 // U groups per lane: kFlatU, or 9 for a one-round grid whose stores wait behind the
-// store gate (t0: the workgroup's start on the wall clock; gate 0 = no gate).
+// store gate (gc: gate_begin at the workgroup start; gate 0 = no gate).
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U = kFlatU>
 __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float *__restrict__ y,
                                              uint8_t *__restrict__ codes, uint64_t *__restrict__ mask,
-                                             int64_t n, const QP &p, int64_t blk, uint64_t t0 = 0,
+                                             int64_t n, const QP &p, int64_t blk, GateClk gc = GateClk{0},
                                              uint32_t gate = 0) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * U + threadIdx.x;   // lanes chunk-aligned
@@ -29,7 +29,7 @@ __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float 
     go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4<ACT>(v[u]), p, base + u * kBlock, n);
     if (MASK) mask_put(mlo, mhi, u, go[u].b);
   }
-  if (gate) store_gate(t0, gate);
+  gate_pass(gate, gc);
   const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int u = 0; u < U; ++u) {

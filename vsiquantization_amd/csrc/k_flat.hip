@@ -561,6 +561,10 @@ int vsiq_set_tuning(int key, int value) {
       if (value < -1 || value > 4000) return VSIQ_E_ARG;
       g_tune.store_gate = value;
       return 0;
+    case VSIQ_TUNE_GATE_AUTOTUNE:
+      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      g_tune.gate_autotune = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;

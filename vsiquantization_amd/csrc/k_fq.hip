@@ -10,30 +10,31 @@ __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, 
                                                    uint8_t *__restrict__ codes,
                                                    uint64_t *__restrict__ mask, int64_t n,
                                                    QPSrc src, uint32_t gate) {
-  const uint64_t t0 = gate ? wall_clock64() : 0;
+  const GateClk gc = gate_begin(gate);
   const QP p = load_qp(src);
-  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, t0, gate);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, gc, gate);
 }
 
 // One-round grids of 9 groups per lane with the store gate where that applies
-// (store_gate_ticks: >= 2 workgroups per CU, all resident), else kFlatU groups per lane.
+// (store_gate_select: >= 2 workgroups per CU, all resident), else kFlatU groups per lane.
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
 void launch_fq_k(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
                  const QPSrc &src, hipStream_t st) {
   const int64_t ng = cdiv(n, 4);
   const int64_t grid9 = cdiv(ng, (int64_t)kBlock * 9);
-  uint32_t gate = 0;
+  GateSel gs;
   if (g_tune.store_gate != 0 && grid9 * kBlock * 9 - ng <= ng / 8) {
-    static const int occ =
-        occupancy_blocks(reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), kBlock);
-    gate = store_gate_ticks(grid9, occ, 4 * n);
+    const void *kern = reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>);
+    static const int occ = occupancy_blocks(kern, kBlock);
+    gs = store_gate_select("k1_fq_fwd", kern, grid9, occ, 4 * n, st);
   }
-  if (gate)
+  if (gs.gate)
     hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), dim3((unsigned)grid9), dim3(kBlock), 0, st,
-                       x, y, codes, mask, n, src, gate);
+                       x, y, codes, mask, n, src, gs.gate);
   else
     hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>), dim3((unsigned)oneshot_grid(ng)),
                        dim3(kBlock), 0, st, x, y, codes, mask, n, src, 0u);
+  store_gate_launched(gs, st);   // a tuning sample of "no gate" times the kFlatU grid
 }
 
 template <int ACT, bool VEC, bool NT>

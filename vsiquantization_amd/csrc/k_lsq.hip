@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_pcr_lsq_bwd(const float *__restrict_
                                                         const double *__restrict__ zp, float lo, float hi,
                                                         double gscale, double *__restrict__ gs_out,
                                                         double *__restrict__ gz_out, uint32_t gate) {
-  const uint64_t t0 = gate ? wall_clock64() : 0;
+  const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x;
   const QP p = load_qp(QPSrc{nullptr, scale + row, zp ? zp + row : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   const int64_t ng = cdiv(rowlen, 4);
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_pcr_lsq_bwd(const float *__restrict_
       gz_out[row] = gz;
     }
   }
-  if (gate) store_gate(t0, gate);
+  gate_pass(gate, gc);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int64_t i = threadIdx.x + k * kBlock;
@@ -281,14 +281,15 @@ template <bool VEC, bool NT, bool ZPL, int NV>
 void launch_pcr_nv(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                    const double *scale, const double *zp, float lo, float hi, double gscale,
                    double *gs, double *gz, hipStream_t st) {
-  uint32_t gate = 0;
+  GateSel sel;
   if (g_tune.store_gate != 0) {
-    static const int occ =
-        occupancy_blocks(reinterpret_cast<const void *>(k_pcr_lsq_bwd<VEC, NT, ZPL, NV>), kBlock);
-    gate = store_gate_ticks(rows, occ, 8 * rows * rowlen);
+    const void *kern = reinterpret_cast<const void *>(k_pcr_lsq_bwd<VEC, NT, ZPL, NV>);
+    static const int occ = occupancy_blocks(kern, kBlock);
+    sel = store_gate_select("k6_pcr_lsq_bwd", kern, rows, occ, 8 * rows * rowlen, st);
   }
   hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV>), dim3((unsigned)rows), dim3(kBlock), 0, st, g, x, gx,
-                     rowlen, scale, zp, lo, hi, gscale, gs, gz, gate);
+                     rowlen, scale, zp, lo, hi, gscale, gs, gz, sel.gate);
+  store_gate_launched(sel, st);
 }
 
 // rows == channels and whole rows fit 9 groups per lane with >= 1 per lane

@@ -115,7 +115,7 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
                                                int64_t row, int par, float *__restrict__ y,
                                                uint8_t *__restrict__ codes,
                                                uint64_t *__restrict__ mask, const PCArgs &a,
-                                               uint64_t t0 = 0) {
+                                               GateClk gc = GateClk{0}) {
   const int64_t ng = cdiv(a.rowlen, 4);
   float mn = __builtin_inff(), mx = -__builtin_inff();
   uint32_t nan = 0;
@@ -143,7 +143,7 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
     if (MASK) mask_put(mlo, mhi, k, go[k].b);
   }
   if (a.defer) defer_stores(a.defer);   // after pc_row_qparams' barrier
-  if (a.gate) store_gate(t0, a.gate);
+  gate_pass(a.gate, gc);
   const int lane = threadIdx.x % kWave;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ 
                                                       float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
                                                       uint64_t *__restrict__ mask, PCArgs a) {
-  const uint64_t t0 = a.gate ? wall_clock64() : 0;
+  const GateClk gc = gate_begin(a.gate);
   const int64_t row0 = (int64_t)blockIdx.x * RPB;
   const int64_t last = a.rows - 1;
   f4 v[RPB][NV];
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ 
   }
   // RPB is 1 or 2; written out because the unroller refuses the (large) loop body
   static_assert(RPB == 1 || RPB == 2, "rows per block");
-  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a, t0);
+  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a, gc);
   if constexpr (RPB == 2) {
     if (row0 + 1 <= last)   // uniform
       pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[RPB - 1], rmn[RPB - 1], rmx[RPB - 1],
@@ -243,14 +243,18 @@ template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS, 
 void launch_pc_k(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
   const auto kern = k_pc_observe_fq<NV, VEC, NT, STATS, MASK, CODES, BS, RPB>;
   PCArgs b = a;
+  GateSel gs;
   if (RPB == 1 && BS == kBlock && a.gate == kGateAuto) {
     // one-round grids of >= 2 rows per CU: stores wait for the grid's read phase
     static const int occ = occupancy_blocks(reinterpret_cast<const void *>(kern), BS);
-    b.gate = store_gate_ticks(a.rows, occ, a.rows * a.rowlen * (int64_t)sizeof(float));
+    gs = store_gate_select("k3_pc_observe_fq", reinterpret_cast<const void *>(kern), a.rows, occ,
+                           a.rows * a.rowlen * (int64_t)sizeof(float), st);
+    b.gate = gs.gate;
   } else if (a.gate == kGateAuto) {
     b.gate = 0;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.rows, RPB)), dim3(BS), 0, st, x, y, c, m, b);
+  store_gate_launched(gs, st);
 }
 
 template <int NV, bool VEC, bool NT, bool STATS, int BS, int RPB>

@@ -67,13 +67,13 @@ __device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
 }
 
 // U groups per lane: kFlatU, or 9 for a one-round grid behind the store gate
-// (gate 0 = none; t0 = the workgroup's start on the wall clock)
+// (gate 0 = none; gc = gate_begin at the workgroup start)
 template <bool VEC, bool NT, bool CODES, bool MASK, int U>
 __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
                                                       uint64_t *__restrict__ mask, uint32_t chunks,
                                                       PCFixed a, uint32_t gate) {
-  const uint64_t t0 = gate ? wall_clock64() : 0;
+  const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
   const QP p = pc_fixed_qp(a, row);
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
     go[u] = fq_out_flat<VEC, CODES, MASK>(v[u], p, base + u * kBlock, a.rowlen);
     if (MASK) mask_put(mlo, mhi, u, go[u].b);
   }
-  if (gate) store_gate(t0, gate);
+  gate_pass(gate, gc);
   uint8_t *cr = CODES ? codes + row * a.rowlen : nullptr;
   const int lane = threadIdx.x % kWave;
 #pragma unroll
@@ -115,20 +115,21 @@ void launch_pc_fixed_k(const float *x, float *y, uint8_t *c, uint64_t *m, const 
                        hipStream_t st) {
   const int64_t ng = cdiv(a.rowlen, 4);
   const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
-  uint32_t gate = 0;
+  GateSel gs;
   if (g_tune.store_gate != 0 && chunks9 * kBlock * 9 - ng <= ng / 8) {
-    static const int occ =
-        occupancy_blocks(reinterpret_cast<const void *>(k_pc_fq_fwd<VEC, NT, CODES, MASK, 9>), kBlock);
-    gate = store_gate_ticks(rows * chunks9, occ, 4 * rows * a.rowlen);
+    const void *kern = reinterpret_cast<const void *>(k_pc_fq_fwd<VEC, NT, CODES, MASK, 9>);
+    static const int occ = occupancy_blocks(kern, kBlock);
+    gs = store_gate_select("pc_fq_fwd", kern, rows * chunks9, occ, 4 * rows * a.rowlen, st);
   }
-  if (gate) {
+  if (gs.gate) {
     hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, CODES, MASK, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock),
-                       0, st, x, y, c, m, (uint32_t)chunks9, a, gate);
-    return;
+                       0, st, x, y, c, m, (uint32_t)chunks9, a, gs.gate);
+  } else {
+    const int64_t chunks = oneshot_grid(ng);
+    hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, CODES, MASK, kFlatU>), dim3((unsigned)(rows * chunks)),
+                       dim3(kBlock), 0, st, x, y, c, m, (uint32_t)chunks, a, 0u);
   }
-  const int64_t chunks = oneshot_grid(ng);
-  hipLaunchKernelGGL((k_pc_fq_fwd<VEC, NT, CODES, MASK, kFlatU>), dim3((unsigned)(rows * chunks)),
-                     dim3(kBlock), 0, st, x, y, c, m, (uint32_t)chunks, a, 0u);
+  store_gate_launched(gs, st);   // a tuning sample of "no gate" times the kFlatU grid
 }
 
 template <bool VEC, bool NT>

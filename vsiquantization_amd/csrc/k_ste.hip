@@ -21,7 +21,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     float *__restrict__ gx, int64_t rowlen,
                                                     uint32_t chunks, const double *__restrict__ sdev,
                                                     double shost, uint32_t defer, uint32_t gate) {
-  const uint64_t t0 = gate ? wall_clock64() : 0;
+  const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
   const SteDiv d = make_stediv((float)(sdev ? sdev[row] : shost));
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
     __syncthreads();
     defer_stores(defer);
   }
-  if (gate) store_gate(t0, gate);
+  gate_pass(gate, gc);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = base + u * kBlock;
@@ -84,23 +84,26 @@ void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *
   const int64_t ng = cdiv(rowlen, 4);
   const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
   const bool fits9 = chunks9 * kBlock * 9 - ng <= ng / 8;
-  uint32_t gate = 0;
+  GateSel gs;
   // one-round grids: store gate (auto; C2 STE 13.3-13.6 -> 12.9-13.0 us in bench.py on
   // MI355X), else the deferred store phase where that was measured to pay
   if (fits9 && g_tune.store_gate != 0) {
-    static const int occ = occupancy_blocks(reinterpret_cast<const void *>(k_ste_bwd<VEC, NT, ACT, 9>), kBlock);
+    const void *kern = reinterpret_cast<const void *>(k_ste_bwd<VEC, NT, ACT, 9>);
+    static const int occ = occupancy_blocks(kern, kBlock);
     const int64_t bytes = rows * rowlen * (int64_t)(ACT ? 8 : 4) + rows * mask_words_per_row(rowlen) * 8;
-    gate = store_gate_ticks(rows * chunks9, occ, bytes);
+    gs = store_gate_select("ste_bwd", kern, rows * chunks9, occ, bytes, st);
   }
-  const uint32_t defer = fits9 && !gate ? store_defer_units(rows * chunks9, true) : 0;
-  if (defer || gate) {
+  // "no gate" (also as a tuning candidate) = the deferred store phase where it applies
+  const uint32_t defer = fits9 && !gs.gate ? store_defer_units(rows * chunks9, true) : 0;
+  if (defer || gs.gate) {
     hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock), 0, st,
-                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer, gate);
-    return;
+                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer, gs.gate);
+  } else {
+    const int64_t chunks = oneshot_grid(ng);
+    hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, kFlatU>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0,
+                       st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u, 0u);
   }
-  const int64_t chunks = oneshot_grid(ng);
-  hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, kFlatU>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0,
-                     st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u, 0u);
+  store_gate_launched(gs, st);
 }
 
 template <int ACT>

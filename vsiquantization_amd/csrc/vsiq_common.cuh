@@ -67,6 +67,7 @@ struct Tuning {
   int obs_grid = 0;            // K2 grid-stride workgroups (0 = kObsGrid)
   int lsq_groups = 0;          // K4 groups per lane 2 / 4 / 8 / 16 (0 = by size)
   int store_gate = -1;         // store gate ticks (10 ns) for one-round grids (-1 = auto, 0 = off)
+  int gate_autotune = 1;       // store gate tuned online per launch site (0 = fixed estimate)
 };
 extern Tuning g_tune;
 
@@ -1031,30 +1032,49 @@ __device__ __forceinline__ void defer_stores(uint32_t units) {
 // read/write turnarounds) without delaying the rows that finish reading after the
 // gate (unlike defer_stores).  A pure delay, wave-uniform (scalar clock), never a
 // correctness issue.
-__device__ __forceinline__ void store_gate(uint64_t t0, uint32_t ticks) {
+__device__ __forceinline__ void store_gate_clock(uint64_t t0, uint32_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
-// host: store gate of a one-round grid of `grid` workgroups (`occ` resident per CU)
-// reading `read_bytes`: 1.05 x the time the reads take at 7.5 TB/s, in 10 ns ticks
-// (MI355X, tools/exp/gate_bench.py, K3 at 1.0 x: 1024 x 9216 14.4 -> 12.1 us,
-// 2048 x 4608 16.0 -> 13.7, 1280 x 9216 18.7 -> 17.5; the optimum sits at 1.0-1.1 x
-// and falls off steeply below 0.9 -- box-to-box HBM speed varies a few %, hence 1.05;
-// in bench.py's C2 step 14.3 -> 13.7 us).  Grids under 2 workgroups per CU gain nothing; grids of
-// more than one round lose (the next round waits behind the gate).
-// Override: vsiq_set_tuning(VSIQ_TUNE_STORE_GATE, ticks); 0 = off.
-constexpr uint32_t kGateAuto = 0xffffffffu;
+struct GateClk {
+  uint64_t t0;   // the workgroup's start on the wall clock (gate != 0)
+};
+
+// at the workgroup's start, before its loads are issued
+__device__ __forceinline__ GateClk gate_begin(uint32_t gate) {
+  return GateClk{gate ? (uint64_t)wall_clock64() : 0ull};
+}
+
+// before the workgroup's first store (wave-uniform)
+__device__ __forceinline__ void gate_pass(uint32_t gate, const GateClk &c) {
+  if (gate) store_gate_clock(c.t0, gate);
+}
+
+// Host: the store gate of a one-round grid (gate_tune.hip).  Eligible grids: >= 2
+// workgroups per CU and all of them resident at once (`occ` per CU); grids under 2
+// workgroups per CU gain nothing and grids of more than one round lose (the next round
+// waits behind the gate).  The gate's optimum is sharp and moves with the box's HBM:
+// K3 at C2 on one MI355X (tools/exp/gate_timeline.py) 4.52 / 5.00 / 5.28 / 5.60 /
+// 6.03 us -> 12.8 / 12.2 / 12.4 / 12.7 / 13.1 us per launch (15.2 without a gate), and
+// the fixed 1.05 x (read bytes at 7.5 TB/s) of round 1 sat at the no-gate time on
+// another box.  So the gate is tuned online per (kernel, grid, bytes, device): the
+// first launches of a site cycle through candidate gates of f x the 7.5 TB/s estimate
+// (and no gate), each timed with a pair of HIP events around the launch (no host
+// sync: results are harvested by later calls), and the best median is kept.  Capture
+// (HIP graphs) uses the current best or the estimate.  Results are identical for every
+// gate (a pure delay).  Override: vsiq_set_tuning(VSIQ_TUNE_STORE_GATE, ticks), 0 =
+// off; VSIQ_TUNE_GATE_AUTOTUNE 0 = the 1.05 x estimate without tuning.
+constexpr uint32_t kGateAuto = 0xffffffffu;   // PCArgs::gate: resolved at launch
 int device_cus();
 int occupancy_blocks(const void *kernel, int block);
 int device_wall_clock_khz();
-inline uint32_t store_gate_ticks(int64_t grid, int occ, int64_t read_bytes) {
-  if (g_tune.store_gate >= 0) return (uint32_t)g_tune.store_gate;
-  const int64_t cus = device_cus();
-  if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return 0;
-  // 1.05 x read_bytes / 7.5 TB/s in wall-clock ticks (100 MHz on MI355X: bytes / 71500)
-  const double ticks = 1.05 * (double)read_bytes / 7.5e12 * 1e3 * (double)device_wall_clock_khz();
-  return (uint32_t)std::min(40.0 * device_wall_clock_khz() / 1e3, ticks);   // <= 40 us
-}
+struct GateSel {
+  uint32_t gate = 0;    // wall-clock ticks for the launch (0 = no gate)
+  void *timing = nullptr;   // tuner sample in flight (record its end after the launch)
+};
+GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, int occ, int64_t read_bytes,
+                          hipStream_t st);
+void store_gate_launched(GateSel &sel, hipStream_t st);
 
 // host: defer_stores units for a one-round grid of `grid` workgroups of 256 lanes x 9
 // groups (override: vsiq_set_tuning(VSIQ_TUNE_STORE_DEFER, units)).  Automatic only
