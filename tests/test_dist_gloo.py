@@ -94,3 +94,33 @@ def test_replay_minmax_tensor_equals_sequential_fold():
         got = (float(mn[i]), float(mx[i]))
         assert got == tuple(float(w) for w in want)
         assert np.signbit(got[0]) == np.signbit(float(want[0]))
+
+
+def _count_worker(rank, world, port, counts_by_rank, ret):
+    from vsiquantization_amd.distributed import check_call_counts
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        check_call_counts(counts_by_rank[rank], torch.device("cpu"))
+        ret[rank] = "ok"
+    except RuntimeError as e:
+        ret[rank] = str(e)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("counts,ok", [([[16, 16, 16], [16, 16, 16]], True),
+                                       ([[16, 16, 16], [16, 16, 15]], False),    # one missing call
+                                       ([[16, 16, 16], [16, 16]], False),        # one missing layer
+                                       ([[16, 15, 16], [15, 16, 16]], False)])   # same total, moved
+def test_sync_calibration_call_count_check(counts, ok):
+    """sync_calibration's pre-check (distributed.check_call_counts): every rank raises the
+    same error when the ranks' deferred calls differ, instead of folding different calls
+    together (uneven shards)."""
+    port = 29600 + os.getpid() % 1000
+    ret = mp.Manager().dict()
+    mp.spawn(_count_worker, args=(2, port, counts, ret), nprocs=2, join=True)
+    if ok:
+        assert ret[0] == ret[1] == "ok"
+    else:
+        assert "different deferred observer calls" in ret[0] and "different deferred observer calls" in ret[1]

@@ -118,3 +118,48 @@ def test_fused_model_training_step_graph_replay_equals_eager():
             torch.testing.assert_close(p.grad, gr, rtol=1e-5, atol=1e-12, msg=name)
         else:
             assert torch.equal(p.grad, gr), name
+
+
+def test_two_graphs_own_workspaces_and_replay_concurrently():
+    """Each captured graph gets its own reduction workspace + arrival counter (keyed by
+    the capture id, _hip.workspace), so two graphs replayed at the same time on two
+    streams do not share a counter: both give their eager results bit for bit."""
+    from vsiquantization_amd import _hip as H
+    torch.manual_seed(1)
+    q = V.UniformQuantizer(8, True)
+    xs = [torch.randn(64, 32, 56, 56, device=DEV, requires_grad=True) for _ in range(2)]
+    gs = [torch.randn(64, 32, 56, 56, device=DEV) for _ in range(2)]
+    ss = [torch.nn.Parameter(torch.tensor(v, dtype=torch.float64, device=DEV)) for v in (0.03, 0.05)]
+    ref = []
+    for x, g, s in zip(xs, gs, ss):
+        _step(q, x, g, s, None)
+        ref.append((x.grad.clone(), s.grad.clone()))
+        x.grad, s.grad = None, None
+    before = {k for k in H._WS if "capture" in k}
+    graphs = []
+    for x, g, s in zip(xs, gs, ss):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            _step(q, x, g, s, None)
+        torch.cuda.current_stream().wait_stream(side)
+        x.grad, s.grad = None, None
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            _step(q, x, g, s, None)
+        graphs.append(gr)
+    new = {k for k in H._WS if "capture" in k} - before
+    assert len(new) == 2, new
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for _ in range(5):
+        for x, s in zip(xs, ss):
+            x.grad.zero_()
+            s.grad.zero_()
+        torch.cuda.synchronize()
+        for gr, st in zip(graphs, streams):
+            with torch.cuda.stream(st):
+                gr.replay()
+        torch.cuda.synchronize()
+        for (gx, gsr), x, s in zip(ref, xs, ss):
+            assert torch.equal(x.grad, gx)
+            assert torch.equal(s.grad, gsr)

@@ -245,14 +245,34 @@ class _Workspace:
 
 
 _WS = {}
+_HIPRT = []
+
+
+def _capture_id(stream: c_p):
+    """hipStreamGetCaptureInfo id of the capture `stream` is in, or None."""
+    if not _HIPRT:
+        rt = ctypes.CDLL("libamdhip64.so")
+        rt.hipStreamGetCaptureInfo.argtypes = [c_p, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_ulonglong)]
+        rt.hipStreamGetCaptureInfo.restype = c_int
+        _HIPRT.append(rt)
+    status, cid = c_int(0), ctypes.c_ulonglong(0)
+    if _HIPRT[0].hipStreamGetCaptureInfo(stream, ctypes.byref(status), ctypes.byref(cid)) != 0:
+        return None
+    return cid.value if status.value == 1 else None   # hipStreamCaptureStatusActive
 
 
 def workspace(device, n: int = 0) -> _Workspace:
     """Workspace for a reducing launch over n elements on the current stream of `device`.
     (Growing it while a previous launch still reads the old buffer is safe: the caching
-    allocator only recycles the old block after work queued on this stream.)"""
+    allocator only recycles the old block after work queued on this stream.)  Under
+    HIP-graph capture the key is the capture: every graph gets its own workspace and
+    counter (allocated from its pool), so graphs replayed concurrently on different
+    streams never share a counter."""
     dev = torch.device(device)
-    key = (dev.index, stream_of(dev).value)
+    st = stream_of(dev)
+    key = (dev.index, st.value)
+    if torch.cuda.is_current_stream_capturing():
+        key = (dev.index, "capture", _capture_id(st))
     w = _WS.get(key)
     if w is None:
         w = _WS[key] = _Workspace(dev, n)

@@ -382,7 +382,8 @@ inline int obs_groups_per_lane(int64_t ng) {
 inline int64_t observe_grid(int64_t ng) {
   if (g_tune.obs_kernel == 1) return lsq_grid(ng, obs_groups_per_lane(ng));
   if (ng <= kObsSingle && g_tune.obs_grid == 0) return 1;
-  const int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : kObsGrid;
+  const int og = g_tune.obs_grid;
+  const int64_t cap = og > 0 ? og : kObsGrid;
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(ng, (int64_t)kBlock * kObsU)));
 }
 
@@ -447,7 +448,8 @@ inline int64_t observe_part_grid(int64_t n) {
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
   const int u = observe_part_u(n);
   // large tensors: kObsGrid workgroups striding over the tensor; small: one step each
-  int64_t cap = g_tune.obs_grid > 0 ? g_tune.obs_grid : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS / kWaves);
+  const int og = g_tune.obs_grid;
+  int64_t cap = og > 0 ? og : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS / kWaves);
   cap = std::min<int64_t>(cap, VSIQ_EXP_PART_CAP);
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(units, u)));
 }
@@ -479,8 +481,10 @@ int occupancy_blocks(const void *kernel, int block) {
   return n;
 }
 
+// per-device attribute caches: relaxed atomics (any thread may fill them; the value
+// is the same whoever wins)
 int device_wall_clock_khz() {
-  static int khz[64] = {0};
+  static std::atomic<int> khz[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 100000;
   if (!khz[dev]) {
@@ -492,7 +496,7 @@ int device_wall_clock_khz() {
 }
 
 int device_cus() {
-  static int cus[64] = {0};
+  static std::atomic<int> cus[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
   if (!cus[dev]) {

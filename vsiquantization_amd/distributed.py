@@ -95,6 +95,45 @@ def replay_minmax_tensor(init_min, init_max, recs: torch.Tensor):
     return torch.where(mins < lo, mins, lo), torch.where(maxs > hi, maxs, hi)
 
 
+def check_call_counts(counts, device, group=None):
+    """All ranks must hold the same deferred calls (managers x calls each) before their
+    records are all-reduced row by row: a rank with an extra or missing calibration batch
+    would otherwise fold different calls together (or hang on mismatched sizes).  One
+    tiny MAX all-reduce of [h, -h] over (manager count, call count, order hash); raises
+    RuntimeError on every rank when any differs."""
+    h = 0
+    for c in counts:
+        h = (h * 1000003 + int(c) + 1) % 2147483647
+    head = torch.tensor([len(counts), sum(counts), h], dtype=torch.float64)
+    both = torch.cat([head, -head]).to(device)
+    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+    hi, lo = both[:3].cpu(), -both[3:].cpu()
+    if not torch.equal(hi, lo):
+        raise RuntimeError(f"sync_calibration: ranks hold different deferred observer calls "
+                           f"(managers / calls: local {len(counts)} / {sum(counts)}, across ranks "
+                           f"{int(lo[0])}..{int(hi[0])} / {int(lo[1])}..{int(hi[1])}); every rank "
+                           "must run the same calibration batches through the same layers")
+
+
+def fold_slots(slots):
+    """Stats records [calls, ST_LEN] of K2p slots of any sizes, in call order: one
+    fold_parts launch per distinct slot length (each call's slot is sized for its
+    tensor, part_slot_doubles(numel), instead of the largest possible)."""
+    from .fakequant import fold_parts
+    by_len = {}
+    for i, p in enumerate(slots):
+        by_len.setdefault(p.numel(), []).append(i)
+    if len(by_len) == 1:
+        return fold_parts(torch.stack(slots))
+    order, parts = [], []
+    for idx in by_len.values():
+        order.extend(idx)
+        parts.append(fold_parts(torch.stack([slots[i] for i in idx])))
+    inv = torch.empty(len(order), dtype=torch.int64)
+    inv[torch.tensor(order)] = torch.arange(len(order))
+    return torch.cat(parts).index_select(0, inv.to(slots[0].device, non_blocking=True))
+
+
 def _deferred_managers(model):
     from .quantizers.quantization_manager import QuantizationManager
     for m in model.modules():
@@ -108,14 +147,12 @@ def sync_calibration(model, group=None):
     running-state replay per layer.  ``group``: the process group of the all-reduce;
     None = the managers' own ``dist_group`` (no collective when that is None too: a
     single-GPU deferred calibration)."""
-    from .fakequant import fold_parts
     mgrs = list(_deferred_managers(model))
     if not mgrs:
         return 0
     for m in mgrs:
         m._join()   # records may still be in flight on an observer side stream
     counts = [len(m._pending_records) for m in mgrs]
-    stats = fold_parts(torch.stack([p for m in mgrs for p in m._pending_records]))
     if group is None:
         groups = {id(m.dist_group): m.dist_group for m in mgrs if m.dist_group is not None}
         if len(groups) > 1:
@@ -125,6 +162,11 @@ def sync_calibration(model, group=None):
         collective = group is not None
     else:
         collective = True
+    slots = [p for m in mgrs for p in m._pending_records]
+    dev = slots[0].device
+    if collective:
+        check_call_counts(counts, dev, group)
+    stats = fold_slots(slots)
     if collective:
         stats = allreduce_stats(stats, group=group)
     host = stats.cpu()

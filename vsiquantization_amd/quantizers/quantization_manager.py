@@ -193,7 +193,7 @@ class QuantizationManager(nn.Module):
                                    "(calibration); use per-call mode to quantize while observing")
             if not self._pending_records:
                 self._calib_init = (obs.min_val, obs.max_val)
-            slot = torch.empty(part_slot_doubles(), dtype=torch.float64, device=x.device)
+            slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
             self._pending_records.append(observe_parts(x, out=slot, act=act))
             return
         _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
