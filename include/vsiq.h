@@ -207,6 +207,23 @@ int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_st
                             double *stats_out, void *stream);
 
 /*
+ * Multi-tensor K2p (K2m): `count` deferred observer calls of one activation `act` in
+ * one launch per 32 calls (blocks map to (call, block) through a descriptor table in
+ * the kernel arguments).  Each call's records are bit-identical to its own
+ * vsiq_act_observe_part_f32 launch.  Replaces, for a calibration forward, the
+ * per-layer observer launches of minmax.py:42-43 + quantization_manager.py:66-68
+ * (calibrate_qat_model, utils/quantize_manager.py:4-31): the calls of consecutive
+ * layers are queued and observed together (QuantizationManager deferred mode).
+ */
+typedef struct vsiq_part_tensor {
+  const float *c;       /* observed tensor (pre-activation when act != NONE), n floats */
+  int64_t n;
+  double *parts;        /* this call's slot, parts_len >= vsiq_observe_part_records(n) * VSIQ_PART_LEN */
+  int64_t parts_len;
+} vsiq_part_tensor;
+int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, int act, void *stream);
+
+/*
  * Per-channel fused observe + qparams + fake-quant forward (K3), axis 0 of a
  * row-major [rows, rowlen] view (OIHW weight: rows = O, rowlen = I*H*W).
  * Build-defined per-channel MinMax: row c is processed as

@@ -109,3 +109,49 @@ def test_fold_parts_unwritten_slot_folds_nothing():
     st = FQ.fold_parts(slots).cpu()
     assert torch.all(st[:, H.ST_N] == 0)
     assert torch.all(torch.isinf(st[:, H.ST_MIN])) and torch.all(st[:, H.ST_MIN] > 0)
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+def test_observe_parts_multi_records_bitwise_equal_per_call(act):
+    """K2m (vsiq_act_observe_part_multi_f32): every tensor's partial records are the
+    same bits as its own K2p launch -- 40 tensors (two launches of 32 + 8) of mixed
+    sizes across all three groups-per-lane classes, ragged n, a misaligned view, NaNs."""
+    from vsiquantization_amd import fakequant as FQ
+    g = torch.Generator(device=DEV).manual_seed(3)
+    sizes = [1, 7, 4096, 1000003, 3 * 2**20 + 5, 13107200, 52428800, 65536, 999, 2**20]
+    xs = [torch.randn(sizes[i % len(sizes)] + (i // len(sizes)), device=DEV, generator=g) * (1 + i)
+          for i in range(39)]
+    xs[5][3] = float("nan")
+    xs.append(torch.randn(4097, device=DEV, generator=g)[1:])   # misaligned view
+    per = [FQ.observe_parts(x, act=act) for x in xs]
+    multi = FQ.observe_parts_multi(xs, None, act=act)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(per, multi)):
+        assert a.numel() == b.numel()
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), i
+
+
+def test_queued_deferred_calibration_equals_unqueued(monkeypatch):
+    """QuantizationManager's deferred calls queued and observed by K2m (default) give
+    the same running min/max, qparams and stats lists, bit for bit, as one K2p launch per
+    call (VSIQ_OBSERVE_BATCH=0)."""
+    a = _model()
+    b = copy.deepcopy(a)
+    calibrate_qat_model(a, _loader(), data_calib, DEV)
+    monkeypatch.setenv("VSIQ_OBSERVE_BATCH", "0")
+    calibrate_qat_model(b, _loader(), data_calib, DEV)
+    assert _state(a) == _state(b)
+    from vsiquantization_amd import observe_batch
+    assert observe_batch.pending() == 0
+
+
+def test_queued_observer_detects_in_place_change():
+    from vsiquantization_amd import observe_batch
+    from vsiquantization_amd.fakequant import part_slot_doubles
+    x = torch.randn(1000, device=DEV)
+    slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=DEV)
+    observe_batch.add(x, None, slot)
+    x.mul_(2)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        observe_batch.flush()
+    assert observe_batch.pending() == 0

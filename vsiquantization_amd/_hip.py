@@ -85,6 +85,7 @@ _SIGS = {
                              c_int),
     "vsiq_observe_part_records": ([c_i64], c_i64),
     "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
+    "vsiq_act_observe_part_multi_f32": ([c_p, c_int, c_int, c_p], c_int),
     "vsiq_observe_fold_parts": ([c_p, c_i64, c_i64, c_p, c_p], c_int),
     "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
     "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),
@@ -102,6 +103,11 @@ class LsqTensor(ctypes.Structure):
                 ("grad_out", c_p), ("n", c_i64), ("scale_host", c_d), ("zp_host", c_d), ("gscale", c_d),
                 ("qmin", ctypes.c_int32), ("qmax", ctypes.c_int32), ("zp_learn", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
+
+
+class PartTensor(ctypes.Structure):
+    """vsiq_part_tensor (include/vsiq.h): one call of a multi-tensor deferred observer launch."""
+    _fields_ = [("c", c_p), ("n", c_i64), ("parts", c_p), ("parts_len", c_i64)]
 
 
 class VsiqError(RuntimeError):

@@ -141,13 +141,16 @@ __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *_
 
 // Grid-stride accumulation of a fixed grid over x (U groups per lane per step): the
 // body shared by k_observe_loop and k_observe_part.
+// Block `blk` of an `nblk`-block grid over x (the multi-tensor K2m runs the same body
+// on its tensors' block ranges).
 template <bool VEC, bool NT, int ACT, int U>
-__device__ __forceinline__ void observe_stride(const float *__restrict__ x, int64_t n, ObsAcc &a) {
+__device__ __forceinline__ void observe_stride_b(const float *__restrict__ x, int64_t n, ObsAcc &a,
+                                                 int64_t blk, int64_t nblk) {
   obs_init(a);
   const int64_t ng = cdiv(n, 4);
   const int64_t nfull = n / 4;
-  const int64_t step = (int64_t)gridDim.x * kBlock * U;
-  for (int64_t b = (int64_t)blockIdx.x * kBlock * U; b < ng; b += step) {
+  const int64_t step = nblk * kBlock * U;
+  for (int64_t b = blk * kBlock * U; b < ng; b += step) {
     f4 v[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
@@ -165,6 +168,11 @@ __device__ __forceinline__ void observe_stride(const float *__restrict__ x, int6
       }
     }
   }
+}
+
+template <bool VEC, bool NT, int ACT, int U>
+__device__ __forceinline__ void observe_stride(const float *__restrict__ x, int64_t n, ObsAcc &a) {
+  observe_stride_b<VEC, NT, ACT, U>(x, n, a, blockIdx.x, gridDim.x);
 }
 
 // One-shot: G groups per lane (grid = ng / (256 G)), all G loads issued up front
@@ -211,6 +219,25 @@ __global__ __launch_bounds__(kBlock) void k_observe_loop(const float *__restrict
   observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
 }
 
+// One K2p record per WAVE (DPP reductions only): no LDS round trip and no barrier in
+// the tail of the grid (C5 observe phase 263 -> 253-258 us on MI355X,
+// tools/exp/floor_bench.py).  Record {min, max, nan count, sum|x|, sum x, sum x^2, n,
+// records} of wave w of block blk.
+__device__ __forceinline__ void store_part_record(ObsAcc &a, double *__restrict__ parts, int64_t blk,
+                                                  int64_t nblk, int64_t n) {
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  if (threadIdx.x % kWave == 0) {
+    double *r = parts + (blk * kWaves + threadIdx.x / kWave) * VSIQ_PART_LEN;
+    r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan; r[3] = a.sa;
+    r[4] = a.s1; r[5] = a.s2; r[6] = (double)n; r[7] = (double)nblk * kWaves;
+  }
+}
+
 // K2p: the grid-stride pass of k_observe_loop WITHOUT the cross-workgroup fold.  Each
 // wave stores its record {min, max, nan count, sum|x|, sum x, sum x^2, n, records}
 // (VSIQ_PART_LEN doubles, plain stores) and exits: no arrival atomics, no
@@ -222,19 +249,51 @@ __global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict
                                                           double *__restrict__ parts) {
   ObsAcc a;
   observe_stride<VEC, NT, ACT, U>(x, n, a);
-  // one record per WAVE (DPP reductions only): no LDS round trip and no barrier in the
-  // tail of the grid (C5 observe phase 263 -> 253-258 us on MI355X, tools/exp/floor_bench.py)
-  a.mn = wave_reduce(a.mn, MinOp());
-  a.mx = wave_reduce(a.mx, MaxOp());
-  a.nan = wave_reduce(a.nan, AddU());
-  a.sa = wave_reduce(a.sa, AddD());
-  a.s1 = wave_reduce(a.s1, AddD());
-  a.s2 = wave_reduce(a.s2, AddD());
-  if (threadIdx.x % kWave == 0) {
-    double *r = parts + ((int64_t)blockIdx.x * kWaves + threadIdx.x / kWave) * VSIQ_PART_LEN;
-    r[0] = a.mn; r[1] = a.mx; r[2] = (double)a.nan; r[3] = a.sa;
-    r[4] = a.s1; r[5] = a.s2; r[6] = (double)n; r[7] = (double)gridDim.x * kWaves;
+  store_part_record(a, parts, blockIdx.x, gridDim.x, n);
+}
+
+// ----------------------------------------------------------------------------
+// K2m: many deferred observer calls (K2p) in ONE launch.  Block b of the launch runs
+// block b - blk0[t] of tensor t's own K2p grid (same grid, groups per lane and body as
+// vsiq_act_observe_part_f32 for that n), so every tensor's records are bit-identical
+// to its single-tensor K2p launch; only the ~3 us launch floor and the grid tail are
+// paid once per batch instead of once per layer (C5: 27 layers per calibration batch).
+// ----------------------------------------------------------------------------
+constexpr int kPartMulti = 32;   // tensors per launch (descriptor table in the kernel arguments)
+
+struct PTensor {
+  const float *x;
+  double *parts;
+  int64_t n;
+  uint32_t grid;
+  int u;      // groups per lane per step (observe_part_u)
+  int vec;
+};
+
+struct PBatch {
+  PTensor t[kPartMulti];
+  uint32_t blk0[kPartMulti + 1];
+  int count;
+};
+
+template <bool NT, int ACT>
+__global__ __launch_bounds__(kBlock) void k_observe_part_multi(const PBatch b) {
+  int t = 0;
+  const uint32_t blk = blockIdx.x;
+  while (t + 1 < b.count && blk >= b.blk0[t + 1]) ++t;   // scalar: blk0 is a kernel argument
+  const PTensor &T = b.t[t];
+  const int64_t lb = (int64_t)blk - b.blk0[t], nb = T.grid;
+  ObsAcc a;
+  if (T.vec) {
+    if (T.u == 8) observe_stride_b<true, NT, ACT, 8>(T.x, T.n, a, lb, nb);
+    else if (T.u == 4) observe_stride_b<true, NT, ACT, 4>(T.x, T.n, a, lb, nb);
+    else observe_stride_b<true, NT, ACT, 2>(T.x, T.n, a, lb, nb);
+  } else {
+    if (T.u == 8) observe_stride_b<false, false, ACT, 8>(T.x, T.n, a, lb, nb);
+    else if (T.u == 4) observe_stride_b<false, false, ACT, 4>(T.x, T.n, a, lb, nb);
+    else observe_stride_b<false, false, ACT, 2>(T.x, T.n, a, lb, nb);
   }
+  store_part_record(a, T.parts, lb, nb, T.n);
 }
 
 // Fold of deferred K2p records: workgroup c folds call c's records (call_stride doubles
@@ -625,6 +684,45 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
   const bool vec = aligned16(c) && n % 4 == 0;
   VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, (hipStream_t)stream);
   return launch_rc();
+}
+
+int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, int act, void *stream) {
+  if (count < 0 || (count > 0 && !tensors) || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  for (int i = 0; i < count; ++i) {
+    const vsiq_part_tensor &T = tensors[i];
+    if (T.n <= 0 || !T.c || !T.parts) return VSIQ_E_ARG;
+    if (T.parts_len < observe_part_grid(T.n) * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
+  }
+  const bool nt = g_tune.nontemporal != 0;
+  for (int i0 = 0; i0 < count; i0 += kPartMulti) {
+    PBatch b{};
+    b.count = std::min(kPartMulti, count - i0);
+    uint32_t blk = 0;
+    for (int k = 0; k < b.count; ++k) {
+      const vsiq_part_tensor &T = tensors[i0 + k];
+      PTensor &P = b.t[k];
+      P.x = T.c;
+      P.parts = T.parts;
+      P.n = T.n;
+      P.grid = (uint32_t)observe_part_grid(T.n);
+      P.u = observe_part_u(T.n);
+      P.vec = aligned16(T.c) && T.n % 4 == 0;
+      b.blk0[k] = blk;
+      blk += P.grid;
+    }
+    b.blk0[b.count] = blk;
+    const hipStream_t st = (hipStream_t)stream;
+#define K2M(A)                                                                                          \
+  if (nt) hipLaunchKernelGGL((k_observe_part_multi<true, A>), dim3(blk), dim3(kBlock), 0, st, b);    \
+  else hipLaunchKernelGGL((k_observe_part_multi<false, A>), dim3(blk), dim3(kBlock), 0, st, b);
+    if (act == kActRelu) { K2M(kActRelu) }
+    else if (act == kActSilu) { K2M(kActSilu) }
+    else { K2M(kActNone) }
+#undef K2M
+    const int rc = launch_rc();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride, double *stats_out,

@@ -150,6 +150,8 @@ def sync_calibration(model, group=None):
     mgrs = list(_deferred_managers(model))
     if not mgrs:
         return 0
+    from . import observe_batch
+    observe_batch.flush()   # queued deferred calls (K2m) write their records now
     for m in mgrs:
         m._join()   # records may still be in flight on an observer side stream
     counts = [len(m._pending_records) for m in mgrs]

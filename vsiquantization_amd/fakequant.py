@@ -373,6 +373,34 @@ def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) ->
     return out
 
 
+def observe_parts_multi(xs, outs, act=None) -> list:
+    """K2m: the deferred observer pass (observe_parts) of every x in ``xs`` into its slot
+    in ``outs`` (None: allocated) in one launch per 32 tensors, on the current stream of
+    the first x's device.  Records bit-identical to one observe_parts call per x."""
+    if not xs:
+        return []
+    dev = xs[0].device
+    arr = (H.PartTensor * len(xs))()
+    res = []
+    for i, x in enumerate(xs):
+        x = H.require_device_f32(x)
+        if x.device != dev:
+            raise ValueError("observe_parts_multi: all tensors must be on one device")
+        if x.numel() == 0:
+            raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+        out = outs[i] if outs is not None else None
+        need = part_slot_doubles(x.numel())
+        if out is None:
+            out = torch.empty(need, dtype=torch.float64, device=dev)
+        elif out.dtype != torch.float64 or out.device != dev or not out.is_contiguous():
+            raise ValueError("observe_parts_multi: slots must be contiguous float64 tensors on x's device")
+        arr[i] = H.PartTensor(x.data_ptr(), x.numel(), out.data_ptr(), out.numel())
+        res.append(out)
+    rc = H.lib().vsiq_act_observe_part_multi_f32(arr, len(xs), H.act_code(act), H.stream_of(dev))
+    H.check(rc, "vsiq_act_observe_part_multi_f32")
+    return res
+
+
 def fold_parts(parts: torch.Tensor) -> torch.Tensor:
     """Fold deferred observer slots ``parts`` [calls, stride] (f64, one call per row) into
     stats records f64 [calls, ST_LEN] in one launch."""

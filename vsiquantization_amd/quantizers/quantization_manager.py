@@ -27,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _hip as H
+from .. import observe_batch
 from ..fakequant import (observe_finalize, observe_parts, observe_tensor, part_slot_doubles,
                          stats_from_row_sums)
 from ..observers.minmax import MinMaxObserver
@@ -194,7 +195,11 @@ class QuantizationManager(nn.Module):
             if not self._pending_records:
                 self._calib_init = (obs.min_val, obs.max_val)
             slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
-            self._pending_records.append(observe_parts(x, out=slot, act=act))
+            if observe_batch.enabled():   # queued: one K2m launch per up to 32 calls
+                observe_batch.add(x, act, slot)
+                self._pending_records.append(slot)
+            else:
+                self._pending_records.append(observe_parts(x, out=slot, act=act))
             return
         _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
                                run_minmax=None, want_qp=False, want_stats=True, act=act)
