@@ -88,7 +88,9 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_OBS_GRID 8           /* K2 grid-stride workgroups, 0 = auto (512), max 2048 */
 #define VSIQ_TUNE_LSQ_GROUPS 9         /* K4 groups per lane 2 / 4 / 8 / 16, 0 = by size */
 #define VSIQ_TUNE_PC_PACKED 10         /* per-channel fq with given qparams + K6: 1 = packed short
-                                          rows (default), 0 = one workgroup per row */
+                                          rows / channel columns for K6 on axis 1 (default),
+                                          2 = packed rows for K6 too (round-1 form),
+                                          0 = one workgroup per row */
 #define VSIQ_TUNE_STORE_GATE 11        /* one-round K3 / STE grids: no stores before workgroup
                                           start + N ticks of the 100 MHz wall clock (-1 = auto,
                                           see VSIQ_TUNE_GATE_AUTOTUNE; 0 = off) */

@@ -60,7 +60,11 @@ def test_golden_lsq_fake_quantize(case):
                                         # whole rows per workgroup, ragged last workgroup
                                         ((16, 32, 10, 10), 1), ((8, 16, 20, 20), 1), ((4, 8, 40, 40), 1),
                                         ((3, 7, 4), 1), ((2, 24, 32, 64), 1), ((1, 5, 12), 1),
-                                        ((97, 3, 8), 1), ((300, 16), 0)])
+                                        ((97, 3, 8), 1), ((300, 16), 0),
+                                        # channel columns (K6 axis 1): several image blocks
+                                        # per channel, a partial last one
+                                        ((100, 8, 10, 10), 1), ((90, 4, 20, 20), 1), ((7, 3, 40, 48), 1),
+                                        ((256, 16, 10, 10), 1)])
 def test_pc_lsq_vs_oracle(shape, axis):
     rng = np.random.default_rng(sum(shape))
     x = (rng.standard_normal(shape) * 2).astype(np.float32)
@@ -81,10 +85,11 @@ def test_pc_lsq_vs_oracle(shape, axis):
     np.testing.assert_allclose(npy(zp.grad), gzo, rtol=1e-9, atol=1e-12)
 
 
-@pytest.mark.parametrize("shape", [(16, 32, 10, 10), (3, 7, 4), (2, 24, 32, 64), (97, 3, 8)])
+@pytest.mark.parametrize("shape", [(16, 32, 10, 10), (3, 7, 4), (2, 24, 32, 64), (97, 3, 8), (100, 8, 10, 10)])
 def test_packed_rows_equal_per_row_grid(shape):
-    """Packed short rows (VSIQ_TUNE_PC_PACKED 1, default) vs one workgroup per row (0):
-    y / grad_x bit for bit, per-channel gradients to float64 reordering."""
+    """Channel columns for K6 (VSIQ_TUNE_PC_PACKED 1, default) and packed short rows (2)
+    vs one workgroup per row (0): y / grad_x bit for bit, per-channel gradients to
+    float64 reordering."""
     from vsiquantization_amd import _hip as H
     rng = np.random.default_rng(7)
     x = (rng.standard_normal(shape) * 2).astype(np.float32)
@@ -94,17 +99,18 @@ def test_packed_rows_equal_per_row_grid(shape):
     z = torch.tensor(np.rint(rng.uniform(0, 255, C)) + 0.2, dtype=torch.float64, device=DEV)
     out = {}
     try:
-        for packed in (1, 0):
+        for packed in (1, 2, 0):
             H.set_tuning(H.TUNE_PC_PACKED, packed)
             y = FQ.per_channel_fake_quant(cu(x), s, z, 0, 255, zp_round=True, axis=1)[0]
             gx, gs, gz = FQ.pc_lsq_backward(cu(g), cu(x), s, z, 0, 255, 1e-3, True, 1)
             out[packed] = [npy(t) for t in (y, gx, gs, gz)]
     finally:
         H.set_tuning(H.TUNE_PC_PACKED, 1)
-    G.assert_bitwise_f32(out[1][0], out[0][0], "y")
-    G.assert_bitwise_f32(out[1][1], out[0][1], "grad_x")
-    np.testing.assert_allclose(out[1][2], out[0][2], rtol=1e-12, atol=1e-15)
-    np.testing.assert_allclose(out[1][3], out[0][3], rtol=1e-12, atol=1e-15)
+    for mode in (1, 2):
+        G.assert_bitwise_f32(out[mode][0], out[0][0], "y")
+        G.assert_bitwise_f32(out[mode][1], out[0][1], "grad_x")
+        np.testing.assert_allclose(out[mode][2], out[0][2], rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(out[mode][3], out[0][3], rtol=1e-12, atol=1e-15)
 
 
 def test_learnable_per_channel_quantizer_weights():

@@ -15,8 +15,12 @@ for kv in os.environ.get("TUNE", "").split():   # e.g. TUNE="11=0 10=0"
 
 def t(fn, reps):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
+    for i in range(400):   # let the store-gate tuner settle this launch site first
         fn()
+        if i % 16 == 15:
+            torch.cuda.synchronize()
+            if H.gate_tuning_pending() == 0:
+                break
     torch.cuda.synchronize(); s.record()
     for _ in range(reps):
         fn()

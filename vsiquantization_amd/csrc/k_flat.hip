@@ -617,7 +617,7 @@ int vsiq_set_tuning(int key, int value) {
       g_tune.store_defer = value;
       return 0;
     case VSIQ_TUNE_PC_PACKED:
-      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      if (value < 0 || value > 2) return VSIQ_E_ARG;
       g_tune.pc_packed = value;
       return 0;
     case VSIQ_TUNE_STORE_GATE:

@@ -328,6 +328,76 @@ void launch_pcp_lsq(const float *g, const float *x, float *gx, int64_t rows, int
                        (uint32_t)rpb, channels, scale, zp, lo, hi, ws);
 }
 
+// K6 stage 1 on channel columns (axis 1, short rows): workgroup (i, c) takes the rows
+// (n, c) of NB consecutive images n = i*NB .. (the same channel, hence one qparam pair
+// and one running {t, z} per thread), ~kPackElems elements; the workgroup's sums go to
+// record i*C + c -- k_pcm_lsq_fold's layout for rows' = cdiv(N, NB) * C, one chunk.  No
+// per-group LDS arrays or per-row reductions (the packed-rows form's tail), one block
+// reduction; rows are rowlen floats contiguous (rowlen % 4 == 0, vector path only).
+constexpr int kColGroups = 4;   // groups per lane
+inline int64_t pcc_images(int64_t rowlen) {
+  return std::max<int64_t>(1, (int64_t)kBlock * kColGroups * 4 / rowlen);
+}
+
+template <bool NT, bool ZPL>
+__global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict__ g,
+                                                        const float *__restrict__ x,
+                                                        float *__restrict__ gx, int64_t images,
+                                                        int64_t rowlen, uint32_t nb_img, int64_t channels,
+                                                        const double *__restrict__ scale,
+                                                        const double *__restrict__ zp, float lo, float hi,
+                                                        double *__restrict__ ws) {
+  const int64_t c = blockIdx.x % channels;
+  const int64_t n0 = (int64_t)(blockIdx.x / channels) * nb_img;
+  const uint32_t nr = (uint32_t)std::min<int64_t>(nb_img, images - n0);
+  const uint32_t gpr = (uint32_t)(rowlen / 4);
+  const uint32_t nj = nr * gpr;
+  const QP p = load_qp(QPSrc{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
+  const int64_t rstride = channels * rowlen;               // floats between (n, c) and (n+1, c)
+  const int64_t base = (n0 * channels + c) * rowlen;
+  f4 xv[kColGroups], gv[kColGroups];
+  int64_t off[kColGroups];
+#pragma unroll
+  for (int k = 0; k < kColGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    const uint32_t jj = j < nj ? j : nj - 1;
+    off[k] = base + (int64_t)(jj / gpr) * rstride + 4 * (jj % gpr);
+    xv[k] = load_group<true, NT>(x + off[k], 0, 4);
+    gv[k] = load_group<true, NT>(g + off[k], 0, 4);
+  }
+  LsqAcc acc{0.0, 0.0};
+  f4 o[kColGroups];
+#pragma unroll
+  for (int k = 0; k < kColGroups; ++k) {
+    const uint32_t j = threadIdx.x + k * kBlock;
+    o[k] = lsq_group_out<ZPL, kActNone>(j < nj ? 0 : 1, 1, 4, xv[k], gv[k], p, acc);   // i=1: no terms
+  }
+#pragma unroll
+  for (int k = 0; k < kColGroups; ++k)
+    if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
+  lsq_block_reduce(acc);
+  if (threadIdx.x == 0) {
+    ws[2 * (int64_t)blockIdx.x] = acc.t;
+    ws[2 * (int64_t)blockIdx.x + 1] = acc.z;
+  }
+}
+
+template <bool NT>
+int64_t launch_pcc_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                       int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
+                       float hi, double *ws, hipStream_t st) {
+  const int64_t images = rows / channels, nb = pcc_images(rowlen);
+  const int64_t iblocks = cdiv(images, nb);
+  const dim3 grid((unsigned)(iblocks * channels)), block(kBlock);
+  if (zp_learn)
+    hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, true>), grid, block, 0, st, g, x, gx, images, rowlen, (uint32_t)nb,
+                       channels, scale, zp, lo, hi, ws);
+  else
+    hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, false>), grid, block, 0, st, g, x, gx, images, rowlen, (uint32_t)nb,
+                       channels, scale, zp, lo, hi, ws);
+  return iblocks * channels;   // record rows for k_pcm_lsq_fold (one chunk each)
+}
+
 template <bool VEC, bool NT>
 void launch_pcm_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                     int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
@@ -389,14 +459,23 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
             gscale, grad_scale_out, grad_zp_out, st);
     return launch_rc();
   }
-  if (pc_packed(rowlen) && g_tune.pc_packed != 0)   // one chunk per row: same record layout
+  int64_t frows = rows, fchunks = chunks;   // record layout the fold reads
+  const int packed = g_tune.pc_packed;
+  if (vec && pc_packed(rowlen) && rows > channels && packed == 1) {   // axis 1, short rows: columns
+    frows = nt ? launch_pcc_lsq<true>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
+                                      (float)qmax, ws, st)
+               : launch_pcc_lsq<false>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
+                                       (float)qmax, ws, st);
+    fchunks = 1;
+  } else if (pc_packed(rowlen) && packed != 0) {   // one chunk per row: same record layout
     VSIQ_B2(launch_pcp_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
             (float)qmax, ws, st);
-  else
+  } else {
     VSIQ_B2(launch_pcm_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
             (float)qmax, ws, st);
-  hipLaunchKernelGGL(k_pcm_lsq_fold, dim3((unsigned)channels), dim3(kBlock), 0, st, ws, rows,
-                     (uint32_t)chunks, channels, zp, zp_learn, (float)qmin, (float)qmax, gscale,
+  }
+  hipLaunchKernelGGL(k_pcm_lsq_fold, dim3((unsigned)channels), dim3(kBlock), 0, st, ws, frows,
+                     (uint32_t)fchunks, channels, zp, zp_learn, (float)qmin, (float)qmax, gscale,
                      grad_scale_out, grad_zp_out);
   return launch_rc();
 }

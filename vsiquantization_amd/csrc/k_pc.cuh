@@ -244,14 +244,12 @@ void launch_pc_k(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs
   const auto kern = k_pc_observe_fq<NV, VEC, NT, STATS, MASK, CODES, BS, RPB>;
   PCArgs b = a;
   GateSel gs;
-  if (RPB == 1 && BS == kBlock && a.gate == kGateAuto) {
+  if (a.gate == kGateAuto) {
     // one-round grids of >= 2 rows per CU: stores wait for the grid's read phase
     static const int occ = occupancy_blocks(reinterpret_cast<const void *>(kern), BS);
-    gs = store_gate_select("k3_pc_observe_fq", reinterpret_cast<const void *>(kern), a.rows, occ,
+    gs = store_gate_select("k3_pc_observe_fq", reinterpret_cast<const void *>(kern), cdiv(a.rows, RPB), occ,
                            a.rows * a.rowlen * (int64_t)sizeof(float), st);
     b.gate = gs.gate;
-  } else if (a.gate == kGateAuto) {
-    b.gate = 0;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.rows, RPB)), dim3(BS), 0, st, x, y, c, m, b);
   store_gate_launched(gs, st);
