@@ -105,7 +105,9 @@ def test_tuning_keys_match_header_and_bounds():
     assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, 4) == 0
     assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, -1) == 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_BLOCK, 384) != 0
-    assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 2) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 3) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 2) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_GATE_AUTOTUNE, 2) != 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 1) == 0
     assert lib.vsiq_set_tuning(99, 0) != 0
 
