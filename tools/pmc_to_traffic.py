@@ -23,8 +23,8 @@ KERNEL_KEYS = {
     # each way for the 27 weights
     "c4": [("k_fq_fwd<", "fwd_all_layers", 27), ("k_lsq_fwd_multi<", "fwd_all_layers", 1),
            ("k_lsq_bwd<", "bwd_all_layers", 27), ("k_lsq_bwd_multi<", "bwd_all_layers", 1)],
-    # C5: 27 fused-ReLU deferred observer launches per calibration batch
-    "c5": [("k_observe_part<", "observe_all_layers", 27)],
+    # C5: ONE multi-tensor (K2m) fused-ReLU deferred observer launch per calibration batch
+    "c5": [("k_observe_part_multi<", "observe_all_layers", 1)],
 }
 
 
