@@ -185,6 +185,21 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
                           double qden, double eps, void *stream);
 
 /*
+ * Per-tensor observe + fake quant of a small tensor in ONE launch (K8): n <=
+ * vsiq_observe_fq_max_elems() (65536).  Equal to vsiq_act_observe_f32(c, n, act,
+ * stats_out, run_minmax, qp_out, ...) followed by vsiq_act_fq_fwd_f32(c, y, codes, mask,
+ * n, act, qp_out, ...): the same running update and f64 qparams record (min/max/qparams
+ * exact, stats sums to float64 reordering), y / codes / 1-bit mask bit for bit.  Replaces
+ * the reference's per-call observe + quantize (quantization_manager.py:73-90 ->
+ * minmax.py:32-74 -> uniform.py:34-56) for one small tensor: BASELINE C1, a calibration
+ * call on a weight.  stats_out / run_minmax / qp_out / codes / mask nullable.
+ */
+int64_t vsiq_observe_fq_max_elems(void);
+int vsiq_act_observe_fq_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                            double *stats_out, float *run_minmax, double *qp_out, int symmetric, double qden,
+                            double eps, int qmin, int qmax, void *stream);
+
+/*
  * Deferred-calibration observer (K2p): the K2 pass over act(c) WITHOUT the
  * cross-workgroup fold.  Replaces, like vsiq_act_observe_f32, minmax.py:42-43 +
  * quantization_manager.py:66-68 for an observe-only call (calibrate_qat_model,

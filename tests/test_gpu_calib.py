@@ -155,3 +155,44 @@ def test_queued_observer_detects_in_place_change():
     with pytest.raises(RuntimeError, match="modified in place"):
         observe_batch.flush()
     assert observe_batch.pending() == 0
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+@pytest.mark.parametrize("sym,qmin,qmax", [(True, -128, 127), (False, 0, 255), (True, -8, 7), (False, 0, 3)])
+@pytest.mark.parametrize("n", [1, 7, 255, 256, 4097, 65535, 65536])
+def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act):
+    """K8 (vsiq_act_observe_fq_f32: observe + qparams + fake quant of a small tensor in one
+    launch) == K2 (vsiq_act_observe_f32) then K1 (vsiq_act_fq_fwd_f32 on its qparams
+    record): running state, qparams record, y, codes and the 1-bit mask bit for bit, the
+    stats sums to float64 reordering; three calls carry the running state (one with a NaN,
+    which changes nothing, minmax.py:42-47); misaligned input takes the scalar path."""
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd import fakequant as FQ
+    g = torch.Generator(device=DEV).manual_seed(n + qmax)
+    xs = [torch.randn(n, device=DEV, generator=g) * (1 + i) for i in range(3)]
+    if n > 1:
+        xs[1][n // 2] = float("nan")
+    xs.append(torch.randn(n + 1, device=DEV, generator=g)[1:])     # misaligned view
+    ra = torch.zeros(2, device=DEV)
+    rb = torch.zeros(2, device=DEV)
+    for x in xs:
+        y, qp, st, mask, codes = FQ.observe_fake_quant(x, symmetric=sym, qmin=qmin, qmax=qmax, run_minmax=ra,
+                                                       act=act, want_mask=True, want_codes=True)
+        qp2, st2 = FQ.observe_tensor(x, symmetric=sym, run_minmax=rb, act=act)
+        y2, mask2, codes2 = FQ.fake_quant(x, None, None, qmin, qmax, qp=qp2, want_mask=True, want_codes=True,
+                                          act=act)
+        torch.cuda.synchronize()
+        assert torch.equal(ra.view(torch.int32), rb.view(torch.int32))
+        assert torch.equal(qp.view(torch.int64), qp2.view(torch.int64))
+        assert torch.equal(y.view(torch.int32), y2.view(torch.int32))
+        assert torch.equal(mask, mask2) and torch.equal(codes, codes2)
+        exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
+        assert torch.equal(st[exact], st2[exact])
+        np.testing.assert_allclose(st.cpu().numpy(), st2.cpu().numpy(), rtol=1e-12, atol=1e-300, equal_nan=True)
+
+
+def test_observe_fq_small_rejects_large():
+    from vsiquantization_amd import fakequant as FQ
+    n = FQ.observe_fq_max_elems() + 1
+    with pytest.raises(Exception):
+        FQ.observe_fake_quant(torch.randn(n, device=DEV), symmetric=True, qmin=-128, qmax=127)

@@ -253,6 +253,117 @@ __global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict
 }
 
 // ----------------------------------------------------------------------------
+// K8: per-tensor observe + qparams + fake quant of a SMALL tensor in one launch.  One
+// 1024-lane workgroup holds the whole tensor in registers (<= 16 groups per lane,
+// 65536 elements): it reduces min / max / NaN / sums (the K2 stats record), applies the
+// running update and the f64 qparams (minmax.py:42-74, qm.py:66-68) and fake-quantizes
+// from registers (uniform.py:55,95) -- K2 + K1 (two launches, the qparams through
+// memory) in one.  The reference's per-call observe+quantize of a small tensor
+// (quantization_manager.py:73-90; a calibration call on a weight, BASELINE C1).
+// ----------------------------------------------------------------------------
+constexpr int kSmallBlock = 1024;
+constexpr int kSmallGroups = 16;
+constexpr int64_t kSmallMax = (int64_t)kSmallBlock * kSmallGroups * 4;
+
+template <bool VEC, bool NT, int ACT, bool MASK, bool CODES, int U>
+__global__ __launch_bounds__(kSmallBlock) void k_observe_fq_small(
+    const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
+    uint64_t *__restrict__ mask, int64_t n, double *__restrict__ stats_out, float *__restrict__ run_minmax,
+    double *__restrict__ qp_out, int sym, double qden, double eps, float lo, float hi) {
+  constexpr int NW = kSmallBlock / kWave;
+  __shared__ float s_mn[NW], s_mx[NW];
+  __shared__ uint32_t s_nan[NW];
+  __shared__ double s_sa[NW], s_s1[NW], s_s2[NW];
+  __shared__ double s_qp[2];
+  const int64_t ng = cdiv(n, 4);
+  f4 v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k)
+    v[k] = act_fwd4<ACT>(load_group_c<VEC, NT>(x, threadIdx.x + k * kSmallBlock, ng, n));
+  ObsAcc a;
+  obs_init(a);
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const int64_t i = threadIdx.x + k * kSmallBlock;
+    if (i < ng) obs_add4(a, v[k], valid_in_group(i, n));
+  }
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) {
+    s_mn[w] = a.mn; s_mx[w] = a.mx; s_nan[w] = a.nan;
+    s_sa[w] = a.sa; s_s1[w] = a.s1; s_s2[w] = a.s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double f[6] = {s_mn[0], s_mx[0], (double)s_nan[0], s_sa[0], s_s1[0], s_s2[0]};
+    for (int i = 1; i < NW; ++i) {   // fixed order
+      f[0] = fminf((float)f[0], s_mn[i]); f[1] = fmaxf((float)f[1], s_mx[i]); f[2] += s_nan[i];
+      f[3] += s_sa[i]; f[4] += s_s1[i]; f[5] += s_s2[i];
+    }
+    if (stats_out) write_stats(stats_out, f, n);
+    observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax, qp_out, sym, qden, eps, &s_qp[0],
+                    &s_qp[1]);
+  }
+  __syncthreads();
+  QP p;
+  p.s = (float)s_qp[0];
+  p.z = (float)s_qp[1];
+  p.lo = lo;
+  p.hi = hi;
+  p.discrete = 0;
+  p.d = make_fastdiv(p.s);
+  p.fast = fq_fast_qp(p.s, p.z);
+  // every load was consumed before the barrier: each group is stored as soon as it is
+  // quantized (no output array held in registers, no vmcnt hazard)
+  uint32_t mlo = 0, mhi = 0;
+  const int lane = threadIdx.x % kWave;
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    const int64_t i = threadIdx.x + k * kSmallBlock;
+    const GroupOut go = fq_out_flat<VEC, CODES, MASK>(v[k], p, i, n);
+    if (MASK) mask_put(mlo, mhi, k, go.b);
+    if (i - lane < ng) fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go);   // wave-uniform test
+  }
+  if (MASK && lane < 4 * U) {   // lane 4k+j: word j of slot k's chunk
+    const int64_t first = (int64_t)threadIdx.x - lane + (lane >> 2) * kSmallBlock;
+    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
+  }
+}
+
+template <bool VEC, bool NT, int ACT>
+void launch_observe_fq_small(const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n, double *st,
+                             float *run, double *qp, int sym, double qden, double eps, float lo, float hi,
+                             hipStream_t s) {
+  // groups per lane: 2 up to 8192 elements (no clamped duplicate loads), else 16
+#define K8(MASK, CODES)                                                                                    \
+  if (n <= (int64_t)kSmallBlock * 2 * 4)                                                                   \
+    hipLaunchKernelGGL((k_observe_fq_small<VEC, NT, ACT, MASK, CODES, 2>), dim3(1), dim3(kSmallBlock), 0, s, x, \
+                       y, c, m, n, st, run, qp, sym, qden, eps, lo, hi);                                    \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_observe_fq_small<VEC, NT, ACT, MASK, CODES, kSmallGroups>), dim3(1), dim3(kSmallBlock), \
+                       0, s, x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi)
+  if (m && c) { K8(true, true); }
+  else if (m) { K8(true, false); }
+  else if (c) { K8(false, true); }
+  else { K8(false, false); }
+#undef K8
+}
+
+template <int ACT>
+void launch_observe_fq_small_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
+                                 double *st, float *run, double *qp, int sym, double qden, double eps, float lo,
+                                 float hi, hipStream_t s) {
+  if (vec && nt) launch_observe_fq_small<true, true, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
+  else if (vec) launch_observe_fq_small<true, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
+  else launch_observe_fq_small<false, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
+}
+
+// ----------------------------------------------------------------------------
 // K2m: many deferred observer calls (K2p) in ONE launch.  Block b of the launch runs
 // block b - blk0[t] of tensor t's own K2p grid (same grid, groups per lane and body as
 // vsiq_act_observe_part_f32 for that n), so every tensor's records are bit-identical
@@ -723,6 +834,20 @@ int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, 
     if (rc) return rc;
   }
   return 0;
+}
+
+int64_t vsiq_observe_fq_max_elems(void) { return kSmallMax; }
+
+int vsiq_act_observe_fq_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                            double *stats_out, float *run_minmax, double *qp_out, int symmetric, double qden,
+                            double eps, int qmin, int qmax, void *stream) {
+  if (n <= 0 || n > kSmallMax || !c || !y || qmin > qmax || act < kActNone || act > kActSilu)
+    return VSIQ_E_ARG;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
+  VSIQ_ACT(act, launch_observe_fq_small_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n,
+           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, (hipStream_t)stream);
+  return launch_rc();
 }
 
 int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride, double *stats_out,

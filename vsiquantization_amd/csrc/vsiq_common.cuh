@@ -989,9 +989,11 @@ __device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, do
 
 // Running-state update + qparams (observers/minmax.py:42-47 then :49-74).  A call
 // whose tensor holds a NaN changes nothing: `nan < v` is False in Python.
+// Returns the f64 (scale, zp) in *s_out / *z_out when those are given.
 __device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_nan,
                                                 float *run_minmax, double *qp_out, int sym,
-                                                double qden, double eps) {
+                                                double qden, double eps, double *s_out = nullptr,
+                                                double *z_out = nullptr) {
   float mn = 0.f, mx = 0.f;
   if (run_minmax) { mn = run_minmax[0]; mx = run_minmax[1]; }
   if (!has_nan) {
@@ -999,13 +1001,16 @@ __device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_n
     if (cmx > mx) mx = cmx;
   }
   if (run_minmax) { run_minmax[0] = mn; run_minmax[1] = mx; }
-  if (qp_out) {
+  if (qp_out || s_out) {
     double s, z;
     minmax_qparams((double)mn, (double)mx, sym, qden, eps, &s, &z);
-    qp_out[VSIQ_QP_SCALE] = s;
-    qp_out[VSIQ_QP_ZP] = z;
-    qp_out[VSIQ_QP_MIN] = mn;
-    qp_out[VSIQ_QP_MAX] = mx;
+    if (qp_out) {
+      qp_out[VSIQ_QP_SCALE] = s;
+      qp_out[VSIQ_QP_ZP] = z;
+      qp_out[VSIQ_QP_MIN] = mn;
+      qp_out[VSIQ_QP_MAX] = mx;
+    }
+    if (s_out) { *s_out = s; *z_out = z; }
   }
 }
 

@@ -345,6 +345,57 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     return qp, st
 
 
+def observe_fq_max_elems() -> int:
+    """Largest tensor observe_fake_quant takes (K8: one workgroup holds it in registers)."""
+    return int(H.lib().vsiq_observe_fq_max_elems())
+
+
+def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: float = 1e-8,
+                       qmin: int, qmax: int, run_minmax: torch.Tensor | None = None, act=None,
+                       want_mask: bool = False, want_codes: bool = False):
+    """K8: per-tensor observe (running update, f64 qparams, stats) + fake quant of a small
+    tensor in one launch -- observe_tensor + fake_quant(qp=...) fused.
+    Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None, codes | None)."""
+    x = H.require_device_f32(x)
+    n = x.numel()
+    if n == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    dev = x.device
+    y = torch.empty_like(x)
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev)
+    st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev)
+    mask = H.mask_buffer(1, n, dev) if want_mask else None
+    codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev) if want_codes else None
+    rc = H.lib().vsiq_act_observe_fq_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n), H.act_code(act),
+                                         H.ptr(st), H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
+                                         qden(symmetric, num_bits, eps), float(eps), int(qmin), int(qmax),
+                                         H.stream_of(dev))
+    H.check(rc, "vsiq_act_observe_fq_f32")
+    return y, qp, st, mask, codes
+
+
+class ObserveFakeQuantFn(torch.autograd.Function):
+    """K8 forward (observe + fake quant in one launch) with the reference's STE gradient
+    at fp32(scale) of this call (the FakeQuantFixedFn backward)."""
+
+    @staticmethod
+    def forward(ctx, x, symmetric, num_bits, eps, qmin, qmax, run_minmax, act):
+        y, qp, st, mask, _ = observe_fake_quant(x, symmetric=symmetric, num_bits=num_bits, eps=eps, qmin=qmin,
+                                                qmax=qmax, run_minmax=run_minmax, act=act, want_mask=True)
+        ctx.act = act
+        ctx.save_for_backward(mask, x) if H.act_code(act) != H.ACT_NONE else ctx.save_for_backward(mask)
+        ctx.scale = qp[H.QP_SCALE:H.QP_SCALE + 1]
+        ctx.mark_non_differentiable(qp, st)
+        return y, qp, st
+
+    @staticmethod
+    def backward(ctx, gy, _gqp, _gst):
+        saved = ctx.saved_tensors
+        pre = saved[1] if len(saved) > 1 else None
+        gx = ste_backward(gy.contiguous(), saved[0], ctx.scale, pre=pre, act=ctx.act)
+        return gx, None, None, None, None, None, None, None
+
+
 def part_slot_doubles(n: int | None = None) -> int:
     """Doubles of one deferred-observer slot for n elements (K2p records x VSIQ_PART_LEN);
     n None: a slot that fits any n."""

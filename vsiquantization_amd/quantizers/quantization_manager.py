@@ -43,6 +43,12 @@ _ACTS = {"relu": F.relu, "silu": F.silu}
 # model's next layers do not wait for it (its reduction tail overlaps their work).
 # Managers are spread round-robin over a small per-device pool; each manager always
 # uses the same stream, so its own running state stays stream-ordered.
+# K8 (one launch: observe + qparams + fake quant) for per-call observe+quantize up to this
+# many elements.  One workgroup holds the tensor: through this API (host-bound) a call is
+# 10.9-12.1 us against 17.9-18.2 us for K2 + K1 at 432-16384 elements, but its GPU time
+# grows past K2 + K1's ~9 us above ~16K elements (65536: 16.2 us; tools/exp/k8_bench.py).
+_K8_MAX = 16384
+
 _OBS_POOL = 4
 _OBS_STREAMS = {}
 _MGR_IDS = itertools.count()
@@ -253,6 +259,10 @@ class QuantizationManager(nn.Module):
             self._record_stats(stats_from_row_sums(rs, x.numel()))
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
             return y
+        if act is None or self._act_fusable(x):
+            y = self._observe_quantize_small(x, act)
+            if y is not None:
+                return y
         self.collect_qparameter(x, act)
         if self.is_quantize:
             if act is None:
@@ -260,6 +270,36 @@ class QuantizationManager(nn.Module):
             return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale,
                                            act=act)
         return x
+
+    def _observe_quantize_small(self, x, act):
+        """Observe + quantize of a small tensor in ONE launch (K8) when this call is the
+        reference's per-call observe+quantize (qm.py:73-90) with this package's per-tensor
+        MinMaxObserver and UniformQuantizer, single GPU; None when it does not apply."""
+        from ..fakequant import ObserveFakeQuantFn, observe_fake_quant, observe_fq_max_elems
+        from .uniform import UniformQuantizer
+        obs = self.observer
+        if not (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
+                and type(self.quantizer) is UniformQuantizer and isinstance(obs, MinMaxObserver)
+                and not isinstance(obs, PerChannelMinMaxObserver) and self._device_observer(x)
+                and self.dist_group is None and not self.dist_defer and x.dtype == torch.float32
+                and 0 < x.numel() <= min(_K8_MAX, observe_fq_max_elems())):
+            return None
+        self._join()
+        self._x_device = x.device
+        if obs._obs_stream is not None and obs._obs_stream != torch.cuda.current_stream(x.device):
+            obs._join()
+        state = obs.device_state(x.device)
+        q = self.quantizer
+        if x.requires_grad and torch.is_grad_enabled():
+            y, qp, st = ObserveFakeQuantFn.apply(x, obs.symmetric, obs.num_bits, obs.eps, q.qmin, q.qmax, state,
+                                                 act)
+        else:
+            y, qp, st, _, _ = observe_fake_quant(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
+                                                 qmin=q.qmin, qmax=q.qmax, run_minmax=state, act=act)
+        obs._dirty = True
+        self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+        self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+        return y
 
     # ------------------------------------------------------------------ learnable qparams
     def _home_device(self):
