@@ -543,9 +543,9 @@ class ActQuant:
     quantizers in observe + quantize mode (calibrate, then
     activate_quantizer without learnable qparams) over a batch of 1024 images split
     across the ranks (1024/N per GPU: strong scaling).  Per layer and call: K2 observe
-    of relu(conv output) (4 B/elem) -> with N > 1 the RCCL all-reduce of the stats record
-    (MAX over [-min, max], SUM over the sums) + vsiq_observe_finalize (running update, f64
-    qparams; QuantizationManager.dist_group, distributed.py) -> K1 fused-ReLU fake quant
+    of relu(conv output) (4 B/elem) -> with N > 1 one RCCL all_gather of the 10-double
+    stats records + vsiq_observe_finalize_ranks (rank-order fold, running update, f64
+    qparams; QuantizationManager.dist_group, distributed.gather_finalize) -> K1 fused-ReLU fake quant
     reading those qparams by pointer (8 B/elem).  Symmetric, observer 8-bit, quantizer
     4-bit (the YAML default a4 and the observer quirk)."""
 
@@ -581,22 +581,24 @@ class ActQuant:
             loc = world == 1   # one GPU: the observer pass updates the state and writes qparams itself
             t["obs"] = (P["x"], n, H.ACT_RELU, P["st"], P["rmm"] if loc else None, P["qp"] if loc else None,
                         1, qd, 1e-8, P["ws"], H.c_i64(t["ws"].numel()), P["cnt"], st)
-            t["fin"] = (P["st"], P["rmm"], P["qp"], 1, qd, 1e-8, st)
+            t["gat"] = torch.empty(world * H.ST_LEN, dtype=torch.float64, device=dev)
+            t["fin"] = (H.ptr(t["gat"]), world, P["st"], P["rmm"], P["qp"], 1, qd, 1e-8, st)
             t["fq"] = (P["x"], P["y"], None, None, n, H.ACT_RELU, P["qp"], None, 0.0, None, 0.0, 0, 0,
                        self.qmin, self.qmax, st)
             self.L.append(t)
-        self.f_obs, self.f_fin, self.f_fq = lib.vsiq_act_observe_f32, lib.vsiq_observe_finalize, lib.vsiq_act_fq_fwd_f32
+        self.f_obs, self.f_fin, self.f_fq = (lib.vsiq_act_observe_f32, lib.vsiq_observe_finalize_ranks,
+                                             lib.vsiq_act_fq_fwd_f32)
         self.n = sum(t["x"].numel() for t in self.L)
         self.slots = [None]
         self.kernels = {"observe_quant_all_layers": 12 * self.n}
 
     def launch(self, i):
-        from vsiquantization_amd.distributed import allreduce_stats
+        from vsiquantization_amd.distributed import gather_stats
         rc = 0
         for t in self.L:
             rc |= self.f_obs(*t["obs"])
-            if self.world > 1:
-                allreduce_stats(t["st"])
+            if self.world > 1:   # one all_gather of the 10-double records + one fold launch
+                gather_stats(t["st"], out=t["gat"])
                 rc |= self.f_fin(*t["fin"])
             rc |= self.f_fq(*t["fq"])
         return rc
@@ -948,7 +950,7 @@ def describe(W, key, a, world):
         cfg.update(layers=len(W.layers), total_batch=ACT_BATCH, images_per_gpu=W.batch,
                    elements_per_gpu_per_step=W.n, bits_a=4, observer_bits=8,
                    parallelism=f"dp x{world} (batch {ACT_BATCH} split over the ranks; per layer one "
-                               "RCCL exchange of the observer stats)" if world > 1 else "1 GPU, no exchange",
+                               "RCCL all_gather of the observer stats records)" if world > 1 else "1 GPU, no exchange",
                    note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
     return cfg
 

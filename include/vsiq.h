@@ -185,6 +185,17 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
                           double qden, double eps, void *stream);
 
 /*
+ * The same epilogue from `world` per-rank stats records gathered in rank order
+ * (gathered[world][VSIQ_ST_LEN], an all_gather of each rank's vsiq_observe_f32 record):
+ * folds them (min / max exact, counts and sums in float64 in rank order), writes the
+ * whole batch's stats record (stats_out nullable) and applies the running update +
+ * qparams.  The per-call multi-GPU observer: one collective and one launch
+ * per call.
+ */
+int vsiq_observe_finalize_ranks(const double *gathered, int world, double *stats_out, float *run_minmax,
+                                double *qp_out, int symmetric, double qden, double eps, void *stream);
+
+/*
  * Per-tensor observe + fake quant of a small tensor in ONE launch (K8): n <=
  * vsiq_observe_fq_max_elems() (65536).  Equal to vsiq_act_observe_f32(c, n, act,
  * stats_out, run_minmax, qp_out, ...) followed by vsiq_act_fq_fwd_f32(c, y, codes, mask,

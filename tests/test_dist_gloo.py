@@ -124,3 +124,26 @@ def test_sync_calibration_call_count_check(counts, ok):
         assert ret[0] == ret[1] == "ok"
     else:
         assert "different deferred observer calls" in ret[0] and "different deferred observer calls" in ret[1]
+
+
+def _gather_worker(rank, world, port, ret):
+    from vsiquantization_amd.distributed import gather_stats
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = torch.arange(H.ST_LEN, dtype=torch.float64) + 100 * rank
+        ret[rank] = gather_stats(st).numpy().copy()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_stats_rank_order():
+    """distributed.gather_stats (the per-call exchange: ONE collective per observer call,
+    folded on the device by vsiq_observe_finalize_ranks): every rank holds all records in
+    rank order."""
+    port = 29700 + os.getpid() % 1000
+    ret = mp.Manager().dict()
+    mp.spawn(_gather_worker, args=(3, port, ret), nprocs=3, join=True)
+    want = np.concatenate([np.arange(H.ST_LEN) + 100 * r for r in range(3)]).astype(np.float64)
+    for r in range(3):
+        assert np.array_equal(ret[r], want)

@@ -67,6 +67,7 @@ _SIGS = {
                         c_int),
     "vsiq_observe_f32": ([c_p, c_i64, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p], c_int),
     "vsiq_observe_finalize": ([c_p, c_p, c_p, c_int, c_d, c_d, c_p], c_int),
+    "vsiq_observe_finalize_ranks": ([c_p, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p], c_int),
     "vsiq_pc_observe_fq_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_int, c_int,
                                 c_int, c_d, c_d, c_p], c_int),
     "vsiq_pc_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_p], c_int),

@@ -451,6 +451,30 @@ __global__ void k_observe_finalize(const double *__restrict__ stats, float *__re
                   run_minmax, qp_out, sym, qden, eps);
 }
 
+// Per-call multi-GPU observer exchange, the fold side: `world` stats records gathered
+// from the ranks (all_gather, rank order) -> the whole batch's record (min / max exact,
+// counts and sums in float64 in rank order: the same bits on every rank) -> fp32 means /
+// std (qm.py:66-68) -> running update + f64 qparams (minmax.py:42-74).  One launch
+// instead of two all-reduces plus the host-side finish of round 1.
+__global__ void k_observe_finalize_ranks(const double *__restrict__ gathered, int world,
+                                         double *__restrict__ stats_out, float *__restrict__ run_minmax,
+                                         double *__restrict__ qp_out, int sym, double qden, double eps) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double f[6] = {__builtin_inf(), -__builtin_inf(), 0.0, 0.0, 0.0, 0.0};
+  double n = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const double *g = gathered + (int64_t)r * VSIQ_ST_LEN;
+    f[0] = __builtin_fmin(f[0], g[VSIQ_ST_MIN]);
+    f[1] = __builtin_fmax(f[1], g[VSIQ_ST_MAX]);
+    f[2] += g[VSIQ_ST_NAN];
+    f[3] += g[VSIQ_ST_SUMABS];
+    f[4] += g[VSIQ_ST_SUM];
+    f[5] += g[VSIQ_ST_SUMSQ];
+    n += g[VSIQ_ST_N];
+  }
+  if (stats_out) write_stats(stats_out, f, (int64_t)n);
+  observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax, qp_out, sym, qden, eps);
+}
 
 // ----------------------------------------------------------------------------
 // exhaustive check of fdiv against the IEEE division: every 32-bit pattern a,
@@ -865,6 +889,14 @@ int vsiq_observe_finalize(const double *stats, float *run_minmax, double *qp_out
   if (!stats) return VSIQ_E_ARG;
   hipLaunchKernelGGL(k_observe_finalize, dim3(1), dim3(kWave), 0, (hipStream_t)stream, stats,
                      run_minmax, qp_out, symmetric, qden, eps);
+  return launch_rc();
+}
+
+int vsiq_observe_finalize_ranks(const double *gathered, int world, double *stats_out, float *run_minmax,
+                                double *qp_out, int symmetric, double qden, double eps, void *stream) {
+  if (!gathered || world <= 0) return VSIQ_E_ARG;
+  hipLaunchKernelGGL(k_observe_finalize_ranks, dim3(1), dim3(kWave), 0, (hipStream_t)stream, gathered, world,
+                     stats_out, run_minmax, qp_out, symmetric, qden, eps);
   return launch_rc();
 }
 

@@ -13,8 +13,9 @@ the qparams are therefore bit-identical to a 1-GPU run; the sums differ only in
 float64 summation order.
 
 Two modes:
-* per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): two tiny
-  all-reduces per observer call, needed when the same call also fake-quantizes
+* per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): one tiny
+  all_gather of the stats records per observer call and one fold launch
+  (``gather_finalize``), needed when the same call also fake-quantizes
   (observe+quantize mode, §3.4);
 * deferred  (``dist_defer`` True, calibration): each rank only writes its local
   per-call partial records (K2p, no cross-workgroup fold, no atomics);
@@ -57,6 +58,39 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     stats[..., H.ST_MAX] = mm[..., 1]
     stats[..., _SUM_SLICE] = sums
     return finish_stats(stats)
+
+
+def gather_stats(stats: torch.Tensor, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """One collective: every rank's stats record ``[ST_LEN]`` gathered in rank order into
+    ``[world * ST_LEN]`` (all_gather_into_tensor; the list form where a backend lacks it)."""
+    world = dist.get_world_size(group)
+    if out is None:
+        out = torch.empty(world * H.ST_LEN, dtype=stats.dtype, device=stats.device)
+    src = stats.contiguous()
+    try:
+        dist.all_gather_into_tensor(out, src, group=group)
+    except (RuntimeError, NotImplementedError, ValueError):
+        dist.all_gather(list(out.view(world, H.ST_LEN).unbind(0)), src, group=group)
+    return out
+
+
+def gather_finalize(stats: torch.Tensor, run_minmax: torch.Tensor, *, symmetric: bool, num_bits: int = 8,
+                    eps: float = 1e-8, group=None):
+    """Per-call multi-GPU observer exchange: gather the ranks' stats records (one
+    collective), then ONE launch folds them in rank order (min / max exact, sums in float64
+    -- the same bits on every rank), writes the batch's stats record and applies the
+    running update + f64 qparams (vsiq_observe_finalize_ranks).  Returns (stats f64[ST_LEN],
+    qp f64[QP_LEN]); min/max/qparams bit-identical to one GPU over the whole batch."""
+    from .fakequant import qden
+    gathered = gather_stats(stats, group)
+    dev = stats.device
+    st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev)
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev)
+    rc = H.lib().vsiq_observe_finalize_ranks(H.ptr(gathered), int(dist.get_world_size(group)), H.ptr(st),
+                                             H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
+                                             qden(symmetric, num_bits, eps), float(eps), H.stream_of(dev))
+    H.check(rc, "vsiq_observe_finalize_ranks")
+    return st, qp
 
 
 def replay_minmax(min_val, max_val, records):

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 from .. import _hip as H
 from .. import observe_batch
-from ..fakequant import (observe_finalize, observe_parts, observe_tensor, part_slot_doubles,
+from ..fakequant import (observe_parts, observe_tensor, part_slot_doubles,
                          stats_from_row_sums)
 from ..observers.minmax import MinMaxObserver
 from ..observers.per_channel import PerChannelMinMaxObserver
@@ -190,7 +190,7 @@ class QuantizationManager(nn.Module):
 
     # ------------------------------------------------------------------ multi-GPU observer
     def _collect_distributed(self, x, act=None):
-        from ..distributed import allreduce_stats
+        from ..distributed import gather_finalize
         obs = self.observer
         if self.dist_defer:
             # deferred (calibration): K2p partial records only -- no fold, no running
@@ -209,9 +209,9 @@ class QuantizationManager(nn.Module):
             return
         _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
                                run_minmax=None, want_qp=False, want_stats=True, act=act)
-        allreduce_stats(st, group=self.dist_group)
         state = obs.device_state(x.device)
-        qp = observe_finalize(st, state, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps)
+        st, qp = gather_finalize(st, state, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
+                                 group=self.dist_group)
         obs._dirty = True
         self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
         self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
