@@ -908,6 +908,35 @@ def api_us_per_step(dev, steps=300, warmup=30):
     return reps[2], reps[0]
 
 
+def api_graph_us_per_step(dev, steps=300):
+    """The same public-API C2 step captured once with utils.graph.GraphedStep and replayed
+    (the way to drop the per-step host cost of the Python API and torch's autograd engine):
+    time per replay, median of 5 runs."""
+    import vsiquantization_amd as V
+    from vsiquantization_amd.utils.graph import GraphedStep
+    shape = C2PerChannel.shape
+    gen = torch.Generator(device=dev).manual_seed(11)
+    w = (torch.randn(shape, device=dev, generator=gen) * 0.05).requires_grad_(True)
+    g = torch.randn(shape, device=dev, generator=gen)
+    obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+
+    def step():
+        y, _ = obs.observe_quantize(w, q)
+        y.backward(g)
+        return y
+
+    gs = GraphedStep(step, grads_of=[w])
+    reps = []
+    for r in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps // 5):
+            gs()
+        torch.cuda.synchronize()
+        reps.append((time.perf_counter() - t0) / (steps // 5) * 1e6)
+    return sorted(reps)[2]
+
+
 METRICS = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + achieved HBM GB/s vs roofline",
            "c2": "Melements/s fake-quant fwd+bwd (per-channel int8) + achieved HBM GB/s vs roofline",
            "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
@@ -1036,6 +1065,7 @@ def main(argv=None):
     if a.workload == "c2" and not a.no_api:
         progress("c2: public API timing")
         out["api_us_per_step"], out["api_us_per_step_min"] = api_us_per_step(dev)
+        out["api_graph_us_per_step"] = api_graph_us_per_step(dev)
         torch.cuda.empty_cache()
 
     extras = {}

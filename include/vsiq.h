@@ -106,8 +106,10 @@ int vsiq_set_tuning(int key, int value);
  * Store-gate tuner (VSIQ_TUNE_GATE_AUTOTUNE).  The only state the library keeps
  * between calls besides the knobs: per launch site, a handful of HIP event pairs and
  * the timings they returned (host memory; no device memory, no host sync).
- *   vsiq_gate_tuning_pending: sites still tuning after harvesting finished timings
- *     (a caller that wants steady-state launches runs warm-up calls until it is 0);
+ *   vsiq_gate_tuning_pending: sites launched since the previous call of it that are
+ *     still tuning after harvesting finished timings (a caller that wants steady-state
+ *     launches runs warm-up steps and calls it after each, until it is 0: sites of other
+ *     work that is not running any more do not count);
  *   vsiq_gate_report: one text line per site (label, grid, bytes, chosen ticks, median
  *     launch time per candidate in us) into buf (NUL-terminated, truncated to len);
  *     returns the full length;

@@ -163,3 +163,38 @@ def test_two_graphs_own_workspaces_and_replay_concurrently():
         for (gx, gsr), x, s in zip(ref, xs, ss):
             assert torch.equal(x.grad, gx)
             assert torch.equal(s.grad, gsr)
+
+
+def test_graphed_step_c2_public_api_equals_eager():
+    """utils.graph.GraphedStep on the C2 step through the public API
+    (PerChannelMinMaxObserver.observe_quantize + backward): every replay gives the eager
+    y and dW bit for bit (fresh observer state each step: the same weight, so the same
+    running min/max), and the tuner had settled before the capture."""
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd.utils.graph import GraphedStep
+    torch.manual_seed(3)
+    w = (torch.randn(1024, 256, 3, 3, device=DEV) * 0.05).requires_grad_(True)
+    g = torch.randn_like(w)
+    obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+
+    def step():
+        y, _ = obs.observe_quantize(w, q)
+        y.backward(g)
+        return y
+
+    w.grad = None
+    y_ref = step().detach().clone()
+    gw_ref = w.grad.clone()
+    gs = GraphedStep(step, grads_of=[w])
+    torch.cuda.synchronize()
+    H.gate_tuning_pending()
+    step()          # an eager step launches the same sites: all of them settled
+    torch.cuda.synchronize()
+    assert H.gate_tuning_pending() == 0
+    w.grad = None
+    gs = GraphedStep(step, grads_of=[w])
+    for _ in range(3):
+        y = gs()
+    torch.cuda.synchronize()
+    assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
+    assert torch.equal(w.grad.view(torch.int32), gw_ref.view(torch.int32))

@@ -38,6 +38,7 @@ struct Site {
   int rr = 0;
   bool done = false;
   uint32_t best = 0;
+  uint64_t last_sel = 0;            // g_sel when this site was last launched
 };
 
 struct Sample {
@@ -53,6 +54,8 @@ std::mutex g_mu;
 std::map<Key, Site> g_sites;
 std::vector<Sample *> g_pending;
 std::map<int, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_pool;
+uint64_t g_sel = 0;    // launches through the tuner (a clock for "launched since")
+uint64_t g_mark = 0;   // g_sel at the previous vsiq_gate_tuning_pending()
 
 uint32_t clamp_ticks(double t, int khz) {
   const double cap = kCapUs * khz / 1e3;
@@ -128,6 +131,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   }
   std::lock_guard<std::mutex> lk(g_mu);
   Site &s = g_sites[Key{kernel, grid, read_bytes, dev}];
+  s.last_sel = ++g_sel;
   if (s.grid == 0) {
     s.label = label;
     s.grid = grid;
@@ -205,7 +209,8 @@ int gate_sites_tuning() {
   harvest_locked();
   int n = 0;
   for (auto &kv : g_sites)
-    if (!kv.second.done) ++n;
+    if (!kv.second.done && kv.second.last_sel > g_mark) ++n;
+  g_mark = g_sel;
   return n;
 }
 

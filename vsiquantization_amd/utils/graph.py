@@ -1,0 +1,67 @@
+"""Whole-step HIP-graph capture for QAT steps built on this package (MI355X-native
+replacement for a tracing compiler: the reference runs every step eagerly, one Python
+dispatch per op).
+
+Every kernel of the package launches on torch's current stream, never synchronises the
+host and keeps its reduction workspace per capture (`_hip.workspace`), so a forward +
+backward through the public API (FakeQuantize / QuantizationManager / the fused layers,
+quantizers/uniform.py:34-56, observers/minmax.py:32-88) can be captured once and
+replayed: the replay costs the GPU time plus one graph launch, whatever the number of
+layers.  ``GraphedStep`` adds the two things a capture of this package needs: warm-up
+steps on a side stream (allocator pools, lazily created tensors), and, before the
+capture, steps until the store-gate tuner has settled every launch site the step uses
+(a capture bakes the gate in; csrc/gate_tune.hip never times a captured launch).
+
+    step = GraphedStep(lambda: model(x).square().mean().backward(), grads_of=model.parameters())
+    for _ in range(iters):
+        step()            # replay; inputs are updated in place (x.copy_(batch))
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _hip as H
+
+
+class GraphedStep:
+    """Capture ``fn`` (no arguments; reads and writes persistent tensors) into a HIP graph.
+
+    ``fn`` runs ``warmup`` times on a side stream, then until the store-gate tuner has no
+    site left to tune (at most ``settle_max`` more runs), then once under capture.  Calling
+    the object replays the graph on the current stream and returns what the captured run
+    returned (its tensors are overwritten by every replay).  ``grads_of``: tensors whose
+    ``.grad`` is set to None before each warm-up run and before the capture, so that the
+    captured backward WRITES their gradients (AccumulateGrad then keeps the produced
+    buffer) and every replay leaves exactly one step's gradient there.
+    """
+
+    def __init__(self, fn, warmup: int = 3, settle_max: int = 400, grads_of=()):
+        self.fn = fn
+        self.params = list(grads_of)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._clear()
+                fn()
+            torch.cuda.current_stream().synchronize()
+            H.gate_tuning_pending()   # from here on: the sites this step launches
+            for _ in range(settle_max):
+                self._clear()
+                fn()
+                torch.cuda.current_stream().synchronize()
+                if H.gate_tuning_pending() == 0:
+                    break
+        torch.cuda.current_stream().wait_stream(side)
+        self._clear()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = fn()
+
+    def _clear(self):
+        for p in self.params:
+            p.grad = None
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out
