@@ -345,6 +345,37 @@ int vsiq_lsq_bwd_multi_f32(const vsiq_lsq_tensor *tensors, int count, double *ws
                            uint32_t *counter, void *stream);
 
 /*
+ * Learnable backward with the scale / zero-point gradient fold deferred (K4d).
+ * vsiq_act_lsq_bwd_part_f32 is vsiq_act_lsq_bwd_f32 without the cross-workgroup
+ * reduction: grad_x (bit-identical) plus one {sum t, sum z} record per workgroup into
+ * records[2 * vsiq_lsq_part_records(n)] -- no workspace drain, no arrival atomics, no
+ * last-block fold (3-5 us of every K4 launch at 2-26M elements).  vsiq_lsq_fold_multi
+ * then folds `count` such calls (each its own records) into grad_out[2] = {grad_scale,
+ * grad_zp} exactly as vsiq_act_lsq_bwd_f32 defines them (to float64 summation order), 64
+ * calls per launch.  The activation quantizers of a QAT model (quantize_out of every fused
+ * layer, fake_quantize.py:49-50 -> uniform.py:47-56) are folded in one launch when
+ * autograd has been through all of them (quantizers/deferred.py).
+ */
+typedef struct vsiq_lsq_fold {
+  const double *records;   /* the call's records, nrec x {sum t, sum z} */
+  int64_t nrec;            /* vsiq_lsq_part_records(n) of the call */
+  const double *zp_dev;    /* the zero point the forward used (NULL: zp_host) */
+  double zp_host;
+  double gscale;           /* ScaleGradient factor */
+  double *grad_out;        /* f64[2] {grad_scale, grad_zp}, overwritten */
+  int32_t qmin;
+  int32_t qmax;
+  int32_t zp_learn;
+  int32_t reserved;
+} vsiq_lsq_fold;
+int64_t vsiq_lsq_part_records(int64_t n);
+int vsiq_act_lsq_bwd_part_f32(const float *g, const float *c, float *gc, int64_t n, int act,
+                              const double *scale_dev, double scale_host, const double *zp_dev, double zp_host,
+                              int zp_learn, int qmin, int qmax, double *records, int64_t records_len,
+                              void *stream);
+int vsiq_lsq_fold_multi(const vsiq_lsq_fold *folds, int count, void *stream);
+
+/*
  * Fused activation + activation fake-quant (K5).  Replaces, in the fused layers,
  * F.relu / F.silu after the conv (modules/fused.py:124-134, :198-206) followed by
  * quantize_out (quantizers/fake_quantize.py:49-50): the conv output c is read

@@ -1,0 +1,172 @@
+"""Deferred learnable-qparam gradient fold (K4d: vsiq_act_lsq_bwd_part_f32 +
+vsiq_lsq_fold_multi; quantizers/deferred.py).  grad_x bit for bit equal to K4's, the
+folded scale / zero-point gradients equal to K4's in-kernel fold to float64 summation
+order and to the oracle's f64 closed form (uniform.py:47-56, ScaleGradient :242-255);
+through autograd, a fused QAT model's step equals the per-call path."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import vsiquantization_amd as V
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import fakequant as FQ
+from vsiquantization_amd.quantizers import deferred as D
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("act", [None, "relu"])
+@pytest.mark.parametrize("learn_zp", [False, True])
+def test_part_and_fold_equal_k4_and_oracle(act, learn_zp):
+    rng = np.random.default_rng(17 + int(learn_zp))
+    sizes = [1, 7, 1000, 65536, 1 << 20, 3 * (1 << 20) + 3] + [4096 + 13 * k for k in range(66)]   # 72 calls
+    qmin, qmax = (0, 15) if learn_zp else (-8, 7)
+    calls = []
+    for n in sizes:
+        x = (rng.standard_normal(n) * 0.3).astype(np.float32)
+        g = rng.standard_normal(n).astype(np.float32)
+        s, z = float(rng.uniform(0.01, 0.1)), (float(rng.integers(3, 12)) + 0.3 if learn_zp else 0.0)
+        gscale = (qmax * n) ** -0.5
+        calls.append((x, g, s, z, gscale))
+    folds = []
+    for x, g, s, z, gscale in calls:
+        xd, gd = torch.from_numpy(x).to(DEV), torch.from_numpy(g).to(DEV)
+        sd = torch.tensor(s, dtype=torch.float64, device=DEV)
+        zd = torch.tensor(z, dtype=torch.float64, device=DEV) if learn_zp else 0.0
+        gx_ref, grads_ref = FQ.lsq_backward(gd, xd, sd, zd, qmin, qmax, gscale, learn_zp, act=act)
+        e = D._Fold()
+        e.nrec = int(H.lib().vsiq_lsq_part_records(H.c_i64(x.size)))
+        e.records = torch.full((2 * e.nrec,), float("nan"), dtype=torch.float64, device=DEV)
+        gx, e.zd, e.zh = D.lsq_backward_part(gd, xd, sd, zd, qmin, qmax, learn_zp, act, e.records)
+        e.gscale, e.qmin, e.qmax, e.learn_zp = gscale, qmin, qmax, learn_zp
+        e.out = torch.empty(2, dtype=torch.float64, device=DEV)
+        e.keep = (sd, zd)
+        folds.append((e, gx, gx_ref, grads_ref, x, g, s, z, gscale))
+    D.fold([f[0] for f in folds])
+    torch.cuda.synchronize()
+    for e, gx, gx_ref, grads_ref, x, g, s, z, gscale in folds:
+        assert torch.equal(gx.view(torch.int32), gx_ref.view(torch.int32))
+        got, ref = e.out.cpu().numpy(), grads_ref.cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
+        if act is None:
+            _, gxo, gso, gzo = O.lsq_forward_backward(x, g, s, z, qmin, qmax, gscale, learn_zp=learn_zp)
+            G.assert_bitwise_f32(gx.cpu().numpy(), gxo, "grad_x")
+            np.testing.assert_allclose(got[0], gso, rtol=1e-9, atol=1e-300)
+            if learn_zp:
+                np.testing.assert_allclose(got[1], gzo, rtol=1e-9, atol=1e-300)
+
+
+def _model(act_learn_zp=False):
+    from vsiquantization_amd.modules.fused import ConvBnReLU
+    from vsiquantization_amd.utils.quantize_manager import (activate_learning_qparam, activate_quantizer,
+                                                            calibrate_qat_model, data_calib)
+    torch.manual_seed(0)
+    layers = []
+    for cin, cout in ((3, 16), (16, 32), (32, 32)):
+        bn = nn.BatchNorm2d(cout)
+        bn.running_var.uniform_(0.5, 2.0)
+        layers.append(ConvBnReLU(nn.Conv2d(cin, cout, 3, padding=1, bias=False), bn, nn.ReLU(),
+                                 "MinMaxObserver", "UniformQuantizer", "MinMaxObserver", "UniformQuantizer",
+                                 True, True, True, 4, 4))
+    model = nn.Sequential(*layers).to(DEV)
+    gen = torch.Generator().manual_seed(1)
+    loader = [(torch.randint(0, 256, (4, 3, 32, 32), generator=gen, dtype=torch.uint8), None) for _ in range(2)]
+    calibrate_qat_model(model, loader, data_calib, DEV)
+    activate_learning_qparam(model)
+    activate_quantizer(model)
+    model.eval()
+    return model
+
+
+@pytest.mark.parametrize("multi_weights", [False, True])
+def test_model_step_deferred_equals_per_call(multi_weights):
+    """A fused QAT model's forward + backward with enable_deferred_qparam_grads: output,
+    grad of the input and conv biases bit for bit; the activation quantizers' f64 scale
+    gradients within 1e-12 of the per-call path (float64 summation order); conv weights
+    and weight-quantizer scales within MIOpen's wgrad nondeterminism (1e-5); nothing left
+    pending."""
+    a = _model()
+    b = copy.deepcopy(a)
+    handles = [V.enable_deferred_qparam_grads(a)]
+    if multi_weights:
+        handles += [V.enable_multi_tensor_weights(a), V.enable_multi_tensor_weights(b)]
+    x = torch.rand(4, 3, 32, 32, device=DEV)
+    outs = []
+    for m in (a, b):
+        xi = x.clone().requires_grad_(True)
+        y = m(xi)
+        y.square().mean().backward()
+        outs.append((y.detach(), xi.grad))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    for (na, pa), (nb, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert na == nb
+        if pa.grad is None:
+            assert pb.grad is None, na
+            continue
+        if "activation_quantizer" in na or "input_quantizer" in na:
+            np.testing.assert_allclose(pa.grad.cpu().numpy(), pb.grad.cpu().numpy(), rtol=1e-12, atol=1e-300,
+                                       err_msg=na)
+        elif na.endswith("weight") or "weight_quantizer" in na:
+            # the weight quantizer's gradient is computed from MIOpen's weight-gradient
+            # convolution, which is not bit-reproducible run to run (~1e-7 relative)
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-5, atol=1e-12, msg=na)
+        else:
+            assert torch.equal(pa.grad, pb.grad), na
+    assert not D._PENDING
+    for h in handles:
+        h.remove()
+
+
+def test_model_step_deferred_graph_replay_equals_eager():
+    from vsiquantization_amd.utils.graph import GraphedStep
+    m = _model()
+    h = V.enable_deferred_qparam_grads(m)
+    x = torch.rand(4, 3, 32, 32, device=DEV)
+    params = [p for p in m.parameters() if p.requires_grad]
+
+    def step():
+        y = m(x)
+        y.square().mean().backward()
+        return y
+
+    for p in params:
+        p.grad = None
+    y_ref = step().detach().clone()
+    g_ref = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    gs = GraphedStep(step, grads_of=params)
+    for _ in range(2):
+        y = gs()
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    for n, p in m.named_parameters():
+        if n in g_ref:
+            if n.endswith("conv_fuse.weight") or n.endswith("weight_quantizer.scale"):
+                torch.testing.assert_close(p.grad, g_ref[n], rtol=1e-5, atol=1e-12, msg=n)
+            else:
+                assert torch.equal(p.grad, g_ref[n]), n
+    h.remove()
+
+
+def test_second_use_in_one_forward_takes_per_call_path():
+    """A manager called twice in one forward: the first call uses the bundle, the second
+    the per-call path; gradients equal the per-call path's."""
+    q = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", 8, True, is_learning_scale=True)
+    q.scale = nn.Parameter(torch.tensor(0.05, dtype=torch.float64, device=DEV))
+    x = torch.randn(1000, device=DEV, requires_grad=True)
+    ref = copy.deepcopy(q)
+    D.bundle_qparams([q])
+    (q.quantize(x) + q.quantize(x * 2)).sum().backward()
+    x2 = x.detach().clone().requires_grad_(True)
+    (ref.quantize(x2) + ref.quantize(x2 * 2)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(x.grad, x2.grad)
+    np.testing.assert_allclose(float(q.scale.grad), float(ref.scale.grad), rtol=1e-12)
+    assert not D._PENDING

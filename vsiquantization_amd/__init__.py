@@ -27,5 +27,6 @@ from .quantizers.quantization_manager import QuantizationManager  # noqa: F401
 from .quantizers.fake_quantize import FakeQuantize  # noqa: F401
 from .quantizers.lsq_module import LSQFakeQuantize  # noqa: F401
 from .quantizers.foreach import enable_multi_tensor_weights, quantize_weights_multi  # noqa: F401
+from .quantizers.deferred import bundle_qparams, enable_deferred_qparam_grads  # noqa: F401
 
 __version__ = "0.1.0"

@@ -87,6 +87,10 @@ _SIGS = {
     "vsiq_observe_part_records": ([c_i64], c_i64),
     "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
     "vsiq_act_observe_part_multi_f32": ([c_p, c_int, c_int, c_p], c_int),
+    "vsiq_lsq_part_records": ([c_i64], c_i64),
+    "vsiq_act_lsq_bwd_part_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_p, c_i64,
+                                   c_p], c_int),
+    "vsiq_lsq_fold_multi": ([c_p, c_int, c_p], c_int),
     "vsiq_observe_fq_max_elems": ([], c_i64),
     "vsiq_act_observe_fq_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_int, c_int,
                                  c_p], c_int),
@@ -106,6 +110,13 @@ class LsqTensor(ctypes.Structure):
     _fields_ = [("x", c_p), ("y", c_p), ("g", c_p), ("gx", c_p), ("scale_dev", c_p), ("zp_dev", c_p),
                 ("grad_out", c_p), ("n", c_i64), ("scale_host", c_d), ("zp_host", c_d), ("gscale", c_d),
                 ("qmin", ctypes.c_int32), ("qmax", ctypes.c_int32), ("zp_learn", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class LsqFold(ctypes.Structure):
+    """vsiq_lsq_fold (include/vsiq.h): one call of a deferred scale-gradient fold."""
+    _fields_ = [("records", c_p), ("nrec", c_i64), ("zp_dev", c_p), ("zp_host", c_d), ("gscale", c_d),
+                ("grad_out", c_p), ("qmin", ctypes.c_int32), ("qmax", ctypes.c_int32), ("zp_learn", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
 
 

@@ -4,7 +4,10 @@
 
 namespace vsiq {
 
-template <bool VEC, bool NT, bool ZPL, int ACT, int G>
+// PART: the block record {sum t, sum z} goes to ws[2 * block] with a plain store and
+// the block leaves -- no drain, no arrival, no fold (vsiq_act_lsq_bwd_part_f32: the
+// fold of every layer's records runs later in one launch, k_lsq_fold_multi).
+template <bool VEC, bool NT, bool ZPL, int ACT, int G, bool PART = false>
 __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ x,
                                                     float *__restrict__ gx, int64_t n,
@@ -19,6 +22,14 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o);
   double rec[2], f[2];
   if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
+  if (PART) {
+    if (threadIdx.x == 0) {
+      ws[2 * (int64_t)blockIdx.x] = rec[0];
+      ws[2 * (int64_t)blockIdx.x + 1] = rec[1];
+    }
+    lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
+    return;
+  }
   if (VSIQ_EXP_K4 & 4) {   // experiment: no arrival / fold (gradient not produced)
     lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
     return;
@@ -40,6 +51,15 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
                   double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                   hipStream_t st) {
   const int pf = 0;
+  if (!counter) {   // records only (PART)
+    if (zpl)
+      hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT, G, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g,
+                         x, gx, n, src, gscale, pf, grad_out, ws, counter);
+    else
+      hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT, G, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g,
+                         x, gx, n, src, gscale, pf, grad_out, ws, counter);
+    return;
+  }
   if (zpl)
     hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
                        gx, n, src, gscale, pf, grad_out, ws, counter);
@@ -90,6 +110,65 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
   VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
            (hipStream_t)stream);
   return launch_rc();
+}
+
+// Records-only K4 (PART): same grid, per-element code and block records as lsq_bwd.
+int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, const double *scale_dev,
+                 double scale_host, const double *zp_dev, double zp_host, int zp_learn, int qmin, int qmax,
+                 double *records, int64_t records_len, void *stream) {
+  if (n <= 0 || !g || !x || !gx || !records || qmin > qmax || act < kActNone || act > kActSilu)
+    return VSIQ_E_ARG;
+  const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
+  const int64_t grid = lsq_grid(cdiv(n, 4));
+  if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (records_len < 2 * grid) return VSIQ_E_WS;
+  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
+  const bool nt = g_tune.nontemporal != 0;
+  VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, 0.0, nullptr, records, nullptr, grid,
+           (hipStream_t)stream);
+  return launch_rc();
+}
+
+// ----------------------------------------------------------------------------
+// Fold of records-only K4 calls: workgroup t folds call t's block records (thread j
+// sums records j, j + 256, ... in order, then the fixed block tree) -> grad_out[t] =
+// {sum t * gscale, ClampBackward of the rounded zp ? sum z * gscale : 0}
+// (quantizers/uniform.py:47-56 + ScaleGradient :242-255, zero_point_rounding :98-102).
+// ----------------------------------------------------------------------------
+constexpr int kFoldMulti = 64;   // calls per launch (descriptor table in the kernel arguments)
+
+struct FCall {
+  const double *rec;
+  const double *zdev;
+  double *out;
+  int64_t nrec;
+  double zhost, gscale;
+  float lo, hi;
+  int zpl;
+};
+
+struct FBatch {
+  FCall t[kFoldMulti];
+  int count;
+};
+
+__global__ __launch_bounds__(kBlock) void k_lsq_fold_multi(const FBatch b) {
+  const FCall &T = b.t[blockIdx.x];
+  LsqAcc acc{0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < T.nrec; i += kBlock) {
+    acc.t += T.rec[2 * i];
+    acc.z += T.rec[2 * i + 1];
+  }
+  lsq_block_reduce(acc);
+  if (threadIdx.x == 0) {
+    T.out[0] = acc.t * T.gscale;
+    double gz = 0.0;
+    if (T.zpl) {
+      const double zr = __builtin_rint(T.zdev ? *T.zdev : T.zhost);
+      gz = (zr >= (double)T.lo && zr <= (double)T.hi) ? acc.z * T.gscale : 0.0;
+    }
+    T.out[1] = gz;
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -434,6 +513,39 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
                          void *stream) {
   return lsq_bwd(g, c, gc, n, act, scale_dev, scale_host, zp_dev, zp_host, zp_learn, qmin, qmax,
                  gscale, grad_out, ws, ws_len, counter, stream);
+}
+
+int64_t vsiq_lsq_part_records(int64_t n) {
+  if (n <= 0) return VSIQ_E_ARG;
+  return lsq_grid(cdiv(n, 4));
+}
+
+int vsiq_act_lsq_bwd_part_f32(const float *g, const float *c, float *gc, int64_t n, int act,
+                              const double *scale_dev, double scale_host, const double *zp_dev, double zp_host,
+                              int zp_learn, int qmin, int qmax, double *records, int64_t records_len,
+                              void *stream) {
+  return lsq_bwd_part(g, c, gc, n, act, scale_dev, scale_host, zp_dev, zp_host, zp_learn, qmin, qmax, records,
+                      records_len, stream);
+}
+
+int vsiq_lsq_fold_multi(const vsiq_lsq_fold *folds, int count, void *stream) {
+  if (count < 0 || (count > 0 && !folds)) return VSIQ_E_ARG;
+  for (int i = 0; i < count; ++i)
+    if (!folds[i].records || folds[i].nrec <= 0 || !folds[i].grad_out || folds[i].qmin > folds[i].qmax)
+      return VSIQ_E_ARG;
+  for (int i0 = 0; i0 < count; i0 += kFoldMulti) {
+    FBatch b{};
+    b.count = std::min(kFoldMulti, count - i0);
+    for (int k = 0; k < b.count; ++k) {
+      const vsiq_lsq_fold &F = folds[i0 + k];
+      b.t[k] = FCall{F.records, F.zp_dev, F.grad_out, F.nrec, F.zp_host, F.gscale, (float)F.qmin, (float)F.qmax,
+                     F.zp_learn};
+    }
+    hipLaunchKernelGGL(k_lsq_fold_multi, dim3((unsigned)b.count), dim3(kBlock), 0, (hipStream_t)stream, b);
+    const int rc = launch_rc();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int64_t vsiq_pcm_workspace_doubles(int64_t rows, int64_t rowlen) {
