@@ -58,6 +58,9 @@ def parse(argv=None):
     p.add_argument("--batch", type=int, default=256, help="C4 batch (reference: 256)")
     p.add_argument("--bits-w", type=int, default=2, help="C4 weight bits (YAML default 2; SURVEY also w8)")
     p.add_argument("--bits-a", type=int, default=4, help="C4 activation bits (YAML default 4; SURVEY also a8)")
+    p.add_argument("--per-call-grads", action="store_true",
+                   help="C4: fold each activation scale gradient inside its K4 launch (round 1) instead of "
+                        "records-only K4 + one fold launch (enable_deferred_qparam_grads)")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-api", action="store_true", help="skip the public-API C2 timing")
@@ -330,18 +333,21 @@ class C4Backbone:
     """C4: the YOLOv8n backbone's 27 ConvBnReLU quantizers at 320x320, batch 256, in the
     learning phase: the 27 learnable weight fake quants as one multi-tensor launch each way
     (k_multi.hip, the path of enable_multi_tensor_weights) and per layer the fused ReLU +
-    learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd).  The conv itself is
+    learnable activation fake quant (K5: K1-relu fwd, K4-relu bwd records-only + ONE fold of
+    the 27 activation scale gradients at the end, the path of enable_deferred_qparam_grads;
+    ``deferred=False``: K4 with its in-kernel fold per layer).  The conv itself is
     MIOpen and out of scope: synthetic conv outputs of the right shapes stand in for it."""
 
     key = "c4"
     name = "C4 YOLOv8n backbone ConvBnReLU fake-quant (weights + fused ReLU/act), learnable"
     group = 4
 
-    def __init__(self, dev, slots, seed_base, batch=256, bits_w=2, bits_a=4):
+    def __init__(self, dev, slots, seed_base, batch=256, bits_w=2, bits_a=4, deferred=True):
         from vsiquantization_amd import _hip as H
         self.H = H
         lib = H.lib()
         st = H.stream_of(dev)
+        self.deferred = deferred
         self.layers = yolov8n_backbone()
         self.shape = (batch, 3, 320, 320)
         qw = (-(2 ** (bits_w - 1)), 2 ** (bits_w - 1) - 1)
@@ -370,10 +376,18 @@ class C4Backbone:
             gsw, gsa = (qw[1] * nw) ** -0.5, (qa[1] * na) ** -0.5
             self.fwd.append((lib.vsiq_act_fq_fwd_f32, (P["c"], P["y"], None, None, H.c_i64(na), H.ACT_RELU,
                                                        None, P["sa"], 0.0, None, 0.0, 0, 0, qa[0], qa[1], st)))
-            self.bwd.append((lib.vsiq_act_lsq_bwd_f32, (P["g"], P["c"], P["gc"], H.c_i64(na), H.ACT_RELU,
-                                                        P["sa"], 0.0, None, 0.0, 0, qa[0], qa[1], gsa,
-                                                        P["grads_a"], P["ws_a"], H.c_i64(t["ws_a"].numel()),
-                                                        P["cnt_a"], st)))
+            if deferred:   # records only; the 27 folds in one launch at the end (quantizers/deferred.py)
+                t["nrec"] = int(lib.vsiq_lsq_part_records(H.c_i64(na)))
+                t["rec_a"] = torch.empty(2 * t["nrec"], dtype=torch.float64, device=dev)
+                self.bwd.append((lib.vsiq_act_lsq_bwd_part_f32, (P["g"], P["c"], P["gc"], H.c_i64(na), H.ACT_RELU,
+                                                                 P["sa"], 0.0, None, 0.0, 0, qa[0], qa[1],
+                                                                 H.ptr(t["rec_a"]), H.c_i64(t["rec_a"].numel()), st)))
+                t["gsa"] = gsa
+            else:
+                self.bwd.append((lib.vsiq_act_lsq_bwd_f32, (P["g"], P["c"], P["gc"], H.c_i64(na), H.ACT_RELU,
+                                                            P["sa"], 0.0, None, 0.0, 0, qa[0], qa[1], gsa,
+                                                            P["grads_a"], P["ws_a"], H.c_i64(t["ws_a"].numel()),
+                                                            P["cnt_a"], st)))
             wdesc.append(dict(x=w.data_ptr(), y=t["wq"].data_ptr(), g=gw.data_ptr(), gx=t["gwx"].data_ptr(),
                               scale_dev=t["sw"].data_ptr(), grad_out=t["grads_w"].data_ptr(), n=nw,
                               gscale=gsw, qmin=qw[0], qmax=qw[1]))
@@ -395,6 +409,12 @@ class C4Backbone:
         self.fwd.insert(0, (lib.vsiq_lsq_fwd_multi_f32, (wp, len(wdesc), st)))
         self.bwd.append((lib.vsiq_lsq_bwd_multi_f32, (wp, len(wdesc), H.ptr(self.ws_w), H.c_i64(self.ws_w.numel()),
                                                       H.ptr(self.cnt_w), st)))
+        if deferred:   # autograd reaches the qparam bundle last: ONE fold of the 27 activation calls
+            self.folds = (H.LsqFold * len(self.keep))()
+            for i, t in enumerate(self.keep):
+                self.folds[i] = H.LsqFold(t["rec_a"].data_ptr(), t["nrec"], None, 0.0, t["gsa"],
+                                          t["grads_a"].data_ptr(), qa[0], qa[1], 0, 0)
+            self.bwd.append((lib.vsiq_lsq_fold_multi, (ctypes.cast(self.folds, ctypes.c_void_p), len(self.keep), st)))
         self.n = n_act + n_w
         self.n_act, self.n_w = n_act, n_w
         self.slots = [None]
@@ -950,7 +970,8 @@ METRICS = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + ac
 
 def build_workload(key, a, dev, rank, world):
     if key == "c4":
-        return C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch, bits_w=a.bits_w, bits_a=a.bits_a)
+        return C4Backbone(dev, a.slots, 1000 * rank, batch=a.batch, bits_w=a.bits_w, bits_a=a.bits_a,
+                          deferred=not a.per_call_grads)
     if key == "c5":
         return C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=16)
     if key == "act":
@@ -966,6 +987,8 @@ def describe(W, key, a, world):
     if key == "c4":
         cfg.update(layers=len(W.layers), bits_w=W.bits[0], bits_a=W.bits[1],
                    act_elements_per_step=W.n_act, weight_elements_per_step=W.n_w,
+                   act_scale_grads=("records-only K4 per layer + one fold launch (deferred)" if W.deferred
+                                    else "folded inside each K4 launch"),
                    parallelism=f"dp x{world} (batch {a.batch} per GPU; quantizer path has no "
                                "collective, scale grads ride DDP's all-reduce)",
                    note="conv (MIOpen) excluded: synthetic conv outputs stand in for it")
