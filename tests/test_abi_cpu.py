@@ -90,6 +90,36 @@ def test_argument_validation_without_gpu():
     assert lib.vsiq_lsq_bwd_multi_f32(p, 1, 16, 7, 16, null) == -3       # workspace too small
 
 
+def test_round2_entry_points_validate_on_host():
+    """K2m, K8, K4d and the rank fold reject bad arguments before any launch."""
+    lib = H.lib()
+    null = None
+    assert ctypes.sizeof(H.PartTensor) == 32 and ctypes.sizeof(H.LsqFold) == 64
+    assert lib.vsiq_act_observe_part_multi_f32(null, 0, 0, null) == 0
+    assert lib.vsiq_act_observe_part_multi_f32(null, 1, 0, null) == -1
+    pt = (H.PartTensor * 1)()
+    assert lib.vsiq_act_observe_part_multi_f32(pt, 1, 0, null) == -1                 # n == 0, null pointers
+    pt[0].c, pt[0].n, pt[0].parts, pt[0].parts_len = 16, 16, 16, 4 * H.PART_LEN - 1
+    assert lib.vsiq_act_observe_part_multi_f32(pt, 1, 0, null) == -3                 # slot too small
+    assert lib.vsiq_act_observe_part_multi_f32(pt, 1, 3, null) == -1                 # bad activation
+    assert lib.vsiq_observe_fq_max_elems() == 65536
+    assert lib.vsiq_act_observe_fq_f32(16, 16, null, null, 65537, 0, null, null, null, 1, 127.0, 1e-8, -128, 127,
+                                       null) == -1
+    assert lib.vsiq_act_observe_fq_f32(16, 16, null, 12, 16, 0, null, null, null, 1, 127.0, 1e-8, -128, 127,
+                                       null) == -2                                    # misaligned mask
+    assert lib.vsiq_lsq_part_records(0) == -1
+    assert lib.vsiq_lsq_part_records(1) == 1
+    assert lib.vsiq_act_lsq_bwd_part_f32(16, 16, 16, 0, 0, null, 1.0, null, 0.0, 0, -8, 7, 16, 2, null) == -1
+    assert lib.vsiq_act_lsq_bwd_part_f32(16, 16, 16, 4, 0, null, 1.0, null, 0.0, 0, -8, 7, 16, 1, null) == -3
+    assert lib.vsiq_lsq_fold_multi(null, 0, null) == 0
+    assert lib.vsiq_lsq_fold_multi(null, 1, null) == -1
+    f = (H.LsqFold * 1)()
+    assert lib.vsiq_lsq_fold_multi(f, 1, null) == -1                                 # no records / output
+    assert lib.vsiq_observe_finalize_ranks(null, 2, null, null, null, 1, 127.0, 1e-8, null) == -1
+    assert lib.vsiq_observe_finalize_ranks(16, 0, null, null, null, 1, 127.0, 1e-8, null) == -1
+    assert lib.vsiq_gate_report(None, 0) >= 0
+
+
 def test_tuning_keys_match_header_and_bounds():
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                             "vsiq.h")).read()
