@@ -21,6 +21,9 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     m = model()
+    if os.environ.get("VSIQ_TEST_DEFERRED") == "1":   # deferred qparam-gradient fold under DDP
+        from vsiquantization_amd import enable_deferred_qparam_grads
+        enable_deferred_qparam_grads(m)
     ddp = DDP(m, device_ids=[0])
     x = batch().chunk(world)[rank]
     ddp(x).square().sum().backward()

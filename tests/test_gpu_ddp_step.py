@@ -29,12 +29,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_ddp_learnable_step_two_ranks(tmp_path):
+@pytest.mark.parametrize("deferred", [False, True])
+def test_ddp_learnable_step_two_ranks(tmp_path, deferred):
+    """deferred: the ranks run enable_deferred_qparam_grads (records-only K4 + one fold at the
+    end of the backward, quantizers/deferred.py): DDP's hooks see the folded gradients."""
     out = tmp_path / "grads.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "ddp_step_worker.py"), str(out)]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, VSIQ_TEST_DEFERRED="1" if deferred else "0")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = json.loads(out.read_text())
     dtypes = got.pop("_dtypes")
