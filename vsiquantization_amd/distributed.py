@@ -62,15 +62,15 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
 
 def gather_stats(stats: torch.Tensor, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
     """One collective: every rank's stats record ``[ST_LEN]`` gathered in rank order into
-    ``[world * ST_LEN]`` (all_gather_into_tensor; the list form where a backend lacks it)."""
+    ``[world * ST_LEN]`` (all_gather_into_tensor over RCCL; the list form on gloo)."""
     world = dist.get_world_size(group)
     if out is None:
         out = torch.empty(world * H.ST_LEN, dtype=stats.dtype, device=stats.device)
     src = stats.contiguous()
-    try:
-        dist.all_gather_into_tensor(out, src, group=group)
-    except (RuntimeError, NotImplementedError, ValueError):
+    if dist.get_backend(group) == "gloo":   # CPU rehearsals: the list form everywhere
         dist.all_gather(list(out.view(world, H.ST_LEN).unbind(0)), src, group=group)
+    else:
+        dist.all_gather_into_tensor(out, src, group=group)
     return out
 
 

@@ -63,14 +63,18 @@ def _flush(q: _Queue):
     items, q.items, q.bytes = q.items, [], 0
     if not items:
         return
-    for x, _, _, ver in items:
-        if x._version != ver:
-            raise RuntimeError("a tensor queued for a deferred observer was modified in place before "
-                               "the observer ran; set VSIQ_OBSERVE_BATCH=0 to observe each call at once")
+    changed = [it for it in items if it[0]._version != it[3]]
+    ok = [it for it in items if it[0]._version == it[3]]
     with torch.cuda.stream(q.stream):
-        for act in dict.fromkeys(a for _, a, _, _ in items):
-            sel = [(x, s) for x, a, s, _ in items if a == act]
+        for act in dict.fromkeys(a for _, a, _, _ in ok):
+            sel = [(x, s) for x, a, s, _ in ok if a == act]
             observe_parts_multi([x for x, _ in sel], [s for _, s in sel], act=act)
+        for _, _, slot, _ in changed:   # record count 0: a later fold reads nothing from it
+            slot.zero_()
+    if changed:
+        raise RuntimeError(f"{len(changed)} tensor(s) queued for a deferred observer were modified in place "
+                           "before the observer ran (their calls recorded nothing); set "
+                           "VSIQ_OBSERVE_BATCH=0 to observe each call at once")
 
 
 def flush(device=None):
