@@ -100,6 +100,9 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
                                           per launch site (kernel, grid, bytes, device) from
                                           event-timed launches; 0: fixed 1.05 x the read time
                                           at 7.5 TB/s */
+#define VSIQ_TUNE_XCD_ORDER 13         /* 1 (default): XCD-contiguous workgroup order where
+                                          neighbouring workgroups share cache lines (K6 on
+                                          channel columns); 0: hardware order */
 int vsiq_set_tuning(int key, int value);
 
 /*

@@ -125,7 +125,8 @@ def test_tuning_keys_match_header_and_bounds():
                             "vsiq.h")).read()
     keys = dict(re.findall(r"#define VSIQ_(TUNE_\w+) (\d+)", hdr))
     for name in ("TUNE_PC_ROWS_PER_BLOCK", "TUNE_NONTEMPORAL", "TUNE_PC_BLOCK", "TUNE_STORE_DEFER", "TUNE_OBS_KERNEL",
-                 "TUNE_OBS_GRID", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED", "TUNE_STORE_GATE"):
+                 "TUNE_OBS_GRID", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED", "TUNE_STORE_GATE", "TUNE_GATE_AUTOTUNE",
+                 "TUNE_XCD_ORDER"):
         assert int(keys[name]) == getattr(H, name), name
     assert int(re.search(r"#define VSIQ_COUNTER_WORDS (\d+)", hdr).group(1)) == H.COUNTER_WORDS
     assert int(re.search(r"#define VSIQ_ABI_VERSION (\d+)", hdr).group(1)) == H.ABI_VERSION
@@ -139,6 +140,9 @@ def test_tuning_keys_match_header_and_bounds():
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 2) == 0
     assert lib.vsiq_set_tuning(H.TUNE_GATE_AUTOTUNE, 2) != 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 1) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 2) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 0) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 1) == 0
     assert lib.vsiq_set_tuning(99, 0) != 0
 
 

@@ -30,14 +30,29 @@ def t(fn, reps):
 
 for shape, axis in (((256, 16, 160, 160), 1), ((256, 64, 40, 40), 1), ((256, 256, 10, 10), 1),
                     ((256, 128, 20, 20), 1), ((1024, 1024, 3, 3), 0)):
-    x = torch.randn(shape, device=dev)
-    g = torch.randn(shape, device=dev)
+    if os.environ.get("SHAPE") and os.environ["SHAPE"] != "x".join(map(str, shape)):   # e.g. SHAPE=256x256x10x10
+        continue
+    nsets = max(1, -(-(768 << 20) // (12 * torch.Size(shape).numel())))   # rotate past the 256 MB MALL
+    xs = [torch.randn(shape, device=dev) for _ in range(nsets)]
+    gs = [torch.randn(shape, device=dev) for _ in range(nsets)]
+    x = xs[0]
     C = shape[axis]
     s = torch.rand(C, dtype=torch.float64, device=dev) * 0.05 + 0.01
     z = torch.zeros(C, dtype=torch.float64, device=dev)
     n = x.numel()
     reps = max(10, min(200, (4 << 30) // (12 * n)))
-    fwd = t(lambda: FQ.per_channel_fake_quant(x, s, z, -128, 127, axis=axis), reps)
-    bwd = t(lambda: FQ.pc_lsq_backward(g, x, s, z, -128, 127, 1e-4, True, axis), reps)
-    print(f"{str(shape):22s} axis {axis}  fwd {fwd:8.2f} us ({8 * n / fwd / 1e3:5.0f} GB/s)   "
-          f"bwd(K6) {bwd:8.2f} us ({12 * n / bwd / 1e3:5.0f} GB/s)", flush=True)
+    it = [0]
+
+    def nxt():
+        it[0] += 1
+        return it[0] % nsets
+    for rnd in range(int(os.environ.get("ROUNDS", "1"))):
+        for alt in (os.environ.get("ALT", "").split(";") if os.environ.get("ALT") else [""]):
+            for kv in alt.split():   # ALT="13=1;13=0": alternate knob settings, same process
+                k, v = kv.split("=")
+                H.set_tuning(int(k), int(v))
+            fwd = t(lambda: FQ.per_channel_fake_quant(xs[nxt()], s, z, -128, 127, axis=axis), reps)
+            bwd = t(lambda: (lambda i: FQ.pc_lsq_backward(gs[i], xs[i], s, z, -128, 127, 1e-4, True, axis))(nxt()),
+                    reps)
+            print(f"{str(shape):22s} axis {axis} {alt:8s} fwd {fwd:8.2f} us ({8 * n / fwd / 1e3:5.0f} GB/s)   "
+                  f"bwd(K6) {bwd:8.2f} us ({12 * n / bwd / 1e3:5.0f} GB/s)", flush=True)

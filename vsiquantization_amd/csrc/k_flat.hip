@@ -763,6 +763,10 @@ int vsiq_set_tuning(int key, int value) {
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.gate_autotune = value;
       return 0;
+    case VSIQ_TUNE_XCD_ORDER:
+      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      g_tune.xcd_order = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;

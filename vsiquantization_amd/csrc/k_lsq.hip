@@ -425,9 +425,10 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
                                                         int64_t rowlen, uint32_t nb_img, int64_t channels,
                                                         const double *__restrict__ scale,
                                                         const double *__restrict__ zp, float lo, float hi,
-                                                        double *__restrict__ ws) {
-  const int64_t c = blockIdx.x % channels;
-  const int64_t n0 = (int64_t)(blockIdx.x / channels) * nb_img;
+                                                        double *__restrict__ ws, uint32_t xo) {
+  const uint32_t b = xo ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;   // logical block i*C + c
+  const int64_t c = b % channels;
+  const int64_t n0 = (int64_t)(b / channels) * nb_img;
   const uint32_t nr = (uint32_t)std::min<int64_t>(nb_img, images - n0);
   const uint32_t gpr = (uint32_t)(rowlen / 4);
   const uint32_t nj = nr * gpr;
@@ -456,9 +457,21 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
     if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
   lsq_block_reduce(acc);
   if (threadIdx.x == 0) {
-    ws[2 * (int64_t)blockIdx.x] = acc.t;
-    ws[2 * (int64_t)blockIdx.x + 1] = acc.z;
+    ws[2 * (int64_t)b] = acc.t;
+    ws[2 * (int64_t)b + 1] = acc.z;
   }
+}
+
+template <bool NT, bool ZPL>
+void launch_pcc_k(const float *g, const float *x, float *gx, int64_t images, int64_t rowlen, int64_t nb,
+                  int64_t channels, int64_t grid, const double *scale, const double *zp, float lo, float hi,
+                  double *ws, hipStream_t st) {
+  // XCD-contiguous order where a row ends mid-line: at 10x10 rows ~half of the lines
+  // are shared with the neighbouring channel's workgroup (PMC fetch 1.30x -> 1.04x the
+  // algorithmic bytes, 24.2 -> 21.7 us at 256x256x10x10); 20x20 and up measured slower
+  const uint32_t xo = g_tune.xcd_order != 0 && (rowlen * 4) % 128 != 0 && rowlen * 4 <= 512;
+  hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, ZPL>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, images, rowlen,
+                     (uint32_t)nb, channels, scale, zp, lo, hi, ws, xo);
 }
 
 template <bool NT>
@@ -467,13 +480,10 @@ int64_t launch_pcc_lsq(const float *g, const float *x, float *gx, int64_t rows, 
                        float hi, double *ws, hipStream_t st) {
   const int64_t images = rows / channels, nb = pcc_images(rowlen);
   const int64_t iblocks = cdiv(images, nb);
-  const dim3 grid((unsigned)(iblocks * channels)), block(kBlock);
   if (zp_learn)
-    hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, true>), grid, block, 0, st, g, x, gx, images, rowlen, (uint32_t)nb,
-                       channels, scale, zp, lo, hi, ws);
+    launch_pcc_k<NT, true>(g, x, gx, images, rowlen, nb, channels, iblocks * channels, scale, zp, lo, hi, ws, st);
   else
-    hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, false>), grid, block, 0, st, g, x, gx, images, rowlen, (uint32_t)nb,
-                       channels, scale, zp, lo, hi, ws);
+    launch_pcc_k<NT, false>(g, x, gx, images, rowlen, nb, channels, iblocks * channels, scale, zp, lo, hi, ws, st);
   return iblocks * channels;   // record rows for k_pcm_lsq_fold (one chunk each)
 }
 

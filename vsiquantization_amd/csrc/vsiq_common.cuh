@@ -70,10 +70,23 @@ struct Tuning {
   std::atomic<int> lsq_groups{0};          // K4 groups per lane 2 / 4 / 8 / 16 (0 = by size)
   std::atomic<int> store_gate{-1};         // store gate ticks (10 ns) for one-round grids (-1 = auto, 0 = off)
   std::atomic<int> gate_autotune{1};       // store gate tuned online per launch site (0 = fixed estimate)
+  std::atomic<int> xcd_order{1};           // XCD-contiguous block order where neighbours share lines
 };
 extern Tuning g_tune;
 
 __host__ __device__ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// XCD-contiguous block order.  The dispatcher deals workgroups to the 8 XCDs round
+// robin (block b -> XCD b % 8), each XCD with its own L2.  Where neighbouring blocks
+// share cache lines (per-channel columns of short rows: a 400-byte row ends mid-line),
+// that sends every shared line to two L2s and HBM twice.  xcd_block(b) is the logical
+// block physical block b works on: XCD x walks one contiguous range of logical blocks,
+// its concurrent blocks neighbours (a bijection on [0, grid)).
+constexpr uint32_t kXcds = 8;
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t grid) {
+  const uint32_t x = b % kXcds, k = b / kXcds, per = grid / kXcds, rem = grid % kXcds;
+  return x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+}
 
 // Grid-stride trip count of a workgroup whose first item is `first` (uniform: it
 // depends on blockIdx only, so loops on it are scalar branches and hipcc's
