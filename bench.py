@@ -819,11 +819,13 @@ def load_pmc_traffic(workload, kernel):
         return None
 
 
-def settle_gates(W, cap=4000):
+def settle_gates(W, cap=4000, world=1):
     """Untimed steps until the store-gate tuner (csrc/gate_tune.hip) has chosen the gate
     of every one-round launch site this workload uses: each site's first ~100 launches
     time candidate gates.  A choice of delay only -- results are identical for every gate.
-    Returns (steps run, one dict per tuned site)."""
+    With several ranks the stop is agreed (MAX of the ranks' pending counts), so every
+    rank runs the same steps -- a workload whose step holds a collective would otherwise
+    hang.  Returns (steps run, one dict per tuned site)."""
     from vsiquantization_amd import _hip as H
     n = 0
     while n < cap:   # at least one round, so that every launch site exists
@@ -831,7 +833,13 @@ def settle_gates(W, cap=4000):
             assert W.launch(n) == 0
             n += 1
         torch.cuda.synchronize()
-        if H.gate_tuning_pending() == 0:
+        pending = H.gate_tuning_pending()
+        if world > 1:
+            on_gpu = dist.get_backend() == "nccl"
+            p = torch.tensor([pending], dtype=torch.int64, device=torch.cuda.current_device() if on_gpu else "cpu")
+            dist.all_reduce(p, op=dist.ReduceOp.MAX)
+            pending = int(p)
+        if pending == 0:
             break
     sites = []
     for line in H.gate_report().splitlines():
@@ -849,7 +857,7 @@ def measure(W, steps, warmup, world):
     HIP-event durations (rank-local) -> roofline of the dominant phase."""
     for i in range(warmup):
         assert W.launch(i) == 0
-    settle, gate_sites = settle_gates(W)
+    settle, gate_sites = settle_gates(W, world=world)
     names = list(W.kernels)
     ns = W.group
     groups = [(g0, min(ns, steps - g0)) for g0 in range(0, steps, ns)]

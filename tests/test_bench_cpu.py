@@ -56,3 +56,39 @@ def test_cpu_baseline_c1_reports_threads():
     r = bench.cpu_baseline("c1", 0.2)
     assert r["kind"] == "port" and r["value"] > 0 and r["unit"] == "Melem/s"
     assert str(os.cpu_count()) in r["thread_probe_c1"] and str(r["cores"]) in r["threads_whole"]
+
+
+def _settle_worker(rank, world, port, ret):
+    """settle_gates with a step that holds a collective and a tuner that reports nothing
+    pending from its 2nd query on rank 0 but only from its 4th on rank 1: the agreed
+    stop keeps the ranks in step."""
+    import torch
+    import torch.distributed as dist
+    from vsiquantization_amd import _hip as H
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rounds = {"n": 0}
+
+    def pending():
+        rounds["n"] += 1
+        return 0 if rounds["n"] > (1 if rank == 0 else 3) else 5
+
+    class W:
+        def launch(self, i):
+            t = torch.ones(1)
+            dist.all_reduce(t)              # the step's collective
+            return 0 if float(t) == world else 1
+    H.gate_tuning_pending = pending
+    torch.cuda.synchronize = lambda *a: None
+    try:
+        ret[rank] = bench.settle_gates(W(), world=world)[0]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_settle_gates_agrees_across_ranks():
+    import torch.multiprocessing as mp
+    port = 29700 + os.getpid() % 200
+    ret = mp.Manager().dict()
+    mp.spawn(_settle_worker, args=(2, port, ret), nprocs=2, join=True)
+    assert ret[0] == ret[1] == 32          # 4 rounds of 8 steps on both ranks

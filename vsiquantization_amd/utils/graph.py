@@ -27,7 +27,10 @@ class GraphedStep:
     """Capture ``fn`` (no arguments; reads and writes persistent tensors) into a HIP graph.
 
     ``fn`` runs ``warmup`` times on a side stream, then until the store-gate tuner has no
-    site left to tune (at most ``settle_max`` more runs), then once under capture.  Calling
+    site left to tune (at most ``settle_max`` more runs), then once under capture.  Under
+    torch.distributed (``group``, default the world when initialised) the ranks agree on
+    that stop -- MAX of their pending counts each run -- so a step holding a collective
+    (DDP's all-reduce) runs equally often on every rank.  Calling
     the object replays the graph on the current stream and returns what the captured run
     returned (its tensors are overwritten by every replay).  ``grads_of``: tensors whose
     ``.grad`` is set to None before each warm-up run and before the capture, so that the
@@ -35,9 +38,10 @@ class GraphedStep:
     buffer) and every replay leaves exactly one step's gradient there.
     """
 
-    def __init__(self, fn, warmup: int = 3, settle_max: int = 400, grads_of=()):
+    def __init__(self, fn, warmup: int = 3, settle_max: int = 400, grads_of=(), group=None):
         self.fn = fn
         self.params = list(grads_of)
+        self.group = group
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -50,13 +54,26 @@ class GraphedStep:
                 self._clear()
                 fn()
                 torch.cuda.current_stream().synchronize()
-                if H.gate_tuning_pending() == 0:
+                if self._pending() == 0:
                     break
         torch.cuda.current_stream().wait_stream(side)
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = fn()
+
+    def _pending(self) -> int:
+        n = H.gate_tuning_pending()
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return n
+        g = self.group if self.group is not None else dist.group.WORLD
+        if dist.get_world_size(g) == 1:
+            return n
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(g) == "nccl" else "cpu"
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+        return int(t)
 
     def _clear(self):
         for p in self.params:
