@@ -152,11 +152,21 @@ __device__ __forceinline__ void observe_stride_b(const float *__restrict__ x, in
   const int64_t step = nblk * kBlock * U;
   for (int64_t b = blk * kBlock * U; b < ng; b += step) {
     f4 v[U];
+    if (VEC && b + (int64_t)kBlock * U <= nfull) {
+      // every group of this step is whole (block-uniform): one uniform base pointer and
+      // 32-bit lane offsets (no per-group 64-bit clamp / address arithmetic: -16 VGPRs,
+      // -40 instructions per step at U = 8), straight-line, no per-group exec-mask
+      // branches (they were ~1/3 of the K2p instruction stream)
+      const float *xb = x + 4 * b;
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = ld4<NT>(xb + 4 * (threadIdx.x + k * kBlock));
+#pragma unroll
+      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
     if (b + (int64_t)kBlock * U <= nfull) {
-      // every group of this step is whole (block-uniform): straight-line, no per-group
-      // exec-mask branches (they were ~1/3 of the K2p instruction stream)
 #pragma unroll
       for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
     } else {
@@ -387,7 +397,10 @@ struct PBatch {
   int count;
 };
 
-template <bool NT, int ACT>
+// ALLVEC: every tensor of the batch takes the 16-byte path (the usual case: activation
+// tensors of n % 4 == 0), so the scalar-path variants, which set the register budget
+// of the generic kernel (152 VGPRs: 3 waves per SIMD), are not compiled in.
+template <bool NT, int ACT, bool ALLVEC>
 __global__ __launch_bounds__(kBlock) void k_observe_part_multi(const PBatch b) {
   int t = 0;
   const uint32_t blk = blockIdx.x;
@@ -395,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_multi(const PBatch b) {
   const PTensor &T = b.t[t];
   const int64_t lb = (int64_t)blk - b.blk0[t], nb = T.grid;
   ObsAcc a;
-  if (T.vec) {
+  if (ALLVEC || T.vec) {
     if (T.u == 8) observe_stride_b<true, NT, ACT, 8>(T.x, T.n, a, lb, nb);
     else if (T.u == 4) observe_stride_b<true, NT, ACT, 4>(T.x, T.n, a, lb, nb);
     else observe_stride_b<true, NT, ACT, 2>(T.x, T.n, a, lb, nb);
@@ -851,9 +864,13 @@ int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, 
     }
     b.blk0[b.count] = blk;
     const hipStream_t st = (hipStream_t)stream;
-#define K2M(A)                                                                                          \
-  if (nt) hipLaunchKernelGGL((k_observe_part_multi<true, A>), dim3(blk), dim3(kBlock), 0, st, b);    \
-  else hipLaunchKernelGGL((k_observe_part_multi<false, A>), dim3(blk), dim3(kBlock), 0, st, b);
+    bool allvec = true;
+    for (int k = 0; k < b.count; ++k) allvec = allvec && b.t[k].vec;
+#define K2M(A)                                                                                                 \
+  if (nt && allvec) hipLaunchKernelGGL((k_observe_part_multi<true, A, true>), dim3(blk), dim3(kBlock), 0, st, b); \
+  else if (nt) hipLaunchKernelGGL((k_observe_part_multi<true, A, false>), dim3(blk), dim3(kBlock), 0, st, b);    \
+  else if (allvec) hipLaunchKernelGGL((k_observe_part_multi<false, A, true>), dim3(blk), dim3(kBlock), 0, st, b); \
+  else hipLaunchKernelGGL((k_observe_part_multi<false, A, false>), dim3(blk), dim3(kBlock), 0, st, b);
     if (act == kActRelu) { K2M(kActRelu) }
     else if (act == kActSilu) { K2M(kActSilu) }
     else { K2M(kActNone) }
