@@ -162,6 +162,35 @@ class C2PerChannel:
         ev[2].record()
         return rc
 
+    def codes_variant(self, groups=25):
+        """SURVEY §8d's second C2 figure: the forward with the uint8 codes emitted as well
+        (9 B/elem + the mask bits), timed like the headline (groups of one launch per slot
+        between HIP events, after the store-gate tuner has settled this launch site)."""
+        H, C = self.H, self.shape[0]
+        dev = self.slots[0]["x"].device
+        codes = [torch.empty(self.shape, dtype=torch.uint8, device=dev) for _ in self.slots]
+        args = [(s["fwd"][0], s["fwd"][1], H.ptr(c), *s["fwd"][3:]) for s, c in zip(self.slots, codes)]
+        for k in range(4000):
+            assert self.f_fwd(*args[k % len(args)]) == 0
+            if k % 8 == 7:
+                torch.cuda.synchronize()
+                if H.gate_tuning_pending() == 0:
+                    break
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
+        for e0, e1 in evs:
+            e0.record()
+            for a in args:
+                assert self.f_fwd(*a) == 0
+            e1.record()
+        torch.cuda.synchronize()
+        us = sum(e0.elapsed_time(e1) for e0, e1 in evs) / (groups * len(args)) * 1e3
+        alg = self.kernels["pc_observe_fq_fwd"] + self.n
+        ok = bool(torch.equal(codes[0].reshape(C, -1)[:, :4096].float(),
+                              (self.slots[0]["y"].reshape(C, -1)[:, :4096].double()
+                               / self.slots[0]["scale"][:, None] + self.slots[0]["zp"][:, None]).round().float()))
+        return {"avg_us": us, "alg_bytes": alg, "GBps": alg / us / 1e3, "frac": alg / us / 1e3 / 8000.0,
+                "codes_match_y": ok}
+
     def check(self):
         """Slot 0, 64 rows spread over the tensor, against the reference's formulas restated
         in torch on the host (minmax.py:49-74 in float64, uniform.py:55,95 with IEEE fp32
@@ -1091,6 +1120,9 @@ def main(argv=None):
     }
     if a.tune:
         out["config"]["tuning"] = a.tune
+    if a.workload == "c2":
+        progress("c2: forward with uint8 codes")
+        out["kernels"]["pc_observe_fq_fwd_with_codes"] = W.codes_variant()
     del W
     torch.cuda.empty_cache()
     if a.workload == "c2" and not a.no_api:
