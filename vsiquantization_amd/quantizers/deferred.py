@@ -34,8 +34,12 @@ from .per_channel import PerChannelUniformQuantizer
 from .quantization_manager import QuantizationManager
 from .uniform import UniformQuantizer
 
-# grad_out storage pointer -> pending fold of one records-only backward
+# grad_out storage pointer -> pending fold of one records-only backward.  A backward
+# that never reaches the bundle (torch.autograd.grad for the activations only) leaves
+# its entries behind; the oldest are dropped beyond _PENDING_MAX (a real step holds one
+# per quantizer of the model).
 _PENDING = {}
+_PENDING_MAX = 1 << 14
 
 
 class _Fold:
@@ -95,6 +99,8 @@ class DeferredLearnFn(torch.autograd.Function):
         e.out = torch.empty(2, dtype=torch.float64, device=dev)
         e.keep = (s, z)
         _PENDING[e.out.data_ptr()] = e
+        while len(_PENDING) > _PENDING_MAX:
+            _PENDING.pop(next(iter(_PENDING)))
         gs = e.out[0].view(s.shape) if ctx.needs_input_grad[1] else None
         gz = e.out[1].view(z.shape) if (learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]) else None
         return gx, gs, gz, None, None, None, None, None
