@@ -41,6 +41,13 @@ FLAGS = [
 ]
 
 
+# per-source extra flags.  k_flat.hip (K2 / K2p / K2m observers): without SLP
+# vectorization the observer's |x| sums stay scalar adds with free abs modifiers instead
+# of v_pk_add_f32 fed by v_and / v_mov pairs -- C5's K2m 175 -> 168 us on MI355X (C2 / C3
+# / C4 kernels measured unchanged with it, so they keep the default)
+FILE_FLAGS = {"k_flat.hip": ["-fno-slp-vectorize"]}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):
@@ -77,7 +84,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
         if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
                 and os.path.getmtime(obj) > newest_dep):
             return obj
-        cmd = [cc, *FLAGS, *inc, "-c", "-o", obj + ".tmp", src]
+        cmd = [cc, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *inc, "-c", "-o", obj + ".tmp", src]
         if verbose:
             print("[vsiq build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
