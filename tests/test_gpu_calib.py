@@ -131,6 +131,23 @@ def test_observe_parts_multi_records_bitwise_equal_per_call(act):
         assert torch.equal(a.view(torch.int64), b.view(torch.int64)), i
 
 
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_observe_parts_multi_all_vector_batch_bitwise(act):
+    """A batch whose tensors all take the 16-byte path launches K2m's all-vector variant
+    (84 VGPRs, no scalar-path code): records still the same bits as per-call K2p, over
+    every groups-per-lane class and the whole / partial last step of each tensor."""
+    from vsiquantization_amd import fakequant as FQ
+    g = torch.Generator(device=DEV).manual_seed(5)
+    sizes = [4, 4096, 1000004, 3 * 2**20 + 4, 13107200, 52428800, 65536, 2**20, 6553600, 409600]
+    xs = [torch.randn(n, device=DEV, generator=g) * 3 for n in sizes]
+    xs[2][17] = float("nan")
+    per = [FQ.observe_parts(x, act=act) for x in xs]
+    multi = FQ.observe_parts_multi(xs, None, act=act)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(per, multi)):
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), i
+
+
 def test_queued_deferred_calibration_equals_unqueued(monkeypatch):
     """QuantizationManager's deferred calls queued and observed by K2m (default) give
     the same running min/max, qparams and stats lists, bit for bit, as one K2p launch per
