@@ -432,6 +432,18 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
                          int64_t channels, const double *scale, const double *zp, int zp_learn,
                          int qmin, int qmax, double gscale, double *grad_scale_out,
                          double *grad_zp_out, double *ws, int64_t ws_len, void *stream);
+/*
+ * The same with per-channel arrival counters (uint32 [>= channels], zero before first
+ * use; every call leaves them zero; one set per stream): on the axis-1 channel-column
+ * path the last workgroup of each channel folds its records in the launch -- no second
+ * launch, the same bits as vsiq_pcm_lsq_bwd_f32.  counters NULL: exactly
+ * vsiq_pcm_lsq_bwd_f32.  Other paths ignore the counters.
+ */
+int vsiq_pcm_lsq_bwd_arrive_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                                int64_t channels, const double *scale, const double *zp, int zp_learn,
+                                int qmin, int qmax, double gscale, double *grad_scale_out,
+                                double *grad_zp_out, double *ws, int64_t ws_len, uint32_t *counters,
+                                int64_t counters_len, void *stream);
 
 /*
  * BatchNorm folding (modules/fused.py:100-108, :294-300), fp32, reference order:

@@ -118,6 +118,9 @@ def test_round2_entry_points_validate_on_host():
     assert lib.vsiq_observe_finalize_ranks(null, 2, null, null, null, 1, 127.0, 1e-8, null) == -1
     assert lib.vsiq_observe_finalize_ranks(16, 0, null, null, null, 1, 127.0, 1e-8, null) == -1
     assert lib.vsiq_gate_report(None, 0) >= 0
+    # K6 with per-channel arrival counters: too few counters for the channels
+    assert lib.vsiq_pcm_lsq_bwd_arrive_f32(16, 16, 16, 8, 4, 4, 16, null, 0, -8, 7, 1.0, 16, null, 16, 64, 16, 3,
+                                           null) == -3
 
 
 def test_tuning_keys_match_header_and_bounds():

@@ -119,6 +119,38 @@ def test_packed_rows_equal_per_row_grid(shape):
         np.testing.assert_allclose(out[mode][3], out[0][3], rtol=1e-12, atol=1e-15)
 
 
+@pytest.mark.parametrize("shape,zpl", [((256, 16, 10, 10), True), ((100, 8, 10, 10), False), ((90, 4, 20, 20), True),
+                                       ((7, 3, 40, 48), True), ((256, 37, 10, 10), False), ((3, 300, 8, 8), True)])
+def test_pcc_in_launch_fold_equals_two_launch_fold(shape, zpl):
+    """K6 on channel columns with the channel's last workgroup folding in the launch
+    (vsiq_pcm_lsq_bwd_arrive_f32, what pc_lsq_backward calls) vs the separate fold
+    launch (vsiq_pcm_lsq_bwd_f32): every output bit for bit, twice in a row (the
+    counters are left zero), and the counters zero afterwards."""
+    from vsiquantization_amd import _hip as H
+    rng = np.random.default_rng(sum(shape))
+    x = cu((rng.standard_normal(shape) * 2).astype(np.float32))
+    g = cu(rng.standard_normal(shape).astype(np.float32))
+    C = shape[1]
+    s = torch.tensor(rng.uniform(0.01, 0.1, C), dtype=torch.float64, device=DEV)
+    z = torch.tensor(np.rint(rng.uniform(0, 255, C)) + 0.2, dtype=torch.float64, device=DEV)
+    rows, rowlen = x.numel() // (shape[2] * shape[3]), shape[2] * shape[3]
+    a1 = [npy(t) for t in FQ.pc_lsq_backward(g, x, s, z, 0, 255, 1e-3, zpl, 1)]
+    a2 = [npy(t) for t in FQ.pc_lsq_backward(g, x, s, z, 0, 255, 1e-3, zpl, 1)]
+    gx = torch.empty_like(g)
+    gs = torch.empty(C, dtype=torch.float64, device=DEV)
+    gz = torch.empty(C, dtype=torch.float64, device=DEV)
+    ws = torch.empty(int(H.lib().vsiq_pcm_workspace_doubles(rows, rowlen)), dtype=torch.float64, device=DEV)
+    rc = H.lib().vsiq_pcm_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), H.c_i64(rows), H.c_i64(rowlen), H.c_i64(C),
+                                      H.ptr(s), H.ptr(z), int(zpl), 0, 255, 1e-3, H.ptr(gs), H.ptr(gz), H.ptr(ws),
+                                      H.c_i64(ws.numel()), H.stream_of(torch.device(DEV)))
+    assert rc == 0
+    b = [npy(t) for t in (gx, gs, gz)]
+    for k in range(3):
+        np.testing.assert_array_equal(a1[k], b[k])
+        np.testing.assert_array_equal(a2[k], b[k])
+    assert int(H.workspace(torch.device(DEV)).channel_counters(C).abs().sum()) == 0
+
+
 def test_learnable_per_channel_quantizer_weights():
     """PerChannelUniformQuantizer learnable on an OIHW weight (axis 0, scale [C] f64)."""
     rng = np.random.default_rng(3)

@@ -80,6 +80,8 @@ _SIGS = {
     "vsiq_pcm_workspace_doubles": ([c_i64, c_i64], c_i64),
     "vsiq_pcm_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p,
                               c_p, c_p, c_i64, c_p], c_int),
+    "vsiq_pcm_lsq_bwd_arrive_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p,
+                                     c_p, c_p, c_i64, c_p, c_i64, c_p], c_int),
     "vsiq_bn_fold_f32": ([c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_float, c_p, c_p, c_i64, c_i64, c_p], c_int),
     "vsiq_act_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_d, c_p, c_d, c_int, c_int,
                              c_int, c_int, c_p], c_int),
@@ -264,6 +266,13 @@ class _Workspace:
             self.ws = torch.empty(need, dtype=torch.float64, device=self.device)
             self.ws_len = need
         return self
+
+    def channel_counters(self, channels: int) -> torch.Tensor:
+        """Per-channel arrival counters (zeroed once; every launch leaves them zero)."""
+        c = getattr(self, "_chan", None)
+        if c is None or c.numel() < channels:
+            c = self._chan = torch.zeros(max(channels, 256), dtype=torch.int32, device=self.device)
+        return c
 
 
 _WS = {}

@@ -418,14 +418,24 @@ inline int64_t pcc_images(int64_t rowlen) {
   return std::max<int64_t>(1, (int64_t)kBlock * kColGroups * 4 / rowlen);
 }
 
-template <bool NT, bool ZPL>
+// ARRIVE (vsiq_pcm_lsq_bwd_arrive_f32): instead of a second launch, the channel's last
+// workgroup folds it -- each workgroup stores its record write-through, drains it and
+// bumps counters[c] (agent-scope relaxed add, the arrive_last pattern of K2 / K4); the
+// one whose add returns nib - 1 takes an agent acquire, folds records i*C + c in the
+// fixed order of k_pcm_lsq_fold (same bits), writes grad_scale[c] / grad_zp[c] and
+// resets counters[c].  grad_x is stored after the arrival, so the drain waits only for
+// the record.  No workgroup waits for another.
+template <bool NT, bool ZPL, bool ARRIVE>
 __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict__ g,
                                                         const float *__restrict__ x,
                                                         float *__restrict__ gx, int64_t images,
                                                         int64_t rowlen, uint32_t nb_img, int64_t channels,
                                                         const double *__restrict__ scale,
                                                         const double *__restrict__ zp, float lo, float hi,
-                                                        double *__restrict__ ws, uint32_t xo) {
+                                                        double *__restrict__ ws, uint32_t xo,
+                                                        uint32_t *__restrict__ counters, uint32_t nib,
+                                                        double gscale, double *__restrict__ gs_out,
+                                                        double *__restrict__ gz_out) {
   const uint32_t b = xo ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;   // logical block i*C + c
   const int64_t c = b % channels;
   const int64_t n0 = (int64_t)(b / channels) * nb_img;
@@ -452,38 +462,88 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
     const uint32_t j = threadIdx.x + k * kBlock;
     o[k] = lsq_group_out<ZPL, kActNone>(j < nj ? 0 : 1, 1, 4, xv[k], gv[k], p, acc);   // i=1: no terms
   }
+  if (!ARRIVE) {
+#pragma unroll
+    for (int k = 0; k < kColGroups; ++k)
+      if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
+    lsq_block_reduce(acc);
+    if (threadIdx.x == 0) {
+      ws[2 * (int64_t)b] = acc.t;
+      ws[2 * (int64_t)b + 1] = acc.z;
+    }
+    return;
+  }
+  lsq_block_reduce(acc);
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    partial_store(ws + 2 * (int64_t)b, acc.t);
+    partial_store(ws + 2 * (int64_t)b + 1, acc.z);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(counters + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == nib - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < kColGroups; ++k)
     if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
-  lsq_block_reduce(acc);
+  if (!s_last) return;
+  LsqAcc f{0.0, 0.0};   // k_pcm_lsq_fold's order: thread j sums records j, j + 256, ... then the tree
+  for (uint32_t i = threadIdx.x; i < nib; i += kBlock) {
+    const int64_t rec = (int64_t)i * channels + c;
+    f.t += partial_load(ws + 2 * rec);
+    f.z += partial_load(ws + 2 * rec + 1);
+  }
+  lsq_block_reduce(f);
   if (threadIdx.x == 0) {
-    ws[2 * (int64_t)b] = acc.t;
-    ws[2 * (int64_t)b + 1] = acc.z;
+    gs_out[c] = f.t * gscale;
+    if (gz_out) {
+      double gz = 0.0;
+      if (ZPL) {   // ClampBackward of the rounded zero point (lsq_module.py:339-343)
+        const double zr = __builtin_rint(zp ? zp[c] : 0.0);
+        gz = (zr >= (double)lo && zr <= (double)hi) ? f.z * gscale : 0.0;
+      }
+      gz_out[c] = gz;
+    }
+    __hip_atomic_store(counters + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-template <bool NT, bool ZPL>
+template <bool NT, bool ZPL, bool ARRIVE>
 void launch_pcc_k(const float *g, const float *x, float *gx, int64_t images, int64_t rowlen, int64_t nb,
                   int64_t channels, int64_t grid, const double *scale, const double *zp, float lo, float hi,
-                  double *ws, hipStream_t st) {
+                  double *ws, uint32_t *counters, double gscale, double *gs, double *gz, hipStream_t st) {
   // XCD-contiguous order where a row ends mid-line: at 10x10 rows ~half of the lines
   // are shared with the neighbouring channel's workgroup (PMC fetch 1.30x -> 1.04x the
   // algorithmic bytes, 24.2 -> 21.7 us at 256x256x10x10); 20x20 and up measured slower
   const uint32_t xo = g_tune.xcd_order != 0 && (rowlen * 4) % 128 != 0 && rowlen * 4 <= 512;
-  hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, ZPL>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, images, rowlen,
-                     (uint32_t)nb, channels, scale, zp, lo, hi, ws, xo);
+  hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, ZPL, ARRIVE>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, images,
+                     rowlen, (uint32_t)nb, channels, scale, zp, lo, hi, ws, xo, counters,
+                     (uint32_t)cdiv(images, nb), gscale, gs, gz);
 }
 
+// counters != nullptr: the channel's last workgroup folds (no second launch)
 template <bool NT>
 int64_t launch_pcc_lsq(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                        int64_t channels, const double *scale, const double *zp, int zp_learn, float lo,
-                       float hi, double *ws, hipStream_t st) {
+                       float hi, double *ws, uint32_t *counters, double gscale, double *gs, double *gz,
+                       hipStream_t st) {
   const int64_t images = rows / channels, nb = pcc_images(rowlen);
-  const int64_t iblocks = cdiv(images, nb);
-  if (zp_learn)
-    launch_pcc_k<NT, true>(g, x, gx, images, rowlen, nb, channels, iblocks * channels, scale, zp, lo, hi, ws, st);
-  else
-    launch_pcc_k<NT, false>(g, x, gx, images, rowlen, nb, channels, iblocks * channels, scale, zp, lo, hi, ws, st);
+  const int64_t iblocks = cdiv(images, nb), grid = iblocks * channels;
+#define VSIQ_PCC(ZPL, AR) \
+  launch_pcc_k<NT, ZPL, AR>(g, x, gx, images, rowlen, nb, channels, grid, scale, zp, lo, hi, ws, counters, gscale, gs, gz, st)
+  if (counters) {
+    if (zp_learn) VSIQ_PCC(true, true);
+    else VSIQ_PCC(false, true);
+  } else {
+    if (zp_learn) VSIQ_PCC(true, false);
+    else VSIQ_PCC(false, false);
+  }
+#undef VSIQ_PCC
   return iblocks * channels;   // record rows for k_pcm_lsq_fold (one chunk each)
 }
 
@@ -567,9 +627,18 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
                          int64_t channels, const double *scale, const double *zp, int zp_learn,
                          int qmin, int qmax, double gscale, double *grad_scale_out,
                          double *grad_zp_out, double *ws, int64_t ws_len, void *stream) {
+  return vsiq_pcm_lsq_bwd_arrive_f32(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, qmin, qmax, gscale,
+                                     grad_scale_out, grad_zp_out, ws, ws_len, nullptr, 0, stream);
+}
+
+int vsiq_pcm_lsq_bwd_arrive_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                                int64_t channels, const double *scale, const double *zp, int zp_learn, int qmin,
+                                int qmax, double gscale, double *grad_scale_out, double *grad_zp_out, double *ws,
+                                int64_t ws_len, uint32_t *counters, int64_t counters_len, void *stream) {
   if (rows <= 0 || rowlen <= 0 || channels <= 0 || rows % channels || qmin > qmax || !g || !x ||
       !gx || !scale || !grad_scale_out || !ws || (zp_learn && !zp))
     return VSIQ_E_ARG;
+  if (counters && counters_len < channels) return VSIQ_E_WS;
   const int64_t chunks = pcm_chunks(rowlen);
   if (rows * chunks > 0x7fffffffLL || channels > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < 2 * rows * chunks) return VSIQ_E_WS;
@@ -585,10 +654,11 @@ int vsiq_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows
   const int packed = g_tune.pc_packed;
   if (vec && pc_packed(rowlen) && rows > channels && packed == 1) {   // axis 1, short rows: columns
     frows = nt ? launch_pcc_lsq<true>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
-                                      (float)qmax, ws, st)
+                                      (float)qmax, ws, counters, gscale, grad_scale_out, grad_zp_out, st)
                : launch_pcc_lsq<false>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
-                                       (float)qmax, ws, st);
+                                       (float)qmax, ws, counters, gscale, grad_scale_out, grad_zp_out, st);
     fchunks = 1;
+    if (counters) return launch_rc();   // folded in the launch
   } else if (pc_packed(rowlen) && packed != 0) {   // one chunk per row: same record layout
     VSIQ_B2(launch_pcp_lsq, vec, nt, g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
             (float)qmax, ws, st);

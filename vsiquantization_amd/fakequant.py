@@ -593,11 +593,12 @@ def pc_lsq_backward(g, x, scale, zp, qmin, qmax, gscale, learn_zp, axis):
     gz = torch.empty(C, dtype=torch.float64, device=dev)
     ws = torch.empty(max(1, int(H.lib().vsiq_pcm_workspace_doubles(rows, rowlen))), dtype=torch.float64,
                      device=dev)
-    rc = H.lib().vsiq_pcm_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(rows), _i64(rowlen), _i64(C),
-                                      H.ptr(s), H.ptr(z), int(bool(learn_zp)), int(qmin), int(qmax),
-                                      float(gscale), H.ptr(gs), H.ptr(gz), H.ptr(ws), _i64(ws.numel()),
-                                      H.stream_of(dev))
-    H.check(rc, "vsiq_pcm_lsq_bwd_f32")
+    cnt = H.workspace(dev).channel_counters(C)   # per (device, stream / capture): the fold in the launch
+    rc = H.lib().vsiq_pcm_lsq_bwd_arrive_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(rows), _i64(rowlen), _i64(C),
+                                             H.ptr(s), H.ptr(z), int(bool(learn_zp)), int(qmin), int(qmax),
+                                             float(gscale), H.ptr(gs), H.ptr(gz), H.ptr(ws), _i64(ws.numel()),
+                                             H.ptr(cnt), _i64(cnt.numel()), H.stream_of(dev))
+    H.check(rc, "vsiq_pcm_lsq_bwd_arrive_f32")
     return gx, gs, gz
 
 
