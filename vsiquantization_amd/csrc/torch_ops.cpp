@@ -67,8 +67,9 @@ struct PcObserveFq : public torch::autograd::Function<PcObserveFq> {
     const int64_t C = x.dim() > 0 ? x.size(0) : 1;
     const int64_t rowlen = C > 0 ? x.numel() / C : 0;
     Tensor y = at::empty_like(x);
-    Tensor sz = at::empty({2, C}, x.options().dtype(at::kDouble));
-    Tensor scale = sz[0], zp = sz[1];
+    // separate buffers, not rows of one: view outputs cost the engine extra bookkeeping
+    Tensor scale = at::empty({C}, x.options().dtype(at::kDouble));
+    Tensor zp = at::empty({C}, x.options().dtype(at::kDouble));
     Tensor mask = mask_buffer(C, rowlen, x);
     Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble))
                                : at::empty({0}, x.options().dtype(at::kDouble));
@@ -78,17 +79,23 @@ struct PcObserveFq : public torch::autograd::Function<PcObserveFq> {
                                  (int)qmin, (int)qmax, qden, eps, stream_of(x)),
           "vsiq_pc_observe_fq_f32");
     ctx->save_for_backward({mask, scale});
-    ctx->saved_data["rowlen"] = rowlen;
     ctx->mark_non_differentiable({scale, zp, rs});
+    // the engine would otherwise materialize zero gradients for the three
+    // non-differentiable outputs (two allocations + fill launches per backward)
+    ctx->set_materialize_grads(false);
     return {y, scale, zp, rs};
   }
 
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
+    if (!grads[0].defined())
+      return {Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
     const auto saved = ctx->get_saved_variables();
     const Tensor g = grads[0].contiguous();
     Tensor gx = at::empty_like(g);
+    const int64_t C = saved[1].numel();   // one scale per row
+    const int64_t rowlen = C > 0 ? g.numel() / C : 0;
     check(vsiq_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(saved[0]), ptr<float>(gx), g.numel(),
-                           ptr<double>(saved[1]), ctx->saved_data["rowlen"].toInt(), 0.0, stream_of(g)),
+                           ptr<double>(saved[1]), rowlen, 0.0, stream_of(g)),
           "vsiq_ste_bwd_f32");
     return {gx, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
