@@ -219,9 +219,12 @@ class C2PerChannel:
 class C1PerTensor(C2PerChannel):
     """C1: the reference's minimal config -- MinMaxObserver + UniformQuantizer, per-tensor
     symmetric int8, on a 256x256 fp32 weight (observers/minmax.py:76-88 then
-    quantizers/uniform.py:34-56): per step one K2 observe (running min/max + f64 qparams
-    on the device) and one K1 fake quant reading those qparams by pointer.  65,536
-    elements: latency-bound (launch + reduction chain), the GB/s are not the point."""
+    quantizers/uniform.py:34-56): per step the per-call observe + fake quant the manager
+    runs at this size, K9 (vsiq_act_observe_fq_parts_f32: K2p records, then one fake-quant
+    launch whose every workgroup folds them into the running min/max + f64 qparams; no
+    arrival chain); `C1_K2K1=1` times round 1's K2 observe + K1 fake quant instead.
+    65,536 elements: latency-bound (two launches), the GB/s are not the
+    point."""
 
     key = "c1"
     name = "C1 per-tensor sym int8 MinMax observe + fake-quant fwd, 256x256"
@@ -247,9 +250,30 @@ class C1PerTensor(C2PerChannel):
                         H.c_i64(w.ws_len), H.ptr(w.counter), st)
             s["bwd"] = (P["x"], P["y"], None, None, H.c_i64(n), P["qp"], None, 0.0, None, 0.0, 0, 0, -128, 127, st)
             self.slots.append(s)
+            s["k9"] = (P["x"], P["y"], None, None, H.c_i64(n), 0, None, P["rmm"], P["qp"], 1, qd, 1e-8, -128, 127,
+                       H.ptr(w.ws), H.c_i64(w.ws_len), st)
         self.f_fwd = lib.vsiq_observe_f32
         self.f_bwd = lib.vsiq_fq_fwd_f32
-        self.kernels = {"observe": 4 * n, "fq_fwd": 8 * n}
+        self.f_k9 = lib.vsiq_act_observe_fq_parts_f32
+        self.k2k1 = os.environ.get("C1_K2K1", "0") == "1"
+        # algorithmic bytes: observe reads x (4 B/elem), fake quant reads x, writes y (8)
+        self.kernels = {"observe": 4 * n, "fq_fwd": 8 * n} if self.k2k1 else {"observe_fq": 12 * n}
+
+    def launch(self, i):
+        if self.k2k1:
+            return super().launch(i)
+        return self.f_k9(*self.slots[i % len(self.slots)]["k9"])
+
+    def launch_group(self, i0, cnt, ev):
+        if self.k2k1:
+            return super().launch_group(i0, cnt, ev)
+        ns = len(self.slots)
+        rc = 0
+        ev[0].record()
+        for j in range(cnt):
+            rc |= self.f_k9(*self.slots[(i0 + j) % ns]["k9"])
+        ev[1].record()
+        return rc
 
     def check(self):
         """Slot 0 against the reference's formulas in torch on the host (IEEE fp32 x / s)."""

@@ -216,6 +216,24 @@ int vsiq_act_observe_fq_f32(const float *c, float *y, void *codes, uint64_t *mas
                             double eps, int qmin, int qmax, void *stream);
 
 /*
+ * The same per-call observe + fake quant for mid-size tensors (K9): n <=
+ * vsiq_observe_fq_parts_max_elems() (262144).  Two launches, no cross-workgroup arrival
+ * chain: per-wave K2p records into ws, then every fake-quant workgroup folds them in a
+ * fixed order, derives the running update + f64 qparams itself and quantizes its share.
+ * Results as vsiq_act_observe_fq_f32: min / max / qparams / running state / y / codes /
+ * mask bit for bit equal to vsiq_act_observe_f32 + vsiq_act_fq_fwd_f32, stats sums to
+ * float64 reordering (the order of vsiq_observe_fold_parts).  ws: >= 1024 doubles
+ * (any vsiq_workspace_doubles(n) buffer), stream-ordered like K2's.  Replaces
+ * quantization_manager.py:73-90 -> minmax.py:32-74 -> uniform.py:34-56 for one tensor
+ * (BASELINE C1: 256x256).
+ */
+int64_t vsiq_observe_fq_parts_max_elems(void);
+int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                                  double *stats_out, float *run_minmax, double *qp_out, int symmetric,
+                                  double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
+                                  void *stream);
+
+/*
  * Deferred-calibration observer (K2p): the K2 pass over act(c) WITHOUT the
  * cross-workgroup fold.  Replaces, like vsiq_act_observe_f32, minmax.py:42-43 +
  * quantization_manager.py:66-68 for an observe-only call (calibrate_qat_model,

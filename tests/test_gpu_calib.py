@@ -176,15 +176,20 @@ def test_queued_observer_detects_in_place_change():
 
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("sym,qmin,qmax", [(True, -128, 127), (False, 0, 255), (True, -8, 7), (False, 0, 3)])
-@pytest.mark.parametrize("n", [1, 7, 255, 256, 4097, 65535, 65536])
-def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act):
+@pytest.mark.parametrize("n", [1, 7, 255, 256, 4097, 65535, 65536, 65537, 262143, 262144])
+@pytest.mark.parametrize("parts", [None, False, True])
+def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act, parts):
     """K8 (vsiq_act_observe_fq_f32: observe + qparams + fake quant of a small tensor in one
     launch) == K2 (vsiq_act_observe_f32) then K1 (vsiq_act_fq_fwd_f32 on its qparams
     record): running state, qparams record, y, codes and the 1-bit mask bit for bit, the
     stats sums to float64 reordering; three calls carry the running state (one with a NaN,
-    which changes nothing, minmax.py:42-47); misaligned input takes the scalar path."""
+    which changes nothing, minmax.py:42-47); misaligned input takes the scalar path.
+    The same for K9 (vsiq_act_observe_fq_parts_f32: K2p records, then every fake-quant
+    workgroup folds them; parts=True, and the default above 16384 elements)."""
     from vsiquantization_amd import _hip as H
     from vsiquantization_amd import fakequant as FQ
+    if parts is False and n > FQ.observe_fq_max_elems():
+        pytest.skip("K8 takes at most observe_fq_max_elems()")
     g = torch.Generator(device=DEV).manual_seed(n + qmax)
     xs = [torch.randn(n, device=DEV, generator=g) * (1 + i) for i in range(3)]
     if n > 1:
@@ -194,7 +199,7 @@ def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act):
     rb = torch.zeros(2, device=DEV)
     for x in xs:
         y, qp, st, mask, codes = FQ.observe_fake_quant(x, symmetric=sym, qmin=qmin, qmax=qmax, run_minmax=ra,
-                                                       act=act, want_mask=True, want_codes=True)
+                                                       act=act, want_mask=True, want_codes=True, parts=parts)
         qp2, st2 = FQ.observe_tensor(x, symmetric=sym, run_minmax=rb, act=act)
         y2, mask2, codes2 = FQ.fake_quant(x, None, None, qmin, qmax, qp=qp2, want_mask=True, want_codes=True,
                                           act=act)
@@ -211,5 +216,8 @@ def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act):
 def test_observe_fq_small_rejects_large():
     from vsiquantization_amd import fakequant as FQ
     n = FQ.observe_fq_max_elems() + 1
+    with pytest.raises(Exception):
+        FQ.observe_fake_quant(torch.randn(n, device=DEV), symmetric=True, qmin=-128, qmax=127, parts=False)
+    n = FQ.observe_fq_parts_max_elems() + 1
     with pytest.raises(Exception):
         FQ.observe_fake_quant(torch.randn(n, device=DEV), symmetric=True, qmin=-128, qmax=127)

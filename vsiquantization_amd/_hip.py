@@ -97,6 +97,9 @@ _SIGS = {
     "vsiq_observe_fq_max_elems": ([], c_i64),
     "vsiq_act_observe_fq_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_int, c_int,
                                  c_p], c_int),
+    "vsiq_observe_fq_parts_max_elems": ([], c_i64),
+    "vsiq_act_observe_fq_parts_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_int,
+                                       c_int, c_p, c_i64, c_p], c_int),
     "vsiq_observe_fold_parts": ([c_p, c_i64, c_i64, c_p, c_p], c_int),
     "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
     "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),

@@ -1,7 +1,7 @@
 // k_flat.hip — K2 per-tensor observer (optionally over a fused ReLU/SiLU), the
 // division / fast-path self-tests, and the library-level C ABI entry points
 // (K1 lives in k_fq.hip, K4 in k_lsq.hip, the STE backward in k_ste.hip).
-#include "vsiq_common.cuh"
+#include "k_body.cuh"   // K1 block body (K9); includes vsiq_common.cuh
 
 namespace vsiq {
 
@@ -362,6 +362,103 @@ void launch_observe_fq_small(const float *x, float *y, uint8_t *c, uint64_t *m, 
   else if (c) { K8(false, true); }
   else { K8(false, false); }
 #undef K8
+}
+
+// ----------------------------------------------------------------------------
+// K9: per-call observe + fake quant of a mid-size tensor (K8's limit .. kFoldFqMax) in
+// two launches and WITHOUT K2's cross-workgroup arrival chain (~3 us of atomics, fence
+// and last-block fold at C1's 65536 elements, profiles/r02p_c1_sweep.txt).  K2p writes
+// one record per wave (plain stores); then every workgroup of the fake-quant launch
+// folds all of them in the same fixed order (the same bits in every workgroup), derives
+// the running update and the f64 qparams itself (minmax.py:42-74) and quantizes its
+// share with K1's block body (uniform.py:55,95).  Workgroup 0 alone writes the running
+// state, the qparams record and the stats record.  The running update is idempotent
+// (min / max; a NaN call changes nothing, minmax.py:42-47), so a workgroup that reads
+// the state after workgroup 0 has written it computes the same qparams.
+// ----------------------------------------------------------------------------
+constexpr int kFoldFqGrid = 32;                 // K2p workgroups: <= 128 records per fold
+constexpr int kFoldFqU = 4;                     // K2p groups per lane per step
+constexpr int64_t kFoldFqMax = (int64_t)1 << 18;   // largest n (fq grid <= 128 workgroups)
+
+template <int ACT, int U>
+void launch_observe_part_u(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
+                           hipStream_t st);   // K2p launch, below
+
+inline int64_t fold_fq_part_grid(int64_t n) {
+  const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
+  return std::min<int64_t>(kFoldFqGrid, std::max<int64_t>(1, cdiv(units, kFoldFqU)));
+}
+
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+__global__ __launch_bounds__(kBlock) void k_fold_fq_fwd(
+    const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
+    uint64_t *__restrict__ mask, int64_t n, const double *__restrict__ parts, int nrec,
+    double *__restrict__ stats_out, float *__restrict__ run_minmax, double *__restrict__ qp_out, int sym,
+    double qden, double eps, float lo, float hi) {
+  __shared__ double s_f[kWaves][6];
+  __shared__ double s_qp[2];
+  double f[6];
+  ObsFold::init(f);
+  for (int i = threadIdx.x; i < nrec; i += kBlock) {   // k_observe_fold_parts' order
+    const double *r = parts + (int64_t)i * VSIQ_PART_LEN;
+    const double rr[6] = {r[0], r[1], r[2], r[3], r[4], r[5]};
+    ObsFold::add(f, rr);
+  }
+  ObsFold::wave(f);
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s_f[w][k] = f[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kWaves; ++i) {
+      const double rr[6] = {s_f[i][0], s_f[i][1], s_f[i][2], s_f[i][3], s_f[i][4], s_f[i][5]};
+      ObsFold::add(f, rr);
+    }
+    float state[2] = {0.f, 0.f};
+    if (run_minmax) { state[0] = run_minmax[0]; state[1] = run_minmax[1]; }
+    const bool lead = blockIdx.x == 0;
+    observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax ? state : nullptr, lead ? qp_out : nullptr,
+                    sym, qden, eps, &s_qp[0], &s_qp[1]);
+    if (lead) {
+      if (run_minmax) { run_minmax[0] = state[0]; run_minmax[1] = state[1]; }
+      if (stats_out) write_stats(stats_out, f, n);
+    }
+  }
+  __syncthreads();
+  QP p;
+  p.s = (float)s_qp[0];
+  p.z = (float)s_qp[1];
+  p.lo = lo;
+  p.hi = hi;
+  p.discrete = 0;
+  p.d = make_fastdiv(p.s);
+  p.fast = fq_fast_qp(p.s, p.z);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, kFlatU>(x, y, codes, mask, n, p, blockIdx.x);
+}
+
+template <int ACT>
+void launch_fold_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
+                        double *parts, double *st, float *run, double *qp, int sym, double qden, double eps,
+                        float lo, float hi, hipStream_t s) {
+  const int64_t pgrid = fold_fq_part_grid(n);
+  launch_observe_part_u<ACT, kFoldFqU>(vec, nt, x, n, parts, pgrid, s);
+  const int nrec = (int)(pgrid * kWaves);
+  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4)));
+#define K9(V, T, C, M)                                                                                       \
+  hipLaunchKernelGGL((k_fold_fq_fwd<V, T, C, M, ACT>), grid, dim3(kBlock), 0, s, x, y, c, m, n, parts, nrec, st, \
+                     run, qp, sym, qden, eps, lo, hi)
+#define K9CM(V, T)                  \
+  if (c && m) { K9(V, T, true, true); }        \
+  else if (c) { K9(V, T, true, false); }       \
+  else if (m) { K9(V, T, false, true); }       \
+  else { K9(V, T, false, false); }
+  if (vec && nt) { K9CM(true, true) }
+  else if (vec) { K9CM(true, false) }
+  else { K9CM(false, false) }
+#undef K9CM
+#undef K9
 }
 
 template <int ACT>
@@ -882,6 +979,22 @@ int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, 
 }
 
 int64_t vsiq_observe_fq_max_elems(void) { return kSmallMax; }
+
+int64_t vsiq_observe_fq_parts_max_elems(void) { return kFoldFqMax; }
+
+int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                                  double *stats_out, float *run_minmax, double *qp_out, int symmetric,
+                                  double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
+                                  void *stream) {
+  if (n <= 0 || n > kFoldFqMax || !c || !y || !ws || qmin > qmax || act < kActNone || act > kActSilu)
+    return VSIQ_E_ARG;
+  if (ws_len < fold_fq_part_grid(n) * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
+  VSIQ_ACT(act, launch_fold_fq_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, ws,
+           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, (hipStream_t)stream);
+  return launch_rc();
+}
 
 int vsiq_act_observe_fq_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
                             double *stats_out, float *run_minmax, double *qp_out, int symmetric, double qden,

@@ -345,16 +345,30 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
     return qp, st
 
 
+# K8 (one workgroup holds the tensor) up to here; K9 above: through the API K8 is
+# 10.9-12.1 us against 17.9-18.2 us for K2 + K1 at 432-16384 elements, but its GPU time
+# grows past K2 + K1's ~9 us above ~16K elements (65536: 16.2 us; tools/exp/k8_bench.py).
+_K8_ELEMS = 16384
+
+
 def observe_fq_max_elems() -> int:
-    """Largest tensor observe_fake_quant takes (K8: one workgroup holds it in registers)."""
+    """Largest tensor observe_fake_quant takes in ONE launch (K8: one workgroup holds it
+    in registers)."""
     return int(H.lib().vsiq_observe_fq_max_elems())
+
+
+def observe_fq_parts_max_elems() -> int:
+    """Largest tensor observe_fake_quant takes on the K2p + fold-in-every-workgroup path (K9)."""
+    return int(H.lib().vsiq_observe_fq_parts_max_elems())
 
 
 def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: float = 1e-8,
                        qmin: int, qmax: int, run_minmax: torch.Tensor | None = None, act=None,
-                       want_mask: bool = False, want_codes: bool = False):
-    """K8: per-tensor observe (running update, f64 qparams, stats) + fake quant of a small
-    tensor in one launch -- observe_tensor + fake_quant(qp=...) fused.
+                       want_mask: bool = False, want_codes: bool = False, parts: bool | None = None):
+    """Per-tensor observe (running update, f64 qparams, stats) + fake quant of one tensor
+    -- observe_tensor + fake_quant(qp=...) fused.  K8 (one launch) up to ``_K8_ELEMS``
+    elements, K9 (K2p records + a fake-quant launch whose every workgroup folds them; no
+    arrival chain) above, up to observe_fq_parts_max_elems(); ``parts`` forces one of them.
     Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None, codes | None)."""
     x = H.require_device_f32(x)
     n = x.numel()
@@ -366,11 +380,22 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
     st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev)
     mask = H.mask_buffer(1, n, dev) if want_mask else None
     codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev) if want_codes else None
-    rc = H.lib().vsiq_act_observe_fq_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n), H.act_code(act),
-                                         H.ptr(st), H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
-                                         qden(symmetric, num_bits, eps), float(eps), int(qmin), int(qmax),
-                                         H.stream_of(dev))
-    H.check(rc, "vsiq_act_observe_fq_f32")
+    if parts is None:
+        parts = n > _K8_ELEMS
+    if parts:
+        w = H.workspace(dev, n)
+        rc = H.lib().vsiq_act_observe_fq_parts_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n),
+                                                   H.act_code(act), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
+                                                   int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps),
+                                                   int(qmin), int(qmax), H.ptr(w.ws), _i64(w.ws_len),
+                                                   H.stream_of(dev))
+        H.check(rc, "vsiq_act_observe_fq_parts_f32")
+    else:
+        rc = H.lib().vsiq_act_observe_fq_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n),
+                                             H.act_code(act), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
+                                             int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps),
+                                             int(qmin), int(qmax), H.stream_of(dev))
+        H.check(rc, "vsiq_act_observe_fq_f32")
     return y, qp, st, mask, codes
 
 

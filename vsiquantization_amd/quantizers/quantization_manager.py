@@ -43,11 +43,10 @@ _ACTS = {"relu": F.relu, "silu": F.silu}
 # model's next layers do not wait for it (its reduction tail overlaps their work).
 # Managers are spread round-robin over a small per-device pool; each manager always
 # uses the same stream, so its own running state stays stream-ordered.
-# K8 (one launch: observe + qparams + fake quant) for per-call observe+quantize up to this
-# many elements.  One workgroup holds the tensor: through this API (host-bound) a call is
-# 10.9-12.1 us against 17.9-18.2 us for K2 + K1 at 432-16384 elements, but its GPU time
-# grows past K2 + K1's ~9 us above ~16K elements (65536: 16.2 us; tools/exp/k8_bench.py).
-_K8_MAX = 16384
+# Per-call observe+quantize in one call (fakequant.observe_fake_quant): K8 (one launch,
+# one workgroup holds the tensor) up to 16384 elements, K9 (K2p records + a fake-quant
+# launch folding them in every workgroup, no arrival chain) up to this many.
+_OBSERVE_FQ_MAX = 1 << 18
 
 _OBS_POOL = 4
 _OBS_STREAMS = {}
@@ -280,17 +279,17 @@ class QuantizationManager(nn.Module):
         return x
 
     def _observe_quantize_small(self, x, act):
-        """Observe + quantize of a small tensor in ONE launch (K8) when this call is the
+        """Observe + quantize of a small tensor in one call (K8 / K9) when this call is the
         reference's per-call observe+quantize (qm.py:73-90) with this package's per-tensor
         MinMaxObserver and UniformQuantizer, single GPU; None when it does not apply."""
-        from ..fakequant import ObserveFakeQuantFn, observe_fake_quant, observe_fq_max_elems
+        from ..fakequant import ObserveFakeQuantFn, observe_fake_quant, observe_fq_parts_max_elems
         from .uniform import UniformQuantizer
         obs = self.observer
         if not (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
                 and type(self.quantizer) is UniformQuantizer and isinstance(obs, MinMaxObserver)
                 and not isinstance(obs, PerChannelMinMaxObserver) and self._device_observer(x)
                 and self.dist_group is None and not self.dist_defer and x.dtype == torch.float32
-                and 0 < x.numel() <= min(_K8_MAX, observe_fq_max_elems())):
+                and 0 < x.numel() <= min(_OBSERVE_FQ_MAX, observe_fq_parts_max_elems())):
             return None
         self._join()
         self._x_device = x.device
