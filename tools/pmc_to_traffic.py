@@ -16,7 +16,10 @@ import sys
 # workload -> [(kernel-name fragment, bench.py kernel label, launches of it per step)];
 # a label's bytes per step = sum over its fragments of (mean per dispatch x launches)
 KERNEL_KEYS = {
-    "c1": [("k_observe_loop<", "observe", 1), ("k_fq_fwd<", "fq_fwd", 1)],
+    # C1: K9 (K2p records + the fake-quant launch folding them) = one "observe_fq" step;
+    # C1_K2K1=1 runs K2 + K1 ("observe", "fq_fwd")
+    "c1": [("k_observe_part<", "observe_fq", 1), ("k_fold_fq_fwd<", "observe_fq", 1),
+           ("k_observe_loop<", "observe", 1), ("k_fq_fwd<", "fq_fwd", 1)],
     "c2": [("k_pc_observe_fq<", "pc_observe_fq_fwd", 1), ("k_ste_bwd<", "ste_bwd", 1)],
     "c3": [("k_fq_fwd<", "fq_fwd", 1), ("k_lsq_bwd<", "lsq_bwd", 1)],
     # C4: per step 27 fused-ReLU activation launches each way + ONE multi-tensor launch
