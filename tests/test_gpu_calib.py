@@ -221,3 +221,37 @@ def test_observe_fq_small_rejects_large():
     n = FQ.observe_fq_parts_max_elems() + 1
     with pytest.raises(Exception):
         FQ.observe_fake_quant(torch.randn(n, device=DEV), symmetric=True, qmin=-128, qmax=127)
+
+
+@pytest.mark.parametrize("sym,bits", [(True, 8), (False, 8), (True, 4)])
+@pytest.mark.parametrize("shape", [(256, 256), (7, 13, 41, 43)])
+def test_manager_observe_quantize_mid_size_vs_oracle(shape, sym, bits):
+    """QuantizationManager per-call observe + quantize (qm.py:73-90 -> minmax.py:32-74 ->
+    uniform.py:34-56) at BASELINE C1's 256x256 and an odd 157K-element shape, both on the
+    K9 path: three calls carry the running min/max (the second with a NaN, which changes
+    nothing), then y, the running bounds, scale / zero point and the STE gradient of the
+    last call bit for bit against the oracle."""
+    import vsiquantization_amd as V
+    from oracle import fakequant_np as O
+    rng = np.random.default_rng(sum(shape) + bits)
+    qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", bits, sym, True)
+    qm.is_observer_qparam, qm.is_learning_scale, qm.is_quantize = True, False, True
+    mn, mx = 0, 0
+    for i in range(3):
+        x = (rng.standard_normal(shape) * (1 + i)).astype(np.float32)
+        if i == 1:
+            x.reshape(-1)[x.size // 3] = np.nan
+        g = rng.standard_normal(shape).astype(np.float32)
+        xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+        y = qm.quantize(xt)
+        y.backward(torch.from_numpy(g).to(DEV))
+        mn, mx = O.observe_minmax(x, mn, mx)
+        s, z = O.minmax_qparams(mn, mx, sym, 8)   # the manager's observer is always 8-bit
+        qmin, qmax = O.qrange(bits, sym)
+        yo, _, mask = O.fq_forward(x, s, z, qmin, qmax)
+        gxo = O.fq_backward_fixed(g, mask, s)
+        torch.cuda.synchronize()
+        assert (qm.observer.min_val, qm.observer.max_val) == (mn, mx)
+        assert float(qm.scale) == s and float(qm.zero_point) == z
+        assert np.array_equal(y.detach().cpu().numpy().view(np.uint32), yo.view(np.uint32))
+        assert np.array_equal(xt.grad.cpu().numpy().view(np.uint32), gxo.view(np.uint32))
