@@ -664,14 +664,23 @@ class ActQuant:
         self.n = sum(t["x"].numel() for t in self.L)
         self.slots = [None]
         self.kernels = {"observe_quant_all_layers": 12 * self.n}
+        # distributed.gather_stats with its per-call lookups (world size, backend, output
+        # views) done once: the step issues 27 of them, so at N = 8 their host cost counts
+        self.gather = None
+        if world > 1:
+            if dist.get_backend() == "gloo":   # CPU rehearsals: the list form
+                for t in self.L:
+                    t["gat_views"] = list(t["gat"].view(world, H.ST_LEN).unbind(0))
+                self.gather = lambda t: dist.all_gather(t["gat_views"], t["st"])
+            else:
+                self.gather = lambda t: dist.all_gather_into_tensor(t["gat"], t["st"])
 
     def launch(self, i):
-        from vsiquantization_amd.distributed import gather_stats
         rc = 0
         for t in self.L:
             rc |= self.f_obs(*t["obs"])
-            if self.world > 1:   # one all_gather of the 10-double records + one fold launch
-                gather_stats(t["st"], out=t["gat"])
+            if self.gather is not None:   # one all_gather of the 10-double records + one fold launch
+                self.gather(t)
                 rc |= self.f_fin(*t["fin"])
             rc |= self.f_fq(*t["fq"])
         return rc
