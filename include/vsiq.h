@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 6
+#define VSIQ_ABI_VERSION 7
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -401,15 +401,22 @@ int vsiq_lsq_fold_multi(const vsiq_lsq_fold *folds, int count, void *stream);
  * F.relu / F.silu after the conv (modules/fused.py:124-134, :198-206) followed by
  * quantize_out (quantizers/fake_quantize.py:49-50): the conv output c is read
  * once and act(c) is never materialized.  act: VSIQ_ACT_NONE / _RELU / _SILU.
- *   relu(c) = c < 0 ? 0 : c        bwd: c <= 0 ? 0 : g          (bit-exact)
- *   silu(c) = c / (1 + exp(-c))    bwd: g*sig*(1 + c*(1 - sig))  (GPU expf: within
- *                                  a few ulp of torch's CPU Sleef exp)
+ *   relu(c) = c < 0 ? 0 : c        bwd: c <= 0 ? 0 : g                          (bit-exact)
+ *   silu(c) = c / (1 + exp(-c))    bwd: (g*sig) * fma(c, 1 - sig, 1), sig = 1/(1+exp(-c))
+ *     bit for bit what torch's CPU silu kernels compute on the reference host: exp is
+ *     Sleef_expf_u10 on the vectorized elements and glibc expf on the scalar remainder of
+ *     each at::parallel_for chunk.  Which elements those are depends on the host's
+ *     vector width and torch thread count; pass them with VSIQ_ACT_SILU_REF(W, threads)
+ *     (W = 2 x floats per vector: 32 on AVX-512, 16 on AVX2; plain VSIQ_ACT_SILU = every
+ *     element on the vectorized path).  DESIGN.md §2.1.
  * Each entry point is its plain counterpart applied to act(c); the backward ones
  * take c again and return the gradient with respect to c.
  */
 #define VSIQ_ACT_NONE 0
 #define VSIQ_ACT_RELU 1
 #define VSIQ_ACT_SILU 2
+/* W in {0, 8, 16, 32, 64}, threads in [0, 32767] (0 and 1: one chunk) */
+#define VSIQ_ACT_SILU_REF(W, threads) (VSIQ_ACT_SILU | ((W) << 8) | ((threads) << 16))
 int vsiq_act_fq_fwd_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
                         const double *qp_dev, const double *scale_dev, double scale_host,
                         const double *zp_dev, double zp_host, int zp_round, int discrete, int qmin,
@@ -425,6 +432,17 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
                          double zp_host, int zp_learn, int qmin, int qmax, double gscale,
                          double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
                          void *stream);
+/*
+ * The activation alone (K5's element code, same act argument): y = act(c) and its
+ * backward gc = d act(c)/dc * g.  Replaces F.relu / F.silu of the fused layers
+ * (modules/fused.py:133, torch.nn.functional.silu's CPU kernel) where the activation's
+ * output is not fake-quantized in the same pass (calibration forwards).  act != NONE.
+ */
+int vsiq_act_fwd_f32(const float *c, float *y, int64_t n, int act, void *stream);
+int vsiq_act_bwd_f32(const float *g, const float *c, float *gc, int64_t n, int act, void *stream);
+/* Self-test of the two exps SiLU uses (Sleef expf_u10 / glibc expf, op for op): writes
+ * both for n inputs; tests compare them bitwise with the oracle (tests/test_gpu_silu.py). */
+int vsiq_selftest_exp_f32(const float *x, float *sleef_out, float *glibc_out, int64_t n, void *stream);
 
 /*
  * Per-channel fake quant on a [rows, rowlen] view where row r uses the qparams of

@@ -189,27 +189,87 @@ def lsq_module_grad_scale(x_shape, qmax, per_channel, config_act):
 
 
 # --------------------------------------------------------------------------- fused activation (K5)
-def act_forward(c, act):
+# F.silu on the reference's CPU tensors is torch's CPU silu kernel, whose exp is SLEEF's
+# vectorized expf on most elements and glibc's scalar expf on the remainder of every
+# parallel chunk; oracle/silu_ref.c restates both exps and the chunking (pinned against
+# torch itself by tests/test_silu_oracle.py).  silu_ref = (W, threads) of the reference
+# host: W = 2 x floats per vector (32 AVX-512, 16 AVX2, 0 = all on the vector path).
+SILU_REF_DEFAULT = (32, 1)
+_SILU = []
+
+
+def _silu_lib():
+    if not _SILU:
+        import ctypes
+
+        from oracle import build_oracle
+        lib = ctypes.CDLL(build_oracle.build(verbose=False))
+        P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        lib.oracle_silu_fwd.argtypes = [P, P, I64, I, I, P]
+        lib.oracle_silu_bwd.argtypes = [P, P, P, I64, I, I, P]
+        lib.oracle_silu_scalar_map.argtypes = [P, I64, I, I]
+        lib.oracle_exp_both.argtypes = [P, P, P, I64]
+        _SILU.append(lib)
+    return _SILU[0]
+
+
+def _p(a):
+    import ctypes
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def silu_forward(c, silu_ref=SILU_REF_DEFAULT):
+    """torch CPU F.silu(c) on a host with layout silu_ref (flat element order)."""
+    c = np.ascontiguousarray(c, dtype=F32)
+    y = np.empty_like(c)
+    sc = np.empty(max(c.size, 1), np.uint8)
+    _silu_lib().oracle_silu_fwd(_p(c), _p(y), c.size, int(silu_ref[0]), int(silu_ref[1]), _p(sc))
+    return y
+
+
+def silu_backward(g, c, silu_ref=SILU_REF_DEFAULT):
+    """torch CPU silu_backward(g, c) on a host with layout silu_ref."""
+    g = np.ascontiguousarray(g, dtype=F32)
+    c = np.ascontiguousarray(c, dtype=F32)
+    gx = np.empty_like(c)
+    sc = np.empty(max(c.size, 1), np.uint8)
+    _silu_lib().oracle_silu_bwd(_p(g), _p(c), _p(gx), c.size, int(silu_ref[0]), int(silu_ref[1]), _p(sc))
+    return gx
+
+
+def silu_scalar_map(n, silu_ref=SILU_REF_DEFAULT):
+    """bool[n]: elements torch's CPU kernel computes on its scalar (glibc expf) path."""
+    sc = np.empty(max(n, 1), np.uint8)
+    _silu_lib().oracle_silu_scalar_map(_p(sc), int(n), int(silu_ref[0]), int(silu_ref[1]))
+    return sc[:n].astype(bool)
+
+
+def exp_sleef_glibc(x):
+    """(Sleef expf_u10(x), glibc expf(x)) of the restatement, for pinning."""
+    x = np.ascontiguousarray(x, dtype=F32)
+    a, b = np.empty_like(x), np.empty_like(x)
+    _silu_lib().oracle_exp_both(_p(x), _p(a), _p(b), x.size)
+    return a, b
+
+
+def act_forward(c, act, silu_ref=SILU_REF_DEFAULT):
     """The fused layers' activation before quantize_out (modules/fused.py:133):
-    F.relu (torch CPU: c < 0 -> +0, -0.0 and NaN pass through) or F.silu
-    (torch CPU silu_kernel: c / (1 + exp(-c)), fp32; numpy's exp is within an ulp
-    of torch's Sleef exp, so SiLU parity is toleranced, see tests)."""
+    F.relu (torch CPU: c < 0 -> +0, -0.0 and NaN pass through) or F.silu (torch CPU
+    silu_kernel, bit for bit: silu_forward)."""
     c = np.asarray(c, dtype=F32)
     if act is None or act == "none":
         return c
     if act == "relu":
         return np.where(c < 0, F32(0.0), c).astype(F32)
     if act == "silu":
-        with np.errstate(all="ignore"):
-            return (c / (F32(1.0) + np.exp(-c).astype(F32))).astype(F32)
+        return silu_forward(c, silu_ref).reshape(c.shape)
     raise ValueError(act)
 
 
-def act_backward(g, c, act):
+def act_backward(g, c, act, silu_ref=SILU_REF_DEFAULT):
     """Autograd of act_forward: relu threshold_backward(g, relu(c), 0) = c <= 0 ? 0 : g
-    (NaN passes g); silu_backward (g * sig) * fma(c, 1 - sig, 1): torch's vectorized
-    CPU kernel contracts the inner multiply-add into an FMA (matches its outputs far
-    better than the unfused order; exp itself still differs by an ulp)."""
+    (NaN passes g); silu_backward (g * sig) * fma(c, 1 - sig, 1) with the same exp split
+    as the forward (silu_backward)."""
     g = np.asarray(g, dtype=F32)
     c = np.asarray(c, dtype=F32)
     if act is None or act == "none":
@@ -217,11 +277,7 @@ def act_backward(g, c, act):
     if act == "relu":
         return np.where(c <= 0, F32(0.0), g).astype(F32)
     if act == "silu":
-        with np.errstate(all="ignore"):
-            sig = (F32(1.0) / (F32(1.0) + np.exp(-c).astype(F32))).astype(F32)
-            one_m = (F32(1.0) - sig).astype(F32)
-            inner = (c.astype(np.float64) * one_m.astype(np.float64) + 1.0).astype(F32)   # fma
-            return ((g * sig).astype(F32) * inner).astype(F32)
+        return silu_backward(g, c, silu_ref).reshape(c.shape)
     raise ValueError(act)
 
 

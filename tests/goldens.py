@@ -9,6 +9,11 @@ GOLDEN_DIR = os.path.join(HERE, "golden")
 
 _cache = {}
 
+# The reference host the goldens were generated on (tests/golden/gen_goldens.py, the build
+# container): torch CPU kernels AVX-512 (W = 32 elements per vectorized SiLU step), 8
+# threads.  Every golden tensor is below torch's 32768-element grain, so only W matters.
+GOLDEN_SILU_REF = (32, 8)
+
 
 def load():
     if "d" not in _cache:
@@ -57,8 +62,8 @@ def unpack_mask(words, rows, rowlen):
 
 
 def assert_close_f32(got, want, what="", rtol=1e-5, atol=1e-6):
-    """Toleranced fp32 comparison for SiLU paths (exp differs by ~1 ulp between
-    torch's CPU Sleef exp, numpy and the GPU); NaNs must coincide."""
+    """Toleranced fp32 comparison (floats the reference does not pin bitwise, e.g. MIOpen's
+    weight gradient); NaNs must coincide."""
     got = np.asarray(got, dtype=np.float32)
     want = np.asarray(want, dtype=np.float32)
     assert got.shape == want.shape, f"{what}: shape {got.shape} vs {want.shape}"
@@ -67,16 +72,3 @@ def assert_close_f32(got, want, what="", rtol=1e-5, atol=1e-6):
     ok = np.isclose(got[~gn], want[~wn], rtol=rtol, atol=atol)
     assert ok.all(), (f"{what}: {int((~ok).sum())} of {ok.size} elements beyond rtol={rtol} "
                       f"atol={atol}; max abs diff {np.max(np.abs(got[~gn] - want[~wn]))}")
-
-
-def assert_fq_close(got, want, scale, what="", max_frac=0.01):
-    """SiLU + fake quant: the codes may move by one step where silu(c) itself sits on
-    a rounding boundary (a 1-ulp exp difference); everything else bitwise."""
-    got = np.asarray(got, dtype=np.float32)
-    want = np.asarray(want, dtype=np.float32)
-    gn, wn = np.isnan(got), np.isnan(want)
-    assert np.array_equal(gn, wn), f"{what}: NaN positions differ"
-    d = np.abs(got[~gn].astype(np.float64) - want[~wn].astype(np.float64))
-    bad = d > 0
-    assert (d <= float(np.float32(scale)) * 1.0001 + 1e-12).all(), f"{what}: a code moved by > 1 step"
-    assert bad.mean() <= max_frac, f"{what}: {bad.mean():.4f} of elements moved a step"

@@ -1,0 +1,192 @@
+"""SiLU bit for bit as the reference computes it (F.silu on CPU tensors, modules/fused.py:133):
+every kernel that applies a fused SiLU (K5: K1 / STE / K4 / K4d / K2 / K2p / K2m / K8 / K9,
+and the activation alone) against
+
+* this box's own torch CPU kernels (torch.nn.functional.silu / aten.silu_backward) at
+  several thread counts -- the product follows the host's torch layout by default;
+* the oracle (oracle/silu_ref.c) under pinned multi-chunk layouts (W = 32 / 16 elements
+  per vectorized step, 7 threads), where every chunk of the tensor has a scalar
+  remainder computed with glibc's expf;
+* the two exps themselves (vsiq_selftest_exp_f32) on 2^24 inputs across the whole
+  activation range, the overflow / underflow edges and random bit patterns.
+"""
+import numpy as np
+import pytest
+import torch
+
+import vsiquantization_amd as V
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import fakequant as FQ
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HOST_W = {"AVX512": 32, "AVX2": 16}.get(torch.backends.cpu.get_cpu_capability())
+
+
+def cu(a, grad=False):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t.requires_grad_(True) if grad else t
+
+
+def npy(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture
+def pin():
+    """Pin the product's SiLU layout (and restore host-following + torch threads after)."""
+    t0 = torch.get_num_threads()
+
+    def _pin(w, t):
+        H.set_silu_reference(w, t)
+        return (w, t)
+    yield _pin
+    H.set_silu_reference()
+    torch.set_num_threads(t0)
+
+
+def _inputs(n, seed, scale=4.0):
+    rng = np.random.default_rng(seed)
+    c = (rng.standard_normal(n) * scale).astype(np.float32)
+    if n > 16:
+        c[:10] = [0.0, -0.0, np.nan, np.inf, -np.inf, 1e-40, 88.9, -88.9, 104.5, -104.5]
+    return c, rng.standard_normal(n).astype(np.float32)
+
+
+def test_exps_bitwise_vs_oracle():
+    x = np.concatenate([
+        np.linspace(-110.0, 110.0, 1 << 23, dtype=np.float32),
+        np.linspace(-1.0, 1.0, 1 << 22, dtype=np.float32),
+        np.random.default_rng(0).integers(0, 2**32, 1 << 22, dtype=np.uint64).astype(np.uint32).view(np.float32),
+        np.array([np.inf, -np.inf, np.nan, 0.0, -0.0, 88.72283, 88.72284, -103.97208, -103.97209, 100.0, 100.00001,
+                  -104.0, -104.00001, 1e-45, -1e-45], np.float32)])
+    xs = cu(x)
+    ys, yg = torch.empty_like(xs), torch.empty_like(xs)
+    H.check(H.lib().vsiq_selftest_exp_f32(H.ptr(xs), H.ptr(ys), H.ptr(yg), H.c_i64(x.size), H.stream_of(torch.device(DEV))),
+            "vsiq_selftest_exp_f32")
+    ws, wg = O.exp_sleef_glibc(x)
+    G.assert_bitwise_f32(npy(ys), ws, "Sleef expf_u10")
+    G.assert_bitwise_f32(npy(yg), wg, "glibc expf")
+
+
+@pytest.mark.skipif(HOST_W is None, reason="this host's torch CPU kernels are neither AVX2 nor AVX-512")
+@pytest.mark.parametrize("threads", [1, 5, 16])
+@pytest.mark.parametrize("n", [1, 31, 1296, 32769, 100_003, 1_000_003, 4_000_037])
+def test_activation_equals_host_torch_cpu(n, threads, pin):
+    """Default layout = this host's torch: the HIP activation equals torch's CPU F.silu and
+    silu_backward on the same values, bit for bit, at every thread count."""
+    torch.set_num_threads(threads)
+    c, g = _inputs(n, n + threads)
+    x = cu(c, grad=True)
+    y = FQ.activation(x, "silu")
+    y.backward(cu(g))
+    want_y = torch.nn.functional.silu(torch.from_numpy(c)).numpy()
+    want_g = torch.ops.aten.silu_backward(torch.from_numpy(g), torch.from_numpy(c)).numpy()
+    G.assert_bitwise_f32(npy(y), want_y, "silu")
+    G.assert_bitwise_f32(npy(x.grad), want_g, "silu_backward")
+
+
+LAYOUTS = [(32, 7), (16, 7), (32, 1), (0, 1)]
+SIZES = [33, 40_000, 100_003, 1_000_003]
+
+
+@pytest.mark.parametrize("ref", LAYOUTS, ids=lambda r: f"W{r[0]}T{r[1]}")
+@pytest.mark.parametrize("n", SIZES)
+def test_fixed_fq_and_ste_vs_oracle(n, ref, pin):
+    pin(*ref)
+    c, g = _inputs(n, n)
+    y, mask, _ = FQ.fake_quant(cu(c), 0.021, 3, 0, 255, want_mask=True, act="silu")
+    gc = FQ.ste_backward(cu(g), mask, 0.021, pre=cu(c), act="silu")
+    a = O.act_forward(c, "silu", ref)
+    yo, _, mo = O.fq_forward(a, 0.021, 3, 0, 255)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    assert np.array_equal(G.unpack_mask(npy(mask), 1, n)[0], mo)
+    G.assert_bitwise_f32(npy(gc), O.act_backward(O.fq_backward_fixed(g, mo, 0.021), c, "silu", ref), "grad_c")
+
+
+@pytest.mark.parametrize("ref", LAYOUTS[:2], ids=lambda r: f"W{r[0]}T{r[1]}")
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("deferred", [False, True])
+def test_learnable_vs_oracle(n, ref, deferred, pin):
+    """K1 + K4 (and the records-only K4d with its fold) through a fused SiLU."""
+    pin(*ref)
+    c, g = _inputs(n, n + 1, 2.0)
+    c[2:5] = [0.5, 7.0, -7.0]   # finite: a NaN / inf term would make the scale gradient NaN
+    q = V.UniformQuantizer(8, True)
+    s = torch.nn.Parameter(torch.tensor(0.03, dtype=torch.float64, device=DEV))
+    x = cu(c, grad=True)
+    if deferred:
+        from vsiquantization_amd.quantizers.deferred import DeferredLearnFn, QParamBundleFn
+        sb = QParamBundleFn.apply(s)
+        sb = sb[0] if isinstance(sb, tuple) else sb
+        y = DeferredLearnFn.apply(x, sb, 0, q.qmin, q.qmax, O.grad_scale(q.qmax, n), False, "silu")
+    else:
+        y = q.quantize(x, s, 0, True, act="silu")
+    y.backward(cu(g))
+    a = O.act_forward(c, "silu", ref)
+    yo, gxo, gso, _ = O.lsq_forward_backward(a, g, 0.03, 0, q.qmin, q.qmax, O.grad_scale(q.qmax, n))
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(x.grad), O.act_backward(gxo, c, "silu", ref), "grad_c")
+    assert abs(float(s.grad) - gso) <= 1e-9 * abs(gso)
+
+
+@pytest.mark.parametrize("ref", LAYOUTS[:2], ids=lambda r: f"W{r[0]}T{r[1]}")
+@pytest.mark.parametrize("n", SIZES)
+def test_observers_vs_oracle(n, ref, pin):
+    """K2 (per-call), K2p records + fold, K2m, and K8 / K9 (observe + fake quant)."""
+    pin(*ref)
+    c, _ = _inputs(n, n + 2, 3.0)
+    c[2:5] = [0.5, 7.0, -7.0]   # no NaN in silu(c) (silu(-inf) is NaN): the qparams exist
+    a = O.act_forward(c, "silu", ref)
+    mn, mx = O.observe_minmax(a)
+    s, z = O.minmax_qparams(mn, mx, False, 8)
+    x = cu(c)
+    qp, st = FQ.observe_tensor(x, symmetric=False, act="silu")
+    qph = npy(qp)
+    assert (qph[H.QP_SCALE], qph[H.QP_ZP], qph[H.QP_MIN], qph[H.QP_MAX]) == (s, z, mn, mx)
+    folded = npy(FQ.fold_parts(torch.stack([FQ.observe_parts(x, act="silu")])))[0]
+    assert (folded[H.ST_MIN], folded[H.ST_MAX]) == (mn, mx)
+    multi = FQ.observe_parts_multi([x, x[: n // 2]], None, act="silu")
+    single = FQ.observe_parts(x, act="silu")
+    assert torch.equal(multi[0].view(torch.int64), single.view(torch.int64))
+    if n <= FQ.observe_fq_parts_max_elems():
+        y, qp2, _, _, _ = FQ.observe_fake_quant(x, symmetric=False, qmin=0, qmax=255, act="silu")
+        assert (float(qp2[H.QP_SCALE]), float(qp2[H.QP_ZP])) == (s, z)
+        G.assert_bitwise_f32(npy(y), O.fq_forward(a, s, z, 0, 255)[0], "K8/K9 y")
+    # the half-size tensor has its own chunk layout
+    h = n // 2
+    mh, xh = O.observe_minmax(O.act_forward(c[:h], "silu", ref))
+    fh = npy(FQ.fold_parts(torch.stack([multi[1]])))[0]
+    assert (fh[H.ST_MIN], fh[H.ST_MAX]) == (mh, xh)
+
+
+def test_calibration_forward_hands_on_reference_silu(pin):
+    """A calibration forward (observe only) returns silu(c) for the next layer: the HIP
+    activation, torch CPU's bits (not torch's HIP silu)."""
+    ref = pin(32, 3)
+    qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", 8, True)
+    qm.is_quantize, qm.is_learning_scale, qm.is_observer_qparam = False, False, True
+    c, _ = _inputs(200_003, 9)
+    c[2:5] = [0.25, 7.0, -7.0]
+    out = qm.quantize(cu(c), act="silu")
+    G.assert_bitwise_f32(npy(out), O.act_forward(c, "silu", ref), "calibration output")
+    qm._join()
+    mn, mx = O.observe_minmax(O.act_forward(c, "silu", ref))
+    assert (qm.observer.min_val, qm.observer.max_val) == (mn, mx)
+
+
+def test_silu_act_code_layout():
+    """The act argument carries (W, threads); malformed codes are rejected by the ABI."""
+    H.set_silu_reference(32, 12)
+    try:
+        code = H.act_code("silu")
+        assert code == 2 | (32 << 8) | (12 << 16)
+        x = torch.randn(100, device=DEV)
+        y = torch.empty_like(x)
+        assert H.lib().vsiq_act_fwd_f32(H.ptr(x), H.ptr(y), H.c_i64(100), 2 | (24 << 8), H.stream_of(torch.device(DEV))) != 0
+        assert H.lib().vsiq_act_fwd_f32(H.ptr(x), H.ptr(y), H.c_i64(100), 1 | (32 << 8), H.stream_of(torch.device(DEV))) != 0
+        assert H.lib().vsiq_act_fwd_f32(H.ptr(x), H.ptr(y), H.c_i64(100), code, H.stream_of(torch.device(DEV))) == 0
+    finally:
+        H.set_silu_reference()

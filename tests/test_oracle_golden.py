@@ -137,7 +137,8 @@ def test_manager_sequence(case):
 
 @pytest.mark.parametrize("case", G.cases("act_fq"), ids=lambda c: c["key"])
 def test_act_fq(case):
-    """Fused activation + activation fake quant (K5): ReLU bit-exact, SiLU toleranced."""
+    """Fused activation + activation fake quant (K5): bit-exact for ReLU and SiLU (torch's
+    CPU silu restated with its two exps, oracle/silu_ref.c)."""
     c = G.arr(case["x"])
     g = G.arr(case["g"])
     qmin, qmax = O.qrange(case["bits"], case["sym"])
@@ -154,12 +155,34 @@ def test_act_fq(case):
         y, _, m = O.fq_forward(a, s, z, qmin, qmax)
         gx = O.fq_backward_fixed(g, m, s)
     gc = O.act_backward(gx, c, case["act"])
-    if case["act"] == "relu":
-        G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
-        G.assert_bitwise_f32(gc, G.arr(case["grad_x"]), "grad_c")
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(gc, G.arr(case["grad_x"]), "grad_c")
+
+
+@pytest.mark.parametrize("case", [c for c in G.cases("fused_layer") if c["act"]], ids=lambda c: c["key"])
+@pytest.mark.parametrize("mode", ["observe", "learn"])
+def test_fused_layer_activation(case, mode):
+    """The fused layers' F.relu / F.silu + quantize_out on the reference's own
+    pre-activation (modules/fused.py:133, fake_quantize.py:49-50): y and the gradient
+    with respect to the pre-activation bit-exact.  fz1 / fz9 (SiLU, 1296 and 120
+    elements) have 16 / 24 elements on torch's scalar (glibc expf) path."""
+    if mode not in case:
+        pytest.skip("asymmetric layer: no learnable mode in the reference")
+    rec = case[mode]
+    pre, g = G.arr(rec["pre"]), G.arr(rec["g"])
+    a = O.act_forward(pre, case["act"])
+    qmin, qmax = O.qrange(case["bits_a"], case["a_sym"])
+    if mode == "observe":
+        s, z = O.minmax_qparams(*O.observe_minmax(a), case["a_sym"], 8)
+        assert (s, z) == (rec["act_qp"]["scale"], rec["act_qp"]["zp"])
+        y, _, m = O.fq_forward(a, s, z, qmin, qmax)
+        gx = O.fq_backward_fixed(g, m, s)
     else:
-        G.assert_fq_close(y, G.arr(case["y"]), s, "y")
-        G.assert_close_f32(gc, G.arr(case["grad_x"]), "grad_c")
+        y, gx, gs, _ = O.lsq_forward_backward(a, g, rec["init_scale_a"], 0, qmin, qmax,
+                                              O.grad_scale(qmax, a.size))
+        assert gs == pytest.approx(rec["scale_grad_a"], rel=1e-4)
+    G.assert_bitwise_f32(y, G.arr(rec["y"]), "y")
+    G.assert_bitwise_f32(O.act_backward(gx, pre, case["act"]), G.arr(rec["grad_pre"]), "grad_pre")
 
 
 @pytest.mark.parametrize("case", G.cases("lsq_fake_quantize"), ids=lambda c: c["key"])

@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
@@ -43,15 +43,50 @@ TUNE_XCD_ORDER = 13
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
+# SiLU bit for bit as torch's CPU kernel on this host (include/vsiq.h VSIQ_ACT_SILU_REF):
+# which elements torch computes with glibc's scalar expf instead of the vectorized Sleef
+# exp depends on the vector width of torch's CPU kernels and on its thread count.
+_SILU_W = {"AVX512": 32, "AVX2": 16}
+_SILU_PIN = []   # set_silu_reference(): (W, threads) instead of this host's
+
+
+def set_silu_reference(width=None, threads=None):
+    """Pin the reference CPU layout SiLU is reproduced for: ``width`` = 2 x floats per
+    vector (32 AVX-512, 16 AVX2, 0 = every element on the vectorized path), ``threads`` =
+    torch's CPU thread count.  No arguments: follow this host's torch (the default)."""
+    _SILU_PIN.clear()
+    if width is not None:
+        if width not in (0, 8, 16, 32, 64) or not 0 <= int(threads or 0) < 32768:
+            raise ValueError(f"silu reference width {width} / threads {threads}")
+        _SILU_PIN.append((int(width), int(threads or 1)))
+
+
+def silu_reference():
+    """(W, threads) of the reference CPU layout act="silu" reproduces."""
+    if _SILU_PIN:
+        return _SILU_PIN[0]
+    return _SILU_W.get(torch.backends.cpu.get_cpu_capability(), 16), torch.get_num_threads()
+
 
 def act_code(act) -> int:
-    """None / "relu" / "silu" (or the VSIQ_ACT_* integer) -> VSIQ_ACT_* code."""
+    """None / "relu" / "silu" (or the VSIQ_ACT_* integer) -> the C ABI act argument
+    (SiLU carries the reference CPU layout, VSIQ_ACT_SILU_REF)."""
     if isinstance(act, int) and act in (ACT_NONE, ACT_RELU, ACT_SILU):
-        return act
-    try:
-        return ACT_CODES[act]
-    except KeyError:
-        raise ValueError(f"unsupported fused activation {act!r} (None, 'relu' or 'silu')") from None
+        code = act
+    else:
+        try:
+            code = ACT_CODES[act]
+        except KeyError:
+            raise ValueError(f"unsupported fused activation {act!r} (None, 'relu' or 'silu')") from None
+    if code == ACT_SILU:
+        w, t = silu_reference()
+        return ACT_SILU | (w << 8) | (min(max(t, 0), 32767) << 16)
+    return code
+
+
+def act_kind(code: int) -> int:
+    """The activation of a C ABI act argument (low byte)."""
+    return code & 0xff
 
 _SIGS = {
     "vsiq_abi_version": ([], c_int),
@@ -104,6 +139,9 @@ _SIGS = {
     "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
     "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),
     "vsiq_lsq_bwd_multi_f32": ([c_p, c_int, c_p, c_i64, c_p, c_p], c_int),
+    "vsiq_act_fwd_f32": ([c_p, c_p, c_i64, c_int, c_p], c_int),
+    "vsiq_act_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p], c_int),
+    "vsiq_selftest_exp_f32": ([c_p, c_p, c_p, c_i64, c_p], c_int),
     "vsiq_act_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_i64, c_d, c_p], c_int),
     "vsiq_act_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_d,
                               c_p, c_p, c_i64, c_p, c_p], c_int),

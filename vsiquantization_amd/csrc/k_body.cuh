@@ -16,7 +16,7 @@ template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U = kFlatU>
 __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float *__restrict__ y,
                                              uint8_t *__restrict__ codes, uint64_t *__restrict__ mask,
                                              int64_t n, const QP &p, int64_t blk, GateClk gc = GateClk{0},
-                                             uint32_t gate = 0) {
+                                             uint32_t gate = 0, const SiluLay &L = SiluLay{}) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * U + threadIdx.x;   // lanes chunk-aligned
   f4 v[U];
@@ -26,7 +26,8 @@ __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float 
   uint32_t mlo = 0, mhi = 0;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4<ACT>(v[u]), p, base + u * kBlock, n);
+    go[u] = fq_out_flat<VEC, CODES, MASK>(act_fwd4_at<ACT>(v[u], 4 * (base + u * kBlock), L), p,
+                                          base + u * kBlock, n);
     if (MASK) mask_put(mlo, mhi, u, go[u].b);
   }
   gate_pass(gate, gc);
@@ -108,8 +109,8 @@ __device__ __forceinline__ void lsq_block_reduce(LsqAcc &c) {
 // Returns the group's grad_x (not stored).
 template <bool ZPL, int ACT>
 __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4 xc, f4 gv, const QP &p,
-                                            LsqAcc &c) {
-  const f4 xv = act_fwd4<ACT>(xc);
+                                            LsqAcc &c, const SiluLay &L = SiluLay{}) {
+  const f4 xv = act_fwd4_at<ACT>(xc, 4 * i, L);
   const int nv = i < ng ? valid_in_group(i, n) : 0;
   const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
                   lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p));
@@ -125,7 +126,7 @@ __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4
     o.z = lsq_elem<ZPL, true>(xv.z, gv.z, p, c, nv > 2);
     o.w = lsq_elem<ZPL, true>(xv.w, gv.w, p, c, nv > 3);
   }
-  return act_bwd4<ACT>(o, xc);
+  return act_bwd4_at<ACT>(o, xc, 4 * i, L);
 }
 
 template <bool VEC, bool NT, bool ZPL, int ACT>
@@ -141,7 +142,8 @@ __device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int6
 // leaves grad_x in o[] (stored by lsq_store_block once the block has arrived).
 template <bool VEC, bool NT, bool ZPL, int ACT, int G>
 __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const float *__restrict__ x,
-                                              int64_t n, const QP &p, int64_t blk, LsqAcc &c, f4 (&o)[G]) {
+                                              int64_t n, const QP &p, int64_t blk, LsqAcc &c, f4 (&o)[G],
+                                              const SiluLay &L = SiluLay{}) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * G + threadIdx.x;
   f4 xv[G], gv[G];
@@ -156,7 +158,7 @@ __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const
       xv[k + kLsqPrefetch] = load_group_c<VEC, NT>(x, base + (k + kLsqPrefetch) * kBlock, ng, n);
       gv[k + kLsqPrefetch] = load_group_c<VEC, NT>(g, base + (k + kLsqPrefetch) * kBlock, ng, n);
     }
-    o[k] = lsq_group_out<ZPL, ACT>(base + k * kBlock, ng, n, xv[k], gv[k], p, c);
+    o[k] = lsq_group_out<ZPL, ACT>(base + k * kBlock, ng, n, xv[k], gv[k], p, c, L);
   }
 }
 

@@ -145,7 +145,7 @@ __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *_
 // on its tensors' block ranges).
 template <bool VEC, bool NT, int ACT, int U>
 __device__ __forceinline__ void observe_stride_b(const float *__restrict__ x, int64_t n, ObsAcc &a,
-                                                 int64_t blk, int64_t nblk) {
+                                                 int64_t blk, int64_t nblk, const SiluLay &L) {
   obs_init(a);
   const int64_t ng = cdiv(n, 4);
   const int64_t nfull = n / 4;
@@ -161,28 +161,29 @@ __device__ __forceinline__ void observe_stride_b(const float *__restrict__ x, in
 #pragma unroll
       for (int k = 0; k < U; ++k) v[k] = ld4<NT>(xb + 4 * (threadIdx.x + k * kBlock));
 #pragma unroll
-      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4_at<ACT>(v[k], 4 * (b + threadIdx.x + k * kBlock), L), 4);
       continue;
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
     if (b + (int64_t)kBlock * U <= nfull) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
+      for (int k = 0; k < U; ++k) obs_add4(a, act_fwd4_at<ACT>(v[k], 4 * (b + threadIdx.x + k * kBlock), L), 4);
     } else {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const int64_t i = b + threadIdx.x + k * kBlock;
-        if (i < nfull) obs_add4(a, act_fwd4<ACT>(v[k]), 4);
-        else if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+        if (i < nfull) obs_add4(a, act_fwd4_at<ACT>(v[k], 4 * i, L), 4);
+        else if (i < ng) obs_add4(a, act_fwd4_at<ACT>(v[k], 4 * i, L), valid_in_group(i, n));
       }
     }
   }
 }
 
 template <bool VEC, bool NT, int ACT, int U>
-__device__ __forceinline__ void observe_stride(const float *__restrict__ x, int64_t n, ObsAcc &a) {
-  observe_stride_b<VEC, NT, ACT, U>(x, n, a, blockIdx.x, gridDim.x);
+__device__ __forceinline__ void observe_stride(const float *__restrict__ x, int64_t n, ObsAcc &a,
+                                               const SiluLay &L) {
+  observe_stride_b<VEC, NT, ACT, U>(x, n, a, blockIdx.x, gridDim.x, L);
 }
 
 // One-shot: G groups per lane (grid = ng / (256 G)), all G loads issued up front
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
                                                     double *__restrict__ qp_out, int sym,
                                                     double qden, double eps,
                                                     double *__restrict__ ws,
-                                                    uint32_t *__restrict__ counter) {
+                                                    uint32_t *__restrict__ counter, SiluLay L) {
   ObsAcc a;
   obs_init(a);
   const int64_t ng = cdiv(n, 4);
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_observe(const float *__restrict__ x,
 #pragma unroll
   for (int k = 0; k < G; ++k) {
     const int64_t i = base + k * kBlock;
-    if (i < ng) obs_add4(a, act_fwd4<ACT>(v[k]), valid_in_group(i, n));
+    if (i < ng) obs_add4(a, act_fwd4_at<ACT>(v[k], 4 * i, L), valid_in_group(i, n));
   }
   observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
 }
@@ -223,9 +224,9 @@ __global__ __launch_bounds__(kBlock) void k_observe_loop(const float *__restrict
                                                           double *__restrict__ qp_out, int sym,
                                                           double qden, double eps,
                                                           double *__restrict__ ws,
-                                                          uint32_t *__restrict__ counter) {
+                                                          uint32_t *__restrict__ counter, SiluLay L) {
   ObsAcc a;
-  observe_stride<VEC, NT, ACT, U>(x, n, a);
+  observe_stride<VEC, NT, ACT, U>(x, n, a, L);
   observe_epilogue(a, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
 }
 
@@ -256,9 +257,9 @@ __device__ __forceinline__ void store_part_record(ObsAcc &a, double *__restrict_
 // call's records at once (deferred sync), and the running min/max is replayed there.
 template <bool VEC, bool NT, int ACT, int U>
 __global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict__ x, int64_t n,
-                                                          double *__restrict__ parts) {
+                                                          double *__restrict__ parts, SiluLay L) {
   ObsAcc a;
-  observe_stride<VEC, NT, ACT, U>(x, n, a);
+  observe_stride<VEC, NT, ACT, U>(x, n, a, L);
   store_part_record(a, parts, blockIdx.x, gridDim.x, n);
 }
 
@@ -279,7 +280,7 @@ template <bool VEC, bool NT, int ACT, bool MASK, bool CODES, int U>
 __global__ __launch_bounds__(kSmallBlock) void k_observe_fq_small(
     const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
     uint64_t *__restrict__ mask, int64_t n, double *__restrict__ stats_out, float *__restrict__ run_minmax,
-    double *__restrict__ qp_out, int sym, double qden, double eps, float lo, float hi) {
+    double *__restrict__ qp_out, int sym, double qden, double eps, float lo, float hi, SiluLay L) {
   constexpr int NW = kSmallBlock / kWave;
   __shared__ float s_mn[NW], s_mx[NW];
   __shared__ uint32_t s_nan[NW];
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(kSmallBlock) void k_observe_fq_small(
   f4 v[U];
 #pragma unroll
   for (int k = 0; k < U; ++k)
-    v[k] = act_fwd4<ACT>(load_group_c<VEC, NT>(x, threadIdx.x + k * kSmallBlock, ng, n));
+    v[k] = act_fwd4_at<ACT>(load_group_c<VEC, NT>(x, threadIdx.x + k * kSmallBlock, ng, n),
+                            4 * (int64_t)(threadIdx.x + k * kSmallBlock), L);
   ObsAcc a;
   obs_init(a);
 #pragma unroll
@@ -348,15 +350,15 @@ __global__ __launch_bounds__(kSmallBlock) void k_observe_fq_small(
 template <bool VEC, bool NT, int ACT>
 void launch_observe_fq_small(const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n, double *st,
                              float *run, double *qp, int sym, double qden, double eps, float lo, float hi,
-                             hipStream_t s) {
+                             const SiluLay &L, hipStream_t s) {
   // groups per lane: 2 up to 8192 elements (no clamped duplicate loads), else 16
 #define K8(MASK, CODES)                                                                                    \
   if (n <= (int64_t)kSmallBlock * 2 * 4)                                                                   \
     hipLaunchKernelGGL((k_observe_fq_small<VEC, NT, ACT, MASK, CODES, 2>), dim3(1), dim3(kSmallBlock), 0, s, x, \
-                       y, c, m, n, st, run, qp, sym, qden, eps, lo, hi);                                    \
+                       y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, L);                                    \
   else                                                                                                     \
     hipLaunchKernelGGL((k_observe_fq_small<VEC, NT, ACT, MASK, CODES, kSmallGroups>), dim3(1), dim3(kSmallBlock), \
-                       0, s, x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi)
+                       0, s, x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, L)
   if (m && c) { K8(true, true); }
   else if (m) { K8(true, false); }
   else if (c) { K8(false, true); }
@@ -382,7 +384,7 @@ constexpr int64_t kFoldFqMax = (int64_t)1 << 18;   // largest n (fq grid <= 128 
 
 template <int ACT, int U>
 void launch_observe_part_u(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
-                           hipStream_t st);   // K2p launch, below
+                           const SiluLay &L, hipStream_t st);   // K2p launch, below
 
 inline int64_t fold_fq_part_grid(int64_t n) {
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_fq_fwd(
     const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
     uint64_t *__restrict__ mask, int64_t n, const double *__restrict__ parts, int nrec,
     double *__restrict__ stats_out, float *__restrict__ run_minmax, double *__restrict__ qp_out, int sym,
-    double qden, double eps, float lo, float hi) {
+    double qden, double eps, float lo, float hi, SiluLay L) {
   __shared__ double s_f[kWaves][6];
   __shared__ double s_qp[2];
   double f[6];
@@ -435,20 +437,20 @@ __global__ __launch_bounds__(kBlock) void k_fold_fq_fwd(
   p.discrete = 0;
   p.d = make_fastdiv(p.s);
   p.fast = fq_fast_qp(p.s, p.z);
-  fq_fwd_block<VEC, NT, CODES, MASK, ACT, kFlatU>(x, y, codes, mask, n, p, blockIdx.x);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, kFlatU>(x, y, codes, mask, n, p, blockIdx.x, GateClk{0}, 0u, L);
 }
 
 template <int ACT>
 void launch_fold_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
                         double *parts, double *st, float *run, double *qp, int sym, double qden, double eps,
-                        float lo, float hi, hipStream_t s) {
+                        float lo, float hi, const SiluLay &L, hipStream_t s) {
   const int64_t pgrid = fold_fq_part_grid(n);
-  launch_observe_part_u<ACT, kFoldFqU>(vec, nt, x, n, parts, pgrid, s);
+  launch_observe_part_u<ACT, kFoldFqU>(vec, nt, x, n, parts, pgrid, L, s);
   const int nrec = (int)(pgrid * kWaves);
   const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4)));
 #define K9(V, T, C, M)                                                                                       \
   hipLaunchKernelGGL((k_fold_fq_fwd<V, T, C, M, ACT>), grid, dim3(kBlock), 0, s, x, y, c, m, n, parts, nrec, st, \
-                     run, qp, sym, qden, eps, lo, hi)
+                     run, qp, sym, qden, eps, lo, hi, L)
 #define K9CM(V, T)                  \
   if (c && m) { K9(V, T, true, true); }        \
   else if (c) { K9(V, T, true, false); }       \
@@ -464,10 +466,10 @@ void launch_fold_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c,
 template <int ACT>
 void launch_observe_fq_small_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
                                  double *st, float *run, double *qp, int sym, double qden, double eps, float lo,
-                                 float hi, hipStream_t s) {
-  if (vec && nt) launch_observe_fq_small<true, true, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
-  else if (vec) launch_observe_fq_small<true, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
-  else launch_observe_fq_small<false, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, s);
+                                 float hi, const SiluLay &L, hipStream_t s) {
+  if (vec && nt) launch_observe_fq_small<true, true, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, L, s);
+  else if (vec) launch_observe_fq_small<true, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, L, s);
+  else launch_observe_fq_small<false, false, ACT>(x, y, c, m, n, st, run, qp, sym, qden, eps, lo, hi, L, s);
 }
 
 // ----------------------------------------------------------------------------
@@ -492,6 +494,7 @@ struct PBatch {
   PTensor t[kPartMulti];
   uint32_t blk0[kPartMulti + 1];
   int count;
+  SiluRef sref;   // SiLU: the reference CPU layout (each tensor's chunks from its own n)
 };
 
 // ALLVEC: every tensor of the batch takes the 16-byte path (the usual case: activation
@@ -504,15 +507,17 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_multi(const PBatch b) {
   while (t + 1 < b.count && blk >= b.blk0[t + 1]) ++t;   // scalar: blk0 is a kernel argument
   const PTensor &T = b.t[t];
   const int64_t lb = (int64_t)blk - b.blk0[t], nb = T.grid;
+  SiluLay L{};
+  if constexpr (ACT == kActSilu) L = silu_lay(T.n, b.sref);
   ObsAcc a;
   if (ALLVEC || T.vec) {
-    if (T.u == 8) observe_stride_b<true, NT, ACT, 8>(T.x, T.n, a, lb, nb);
-    else if (T.u == 4) observe_stride_b<true, NT, ACT, 4>(T.x, T.n, a, lb, nb);
-    else observe_stride_b<true, NT, ACT, 2>(T.x, T.n, a, lb, nb);
+    if (T.u == 8) observe_stride_b<true, NT, ACT, 8>(T.x, T.n, a, lb, nb, L);
+    else if (T.u == 4) observe_stride_b<true, NT, ACT, 4>(T.x, T.n, a, lb, nb, L);
+    else observe_stride_b<true, NT, ACT, 2>(T.x, T.n, a, lb, nb, L);
   } else {
-    if (T.u == 8) observe_stride_b<false, false, ACT, 8>(T.x, T.n, a, lb, nb);
-    else if (T.u == 4) observe_stride_b<false, false, ACT, 4>(T.x, T.n, a, lb, nb);
-    else observe_stride_b<false, false, ACT, 2>(T.x, T.n, a, lb, nb);
+    if (T.u == 8) observe_stride_b<false, false, ACT, 8>(T.x, T.n, a, lb, nb, L);
+    else if (T.u == 4) observe_stride_b<false, false, ACT, 4>(T.x, T.n, a, lb, nb, L);
+    else observe_stride_b<false, false, ACT, 2>(T.x, T.n, a, lb, nb, L);
   }
   store_part_record(a, T.parts, lb, nb, T.n);
 }
@@ -658,17 +663,17 @@ __global__ __launch_bounds__(kBlock) void k_selftest_fq(int mode, const float *_
 template <int ACT, bool VEC, bool NT, int G>
 void launch_observe_g(const float *x, int64_t n, double *stats_out, float *run_minmax, double *qp_out,
                       int sym, double qden, double eps, double *ws, uint32_t *counter, int64_t grid,
-                      hipStream_t st) {
+                      const SiluLay &L, hipStream_t st) {
   hipLaunchKernelGGL((k_observe<VEC, NT, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n,
-                     stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+                     stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, L);
 }
 
 template <int ACT, bool VEC, bool NT>
 void launch_observe_loop(const float *x, int64_t n, double *stats_out, float *run_minmax, double *qp_out,
                          int sym, double qden, double eps, double *ws, uint32_t *counter, int64_t grid,
-                         hipStream_t st) {
+                         const SiluLay &L, hipStream_t st) {
   hipLaunchKernelGGL((k_observe_loop<VEC, NT, ACT, kObsU>), dim3((unsigned)grid), dim3(kBlock), 0, st, x,
-                     n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter);
+                     n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, L);
 }
 
 // K2 grid: grid-stride kernel (default) or the one-shot kernel (VSIQ_TUNE_OBS_KERNEL 1)
@@ -694,13 +699,13 @@ inline int64_t observe_grid(int64_t ng) {
 template <int ACT>
 void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_out, float *run_minmax,
                     double *qp_out, int sym, double qden, double eps, double *ws, uint32_t *counter,
-                    hipStream_t st) {
+                    const SiluLay &L, hipStream_t st) {
   const int64_t ng = cdiv(n, 4);
   const int64_t grid = observe_grid(ng);
   if (g_tune.obs_kernel != 1) {
-    if (vec && nt) launch_observe_loop<ACT, true, true>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
-    else if (vec) launch_observe_loop<ACT, true, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
-    else launch_observe_loop<ACT, false, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, st);
+    if (vec && nt) launch_observe_loop<ACT, true, true>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, L, st);
+    else if (vec) launch_observe_loop<ACT, true, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, L, st);
+    else launch_observe_loop<ACT, false, false>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, ws, counter, grid, L, st);
     return;
   }
   // one-shot: K4's groups-per-lane rule (8 -> 4) and grid
@@ -708,11 +713,11 @@ void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_
 #define VSIQ_OBS(V, N)                                                                              \
   (per_lane == kLsqGroups                                                                           \
        ? launch_observe_g<ACT, V, N, kLsqGroups>(x, n, stats_out, run_minmax, qp_out, sym, qden, eps, \
-                                                 ws, counter, grid, st)                             \
+                                                 ws, counter, grid, L, st)                          \
    : per_lane == 4 ? launch_observe_g<ACT, V, N, 4>(x, n, stats_out, run_minmax, qp_out, sym, qden,  \
-                                                    eps, ws, counter, grid, st)                     \
+                                                    eps, ws, counter, grid, L, st)                  \
                    : launch_observe_g<ACT, V, N, 2>(x, n, stats_out, run_minmax, qp_out, sym, qden,  \
-                                                    eps, ws, counter, grid, st))
+                                                    eps, ws, counter, grid, L, st))
   if (vec && nt) VSIQ_OBS(true, true);
   else if (vec) VSIQ_OBS(true, false);
   else VSIQ_OBS(false, false);
@@ -722,13 +727,13 @@ void launch_observe(bool vec, bool nt, const float *x, int64_t n, double *stats_
 int observe(const float *x, int64_t n, int act, double *stats_out, float *run_minmax, double *qp_out,
             int symmetric, double qden, double eps, double *ws, int64_t ws_len, uint32_t *counter,
             void *stream) {
-  if (n <= 0 || !x || !ws || !counter) return VSIQ_E_ARG;
+  if (n <= 0 || !x || !ws || !counter || !act_ok(act)) return VSIQ_E_ARG;
   const bool vec = aligned16(x) && n % 4 == 0;
   const int64_t grid = observe_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
   VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
-           symmetric, qden, eps, ws, counter, (hipStream_t)stream);
+           symmetric, qden, eps, ws, counter, act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
 
@@ -760,22 +765,22 @@ inline int64_t observe_part_grid(int64_t n) {
 
 template <int ACT, int U>
 void launch_observe_part_u(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
-                           hipStream_t st) {
+                           const SiluLay &L, hipStream_t st) {
   if (vec && nt)
-    hipLaunchKernelGGL((k_observe_part<true, true, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+    hipLaunchKernelGGL((k_observe_part<true, true, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts, L);
   else if (vec)
-    hipLaunchKernelGGL((k_observe_part<true, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+    hipLaunchKernelGGL((k_observe_part<true, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts, L);
   else
-    hipLaunchKernelGGL((k_observe_part<false, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts);
+    hipLaunchKernelGGL((k_observe_part<false, false, ACT, U>), dim3((unsigned)grid), dim3(kBlock), 0, st, x, n, parts, L);
 }
 
 template <int ACT>
 void launch_observe_part(bool vec, bool nt, const float *x, int64_t n, double *parts, int64_t grid,
-                         hipStream_t st) {
+                         const SiluLay &L, hipStream_t st) {
   const int u = observe_part_u(n);
-  if (u == 8) launch_observe_part_u<ACT, 8>(vec, nt, x, n, parts, grid, st);
-  else if (u == 4) launch_observe_part_u<ACT, 4>(vec, nt, x, n, parts, grid, st);
-  else launch_observe_part_u<ACT, 2>(vec, nt, x, n, parts, grid, st);
+  if (u == 8) launch_observe_part_u<ACT, 8>(vec, nt, x, n, parts, grid, L, st);
+  else if (u == 4) launch_observe_part_u<ACT, 4>(vec, nt, x, n, parts, grid, L, st);
+  else launch_observe_part_u<ACT, 2>(vec, nt, x, n, parts, grid, L, st);
 }
 
 // CU count of the current device (cached; 256 on MI355X)
@@ -915,7 +920,7 @@ int vsiq_observe_f32(const float *x, int64_t n, double *stats_out, float *run_mi
 int vsiq_act_observe_f32(const float *c, int64_t n, int act, double *stats_out, float *run_minmax,
                          double *qp_out, int symmetric, double qden, double eps, double *ws,
                          int64_t ws_len, uint32_t *counter, void *stream) {
-  if (act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  if (!act_ok(act)) return VSIQ_E_ARG;
   return observe(c, n, act, stats_out, run_minmax, qp_out, symmetric, qden, eps, ws, ws_len, counter,
                  stream);
 }
@@ -927,16 +932,17 @@ int64_t vsiq_observe_part_records(int64_t n) {
 
 int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
                               void *stream) {
-  if (n <= 0 || !c || !parts || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  if (n <= 0 || !c || !parts || !act_ok(act)) return VSIQ_E_ARG;
   const int64_t grid = observe_part_grid(n);
   if (parts_len < grid * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
   const bool vec = aligned16(c) && n % 4 == 0;
-  VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, (hipStream_t)stream);
+  VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, act_lay(act, n),
+           (hipStream_t)stream);
   return launch_rc();
 }
 
 int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, int act, void *stream) {
-  if (count < 0 || (count > 0 && !tensors) || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  if (count < 0 || (count > 0 && !tensors) || !act_ok(act)) return VSIQ_E_ARG;
   for (int i = 0; i < count; ++i) {
     const vsiq_part_tensor &T = tensors[i];
     if (T.n <= 0 || !T.c || !T.parts) return VSIQ_E_ARG;
@@ -946,6 +952,7 @@ int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, 
   for (int i0 = 0; i0 < count; i0 += kPartMulti) {
     PBatch b{};
     b.count = std::min(kPartMulti, count - i0);
+    b.sref = act_ref(act);
     uint32_t blk = 0;
     for (int k = 0; k < b.count; ++k) {
       const vsiq_part_tensor &T = tensors[i0 + k];
@@ -968,8 +975,8 @@ int vsiq_act_observe_part_multi_f32(const vsiq_part_tensor *tensors, int count, 
   else if (nt) hipLaunchKernelGGL((k_observe_part_multi<true, A, false>), dim3(blk), dim3(kBlock), 0, st, b);    \
   else if (allvec) hipLaunchKernelGGL((k_observe_part_multi<false, A, true>), dim3(blk), dim3(kBlock), 0, st, b); \
   else hipLaunchKernelGGL((k_observe_part_multi<false, A, false>), dim3(blk), dim3(kBlock), 0, st, b);
-    if (act == kActRelu) { K2M(kActRelu) }
-    else if (act == kActSilu) { K2M(kActSilu) }
+    if (act_kind(act) == kActRelu) { K2M(kActRelu) }
+    else if (act_kind(act) == kActSilu) { K2M(kActSilu) }
     else { K2M(kActNone) }
 #undef K2M
     const int rc = launch_rc();
@@ -986,25 +993,27 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
                                   double *stats_out, float *run_minmax, double *qp_out, int symmetric,
                                   double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
                                   void *stream) {
-  if (n <= 0 || n > kFoldFqMax || !c || !y || !ws || qmin > qmax || act < kActNone || act > kActSilu)
+  if (n <= 0 || n > kFoldFqMax || !c || !y || !ws || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   if (ws_len < fold_fq_part_grid(n) * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
   const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
   VSIQ_ACT(act, launch_fold_fq_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, ws,
-           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, (hipStream_t)stream);
+           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, act_lay(act, n),
+           (hipStream_t)stream);
   return launch_rc();
 }
 
 int vsiq_act_observe_fq_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
                             double *stats_out, float *run_minmax, double *qp_out, int symmetric, double qden,
                             double eps, int qmin, int qmax, void *stream) {
-  if (n <= 0 || n > kSmallMax || !c || !y || qmin > qmax || act < kActNone || act > kActSilu)
+  if (n <= 0 || n > kSmallMax || !c || !y || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
   const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
   VSIQ_ACT(act, launch_observe_fq_small_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n,
-           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, (hipStream_t)stream);
+           stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, act_lay(act, n),
+           (hipStream_t)stream);
   return launch_rc();
 }
 

@@ -9,17 +9,17 @@ template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U>
 __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, float *__restrict__ y,
                                                    uint8_t *__restrict__ codes,
                                                    uint64_t *__restrict__ mask, int64_t n,
-                                                   QPSrc src, uint32_t gate) {
+                                                   QPSrc src, uint32_t gate, SiluLay L) {
   const GateClk gc = gate_begin(gate);
   const QP p = load_qp(src);
-  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, gc, gate);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, gc, gate, L);
 }
 
 // One-round grids of 9 groups per lane with the store gate where that applies
 // (store_gate_select: >= 2 workgroups per CU, all resident), else kFlatU groups per lane.
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
 void launch_fq_k(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
-                 const QPSrc &src, hipStream_t st) {
+                 const QPSrc &src, const SiluLay &L, hipStream_t st) {
   const int64_t ng = cdiv(n, 4);
   const int64_t grid9 = cdiv(ng, (int64_t)kBlock * 9);
   GateSel gs;
@@ -30,35 +30,35 @@ void launch_fq_k(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64
   }
   if (gs.gate)
     hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), dim3((unsigned)grid9), dim3(kBlock), 0, st,
-                       x, y, codes, mask, n, src, gs.gate);
+                       x, y, codes, mask, n, src, gs.gate, L);
   else
     hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>), dim3((unsigned)oneshot_grid(ng)),
-                       dim3(kBlock), 0, st, x, y, codes, mask, n, src, 0u);
+                       dim3(kBlock), 0, st, x, y, codes, mask, n, src, 0u, L);
   store_gate_launched(gs, st);   // a tuning sample of "no gate" times the kFlatU grid
 }
 
 template <int ACT, bool VEC, bool NT>
 void launch_fq_act(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
-                   const QPSrc &src, hipStream_t st) {
-  if (codes && mask) launch_fq_k<VEC, NT, true, true, ACT>(x, y, codes, mask, n, src, st);
-  else if (codes) launch_fq_k<VEC, NT, true, false, ACT>(x, y, codes, mask, n, src, st);
-  else if (mask) launch_fq_k<VEC, NT, false, true, ACT>(x, y, codes, mask, n, src, st);
-  else launch_fq_k<VEC, NT, false, false, ACT>(x, y, codes, mask, n, src, st);
+                   const QPSrc &src, const SiluLay &L, hipStream_t st) {
+  if (codes && mask) launch_fq_k<VEC, NT, true, true, ACT>(x, y, codes, mask, n, src, L, st);
+  else if (codes) launch_fq_k<VEC, NT, true, false, ACT>(x, y, codes, mask, n, src, L, st);
+  else if (mask) launch_fq_k<VEC, NT, false, true, ACT>(x, y, codes, mask, n, src, L, st);
+  else launch_fq_k<VEC, NT, false, false, ACT>(x, y, codes, mask, n, src, L, st);
 }
 
 template <int ACT>
 void launch_fq(bool vec, bool nt, const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
-               const QPSrc &src, hipStream_t st) {
-  if (vec && nt) launch_fq_act<ACT, true, true>(x, y, codes, mask, n, src, st);
-  else if (vec) launch_fq_act<ACT, true, false>(x, y, codes, mask, n, src, st);
-  else if (nt) launch_fq_act<ACT, false, true>(x, y, codes, mask, n, src, st);
-  else launch_fq_act<ACT, false, false>(x, y, codes, mask, n, src, st);
+               const QPSrc &src, const SiluLay &L, hipStream_t st) {
+  if (vec && nt) launch_fq_act<ACT, true, true>(x, y, codes, mask, n, src, L, st);
+  else if (vec) launch_fq_act<ACT, true, false>(x, y, codes, mask, n, src, L, st);
+  else if (nt) launch_fq_act<ACT, false, true>(x, y, codes, mask, n, src, L, st);
+  else launch_fq_act<ACT, false, false>(x, y, codes, mask, n, src, L, st);
 }
 
 int fq_fwd(const float *x, float *y, void *codes, uint64_t *mask, int64_t n, int act,
            const double *qp_dev, const double *scale_dev, double scale_host, const double *zp_dev,
            double zp_host, int zp_round, int discrete, int qmin, int qmax, void *stream) {
-  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y)) || act < kActNone || act > kActSilu)
+  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y)) || !act_ok(act))
     return VSIQ_E_ARG;
   if (n == 0) return 0;
   if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
@@ -68,7 +68,7 @@ int fq_fwd(const float *x, float *y, void *codes, uint64_t *mask, int64_t n, int
   const bool vec = (n % 4 == 0) && aligned16(x) && aligned16(y) && (!codes || aligned4(codes));
   const bool nt = g_tune.nontemporal != 0;
   uint8_t *c = (uint8_t *)codes;
-  VSIQ_ACT(act, launch_fq, vec, nt, x, y, c, mask, n, src, st);
+  VSIQ_ACT(act, launch_fq, vec, nt, x, y, c, mask, n, src, act_lay(act, n), st);
   return launch_rc();
 }
 

@@ -11,15 +11,14 @@ template <bool VEC, bool NT, bool ZPL, int ACT, int G, bool PART = false>
 __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ x,
                                                     float *__restrict__ gx, int64_t n,
-                                                    QPSrc src, double gscale, int prefetch,
+                                                    QPSrc src, double gscale, SiluLay L,
                                                     double *__restrict__ grad_out,
                                                     double *__restrict__ ws,
                                                     uint32_t *__restrict__ counter) {
   const QP p = load_qp(src);
   LsqAcc c{0.0, 0.0};
-  (void)prefetch;
   f4 o[G];
-  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o);
+  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o, L);
   double rec[2], f[2];
   if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
   if (PART) {
@@ -49,56 +48,54 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
 template <int ACT, bool VEC, bool NT, int G>
 void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
                   double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
-                  hipStream_t st) {
-  const int pf = 0;
+                  const SiluLay &L, hipStream_t st) {
   if (!counter) {   // records only (PART)
     if (zpl)
       hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT, G, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g,
-                         x, gx, n, src, gscale, pf, grad_out, ws, counter);
+                         x, gx, n, src, gscale, L, grad_out, ws, counter);
     else
       hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT, G, true>), dim3((unsigned)grid), dim3(kBlock), 0, st, g,
-                         x, gx, n, src, gscale, pf, grad_out, ws, counter);
+                         x, gx, n, src, gscale, L, grad_out, ws, counter);
     return;
   }
   if (zpl)
     hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, true, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
-                       gx, n, src, gscale, pf, grad_out, ws, counter);
+                       gx, n, src, gscale, L, grad_out, ws, counter);
   else
     hipLaunchKernelGGL((k_lsq_bwd<VEC, NT, false, ACT, G>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x,
-                       gx, n, src, gscale, pf, grad_out, ws, counter);
+                       gx, n, src, gscale, L, grad_out, ws, counter);
 }
 
 template <int ACT, bool VEC, bool NT>
 void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
                     double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
-                    hipStream_t st) {
+                    const SiluLay &L, hipStream_t st) {
   const int per_lane = lsq_groups_per_lane(cdiv(n, 4));
   if (per_lane == kLsqGroups)
-    launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+    launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 8)
-    launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+    launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 4)
-    launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+    launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else
-    launch_lsq_g<ACT, VEC, NT, 2>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+    launch_lsq_g<ACT, VEC, NT, 2>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
 }
 
 template <int ACT>
 void launch_lsq(bool vec, bool nt, const float *g, const float *x, float *gx, int64_t n,
                 const QPSrc &src, int zpl, double gscale, double *grad_out, double *ws,
-                uint32_t *counter, int64_t grid, hipStream_t st) {
-  if (vec && nt) launch_lsq_act<ACT, true, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
-  else if (vec) launch_lsq_act<ACT, true, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
-  else if (nt) launch_lsq_act<ACT, false, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
-  else launch_lsq_act<ACT, false, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, st);
+                uint32_t *counter, int64_t grid, const SiluLay &L, hipStream_t st) {
+  if (vec && nt) launch_lsq_act<ACT, true, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
+  else if (vec) launch_lsq_act<ACT, true, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
+  else if (nt) launch_lsq_act<ACT, false, true>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
+  else launch_lsq_act<ACT, false, false>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
 }
 
 int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const double *scale_dev,
             double scale_host, const double *zp_dev, double zp_host, int zp_learn, int qmin, int qmax,
             double gscale, double *grad_out, double *ws, int64_t ws_len, uint32_t *counter,
             void *stream) {
-  if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax || act < kActNone ||
-      act > kActSilu)
+  if (n <= 0 || !g || !x || !gx || !grad_out || !ws || !counter || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
   const int64_t grid = lsq_grid(cdiv(n, 4));
@@ -108,7 +105,7 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
   const bool nt = g_tune.nontemporal != 0;
   VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
-           (hipStream_t)stream);
+           act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
 
@@ -116,7 +113,7 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
 int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, const double *scale_dev,
                  double scale_host, const double *zp_dev, double zp_host, int zp_learn, int qmin, int qmax,
                  double *records, int64_t records_len, void *stream) {
-  if (n <= 0 || !g || !x || !gx || !records || qmin > qmax || act < kActNone || act > kActSilu)
+  if (n <= 0 || !g || !x || !gx || !records || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
   const int64_t grid = lsq_grid(cdiv(n, 4));
@@ -125,7 +122,7 @@ int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, 
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
   const bool nt = g_tune.nontemporal != 0;
   VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, 0.0, nullptr, records, nullptr, grid,
-           (hipStream_t)stream);
+           act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
 

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ pre,
                                                     float *__restrict__ gx, int64_t rowlen,
                                                     uint32_t chunks, const double *__restrict__ sdev,
-                                                    double shost, uint32_t defer, uint32_t gate) {
+                                                    double shost, uint32_t defer, uint32_t gate, SiluLay L) {
   const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
       o[u].z = ste_ieee(v[u].z, m2, d);
       o[u].w = ste_ieee(v[u].w, m3, d);
     }
-    if (ACT) o[u] = act_bwd4<ACT>(o[u], cv[u]);
+    if (ACT) o[u] = act_bwd4_at<ACT>(o[u], cv[u], row * rowlen + 4 * (base + u * kBlock), L);
   }
   if (defer) {   // kernel-uniform
     __syncthreads();
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kBlock) void k_ste_bwd(const float *__restrict__ g,
 
 template <int ACT, bool VEC, bool NT>
 void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *gx, int64_t rows,
-                    int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
+                    int64_t rowlen, const double *sdev, double shost, const SiluLay &L, hipStream_t st) {
   const int64_t ng = cdiv(rowlen, 4);
   const int64_t chunks9 = cdiv(ng, (int64_t)kBlock * 9);
   const bool fits9 = chunks9 * kBlock * 9 - ng <= ng / 8;
@@ -97,27 +97,27 @@ void launch_ste_act(const float *g, const uint64_t *m, const float *pre, float *
   const uint32_t defer = fits9 && !gs.gate ? store_defer_units(rows * chunks9, true) : 0;
   if (defer || gs.gate) {
     hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, 9>), dim3((unsigned)(rows * chunks9)), dim3(kBlock), 0, st,
-                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer, gs.gate);
+                       g, m, pre, gx, rowlen, (uint32_t)chunks9, sdev, shost, defer, gs.gate, L);
   } else {
     const int64_t chunks = oneshot_grid(ng);
     hipLaunchKernelGGL((k_ste_bwd<VEC, NT, ACT, kFlatU>), dim3((unsigned)(rows * chunks)), dim3(kBlock), 0,
-                       st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u, 0u);
+                       st, g, m, pre, gx, rowlen, (uint32_t)chunks, sdev, shost, 0u, 0u, L);
   }
   store_gate_launched(gs, st);
 }
 
 template <int ACT>
 void launch_ste(bool vec, bool nt, const float *g, const uint64_t *m, const float *pre, float *gx,
-                int64_t rows, int64_t rowlen, const double *sdev, double shost, hipStream_t st) {
-  if (vec && nt) launch_ste_act<ACT, true, true>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
-  else if (vec) launch_ste_act<ACT, true, false>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
-  else if (nt) launch_ste_act<ACT, false, true>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
-  else launch_ste_act<ACT, false, false>(g, m, pre, gx, rows, rowlen, sdev, shost, st);
+                int64_t rows, int64_t rowlen, const double *sdev, double shost, const SiluLay &L, hipStream_t st) {
+  if (vec && nt) launch_ste_act<ACT, true, true>(g, m, pre, gx, rows, rowlen, sdev, shost, L, st);
+  else if (vec) launch_ste_act<ACT, true, false>(g, m, pre, gx, rows, rowlen, sdev, shost, L, st);
+  else if (nt) launch_ste_act<ACT, false, true>(g, m, pre, gx, rows, rowlen, sdev, shost, L, st);
+  else launch_ste_act<ACT, false, false>(g, m, pre, gx, rows, rowlen, sdev, shost, L, st);
 }
 
 int ste_bwd(const float *g, const uint64_t *mask, const float *pre, float *gx, int64_t n, int act,
             const double *scale_dev, int64_t rowlen, double scale_host, void *stream) {
-  if (n < 0 || act < kActNone || act > kActSilu) return VSIQ_E_ARG;
+  if (n < 0 || !act_ok(act)) return VSIQ_E_ARG;
   if (n == 0) return 0;
   if (!g || !mask || !gx || (act != kActNone && !pre)) return VSIQ_E_ARG;
   if (!aligned8(mask)) return VSIQ_E_ALIGN;
@@ -128,7 +128,7 @@ int ste_bwd(const float *g, const uint64_t *mask, const float *pre, float *gx, i
   const bool vec = (rowlen % 4 == 0) && aligned16(g) && aligned16(gx) && (!pre || aligned16(pre));
   const bool nt = g_tune.nontemporal != 0;
   VSIQ_ACT(act, launch_ste, vec, nt, g, mask, pre, gx, rows, rowlen, scale_dev, scale_host,
-           (hipStream_t)stream);
+           act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
 

@@ -334,17 +334,161 @@ __device__ __forceinline__ float ste_ieee(float g, bool m, const SteDiv &d) {
 // applies the activation's backward to the quantizer's grad_x.
 //   relu:  c < 0 ? 0 : c          (torch CPU: relu(-0.0) = -0.0, relu(NaN) = NaN)
 //          bwd: threshold_backward(g, relu(c), 0) = c <= 0 ? 0 : g  (NaN passes g)
-//   silu:  c / (1 + exp(-c))      (torch CPU silu_kernel)
-//          bwd: (g * sig) * fma(c, 1 - sig, 1),  sig = 1 / (1 + exp(-c))  (torch's
-//          vectorized CPU kernel contracts the inner multiply-add); exp differs from
-//          torch's Sleef exp by about an ulp, so SiLU is within a few ulp, not bitwise
+//   silu:  bit for bit what torch's CPU silu_kernel computes (the reference runs F.silu
+//          on CPU tensors): see "SiLU as torch's CPU kernel computes it" below.
 // ----------------------------------------------------------------------------
 enum { kActNone = 0, kActRelu = 1, kActSilu = 2 };
+
+// ----------------------------------------------------------------------------
+// SiLU as torch's CPU kernel computes it (aten/src/ATen/native/cpu/Activation.cpp,
+// silu_kernel / silu_backward_kernel under cpu_kernel_vec):
+//   vectorized loop (2 vectors per step):  c / (1 + Sleef_expf_u10(-c))
+//   scalar remainder of each chunk:        c / (1 + expf(-c))          (glibc libm)
+//   backward, same split:  (g * sig) * fma(c, 1 - sig, 1),  sig = 1 / (1 + exp(-c))
+// The two exps differ in the last bit for ~3.5 % of activation-range inputs, so which
+// elements take the scalar path matters: TensorIterator runs serially below
+// GRAIN_SIZE = 32768 elements (or on one thread), else at::parallel_for splits [0, n)
+// into nt = min(threads, ceil(n / 32768)) chunks of ceil(n / nt); every chunk runs the
+// vector loop over its first len - len % W elements (W = 2 x the vector width: 32 on
+// AVX-512, 16 on AVX2) and the scalar code over the rest.  SiluRef {W, threads}
+// travels in the act argument (VSIQ_ACT_SILU_REF, include/vsiq.h); W = 0 = every
+// element on the vector path.  Both exps are ported op for op below and were checked
+// against the reference host for all 2^32 inputs (tests/test_silu_oracle.py pins the
+// oracle restatement, oracle/silu_ref.c, against torch's CPU kernel).
+// ----------------------------------------------------------------------------
+struct SiluRef {
+  int32_t w, t;   // 2 x vector width (0: vector path only), reference thread count
+};
+struct SiluLay {          // chunk layout of one tensor of n elements (silu_lay)
+  int64_t chunk, last;    // chunk length; start of the last chunk
+  int64_t thr, thr_last;  // first scalar offset inside a chunk / inside the last chunk
+  double inv;             // RN(1 / chunk)
+  int32_t on;             // 0: no element of this tensor takes the scalar path
+};
+
+constexpr int64_t kTorchGrain = 32768;   // at::internal::GRAIN_SIZE
+
+__host__ __device__ inline SiluLay silu_lay(int64_t n, SiluRef r) {
+  SiluLay L{};
+  if (r.w <= 0 || n <= 0) return L;
+  int64_t nt = 1;
+  if (n >= kTorchGrain && r.t > 1) {
+    nt = (n + kTorchGrain - 1) / kTorchGrain;
+    if (nt > r.t) nt = r.t;
+  }
+  L.chunk = (n + nt - 1) / nt;
+  L.last = ((n + L.chunk - 1) / L.chunk - 1) * L.chunk;
+  L.thr = L.chunk - L.chunk % r.w;
+  L.thr_last = (n - L.last) - (n - L.last) % r.w;
+  L.inv = 1.0 / (double)L.chunk;
+  L.on = (L.thr != L.chunk || L.thr_last != n - L.last) ? 1 : 0;
+  return L;
+}
+
+// bit j set: element e0 + j takes torch's scalar path (elements past n: don't care)
+__host__ __device__ inline uint32_t silu_scalar4(int64_t e0, const SiluLay &L) {
+  int64_t cs = L.last;
+  if (e0 < L.last) {
+    cs = (int64_t)((double)e0 * L.inv) * L.chunk;   // off by at most one chunk
+    if (cs > e0) cs -= L.chunk;
+    else if (cs + L.chunk <= e0) cs += L.chunk;
+  }
+  uint32_t m = 0;
+  for (int j = 0; j < 4; ++j) {
+    const int64_t e = e0 + j;
+    const int64_t c = (e - cs >= L.chunk && cs < L.last) ? cs + L.chunk : cs;
+    m |= (uint32_t)(e - c >= (c == L.last ? L.thr_last : L.thr)) << j;
+  }
+  return m;
+}
+
+__host__ __device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+__host__ __device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// Sleef_expf16_u10 (sleefsimdsp.c xexpf, FMA build), op for op
+__host__ __device__ __forceinline__ float sleef_expf_u10(float d) {
+  const float qf = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+  const int q = (int)__builtin_fminf(__builtin_fmaxf(qf, -256.0f), 256.0f);   // |d| > 104: replaced below
+  float s = __builtin_fmaf((float)q, -0.693145751953125f, d);
+  s = __builtin_fmaf((float)q, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+  u = __builtin_fmaf(u, s, 0.5f);
+  u = 1.0f + __builtin_fmaf(s * s, u, s);
+  const int h = q >> 1;   // vldexp2: two exact power-of-two steps
+  u = (u * u2f((uint32_t)(h + 0x7f) << 23)) * u2f((uint32_t)(q - h + 0x7f) << 23);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = __builtin_inff();
+  return d != d ? d : u;
+}
+
+// 2^(i/32) - (i << 47) as doubles' bits (glibc's __exp2f_data.tab)
+#define VSIQ_EXP2F_TAB \
+  0x3ff0000000000000ULL, 0x3fefd9b0d3158574ULL, 0x3fefb5586cf9890fULL, 0x3fef9301d0125b51ULL, \
+  0x3fef72b83c7d517bULL, 0x3fef54873168b9aaULL, 0x3fef387a6e756238ULL, 0x3fef1e9df51fdee1ULL, \
+  0x3fef06fe0a31b715ULL, 0x3feef1a7373aa9cbULL, 0x3feedea64c123422ULL, 0x3feece086061892dULL, \
+  0x3feebfdad5362a27ULL, 0x3feeb42b569d4f82ULL, 0x3feeab07dd485429ULL, 0x3feea47eb03a5585ULL, \
+  0x3feea09e667f3bcdULL, 0x3fee9f75e8ec5f74ULL, 0x3feea11473eb0187ULL, 0x3feea589994cce13ULL, \
+  0x3feeace5422aa0dbULL, 0x3feeb737b0cdc5e5ULL, 0x3feec49182a3f090ULL, 0x3feed503b23e255dULL, \
+  0x3feee89f995ad3adULL, 0x3feeff76f2fb5e47ULL, 0x3fef199bdd85529cULL, 0x3fef3720dcef9069ULL, \
+  0x3fef5818dcfba487ULL, 0x3fef7c97337b9b5fULL, 0x3fefa4afa2a490daULL, 0x3fefd0765b6e4540ULL \
+
+static __constant__ uint64_t kExp2fTabDev[32] = {VSIQ_EXP2F_TAB};
+static const uint64_t kExp2fTabHost[32] = {VSIQ_EXP2F_TAB};
+
+// glibc expf (sysdeps/ieee754/flt-32/e_expf.c, the FMA ifunc variant), op for op:
+// 2^(k/32) from a 32-entry table times a cubic in r, in double
+__host__ __device__ inline float glibc_expf(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const uint64_t *kT = kExp2fTabDev;
+#else
+  const uint64_t *kT = kExp2fTabHost;
+#endif
+  const uint32_t ux = f2u(x), abstop = (ux >> 20) & 0x7ffu;
+  if (abstop >= 0x42bu) {   // |x| >= 88 or NaN
+    if (ux == 0xff800000u) return 0.0f;
+    if (abstop >= 0x7f8u) return x + x;
+    if (x > 0x1.62e42ep6f) return __builtin_inff();
+    if (x < -0x1.9fe368p6f) return 0.0f;
+  }
+  const double InvLn2N = 0x1.71547652b82fep+0 * 32.0, Shift = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / 32768.0, C1 = 0x1.ebfce50fac4f3p-3 / 1024.0,
+               C2 = 0x1.62e42ff0c52d6p-1 / 32.0;
+  const double xd = (double)x;
+  const double kd0 = __builtin_fma(InvLn2N, xd, Shift);
+  const uint64_t ki = __builtin_bit_cast(uint64_t, kd0);
+  const double kd = kd0 - Shift;
+  const double r = __builtin_fma(InvLn2N, xd, -kd);
+  const double s = __builtin_bit_cast(double, kT[ki % 32] + (ki << 47));
+  const double z = __builtin_fma(C0, r, C1);
+  double y = __builtin_fma(C2, r, 1.0);
+  y = __builtin_fma(z, r * r, y);
+  return (float)(y * s);
+}
+
+template <bool SCALAR>
+__host__ __device__ __forceinline__ float silu_exp(float c) {
+  return SCALAR ? glibc_expf(-c) : sleef_expf_u10(-c);
+}
+
+template <bool SCALAR>
+__host__ __device__ __forceinline__ float silu_fwd(float c) {
+  return c / (1.0f + silu_exp<SCALAR>(c));
+}
+
+template <bool SCALAR>
+__host__ __device__ __forceinline__ float silu_bwd(float g, float c) {
+  const float sig = 1.0f / (1.0f + silu_exp<SCALAR>(c));
+  return (g * sig) * __builtin_fmaf(c, 1.0f - sig, 1.0f);
+}
 
 template <int ACT>
 __device__ __forceinline__ float act_fwd(float c) {
   if (ACT == kActRelu) return c < 0.0f ? 0.0f : c;
-  if (ACT == kActSilu) return c / (1.0f + __builtin_expf(-c));
+  if (ACT == kActSilu) return silu_fwd<false>(c);
   return c;
 }
 
@@ -356,13 +500,29 @@ __device__ __forceinline__ f4 act_fwd4(f4 v) {
   return o;
 }
 
+// act of the group whose first element is e0: SiLU elements on torch's scalar path
+// take glibc's exp (rare: at most W - 1 elements per chunk; divergent)
+template <int ACT>
+__device__ __forceinline__ f4 act_fwd4_at(f4 v, int64_t e0, const SiluLay &L) {
+  f4 o = act_fwd4<ACT>(v);
+  if constexpr (ACT == kActSilu) {
+    if (L.on) {
+      const uint32_t sm = silu_scalar4(e0, L);
+      if (sm) {
+        if (sm & 1u) o.x = silu_fwd<true>(v.x);
+        if (sm & 2u) o.y = silu_fwd<true>(v.y);
+        if (sm & 4u) o.z = silu_fwd<true>(v.z);
+        if (sm & 8u) o.w = silu_fwd<true>(v.w);
+      }
+    }
+  }
+  return o;
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_bwd(float g, float c) {
   if (ACT == kActRelu) return c <= 0.0f ? 0.0f : g;
-  if (ACT == kActSilu) {
-    const float sig = 1.0f / (1.0f + __builtin_expf(-c));
-    return (g * sig) * __builtin_fmaf(c, 1.0f - sig, 1.0f);
-  }
+  if (ACT == kActSilu) return silu_bwd<false>(g, c);
   return g;
 }
 
@@ -375,10 +535,42 @@ __device__ __forceinline__ f4 act_bwd4(f4 g, f4 c) {
   return o;
 }
 
-// runtime act -> template dispatch
-#define VSIQ_ACT(ACTV, F, ...)                                   \
-  ((ACTV) == kActRelu ? F<kActRelu>(__VA_ARGS__)                 \
-                      : (ACTV) == kActSilu ? F<kActSilu>(__VA_ARGS__) : F<kActNone>(__VA_ARGS__))
+template <int ACT>
+__device__ __forceinline__ f4 act_bwd4_at(f4 g, f4 c, int64_t e0, const SiluLay &L) {
+  f4 o = act_bwd4<ACT>(g, c);
+  if constexpr (ACT == kActSilu) {
+    if (L.on) {
+      const uint32_t sm = silu_scalar4(e0, L);
+      if (sm) {
+        if (sm & 1u) o.x = silu_bwd<true>(g.x, c.x);
+        if (sm & 2u) o.y = silu_bwd<true>(g.y, c.y);
+        if (sm & 4u) o.z = silu_bwd<true>(g.z, c.z);
+        if (sm & 8u) o.w = silu_bwd<true>(g.w, c.w);
+      }
+    }
+  }
+  return o;
+}
+
+// The act argument of the C ABI: VSIQ_ACT_NONE / _RELU / _SILU in the low byte; for
+// SiLU, bits 8-15 = W and bits 16-30 = the reference thread count (VSIQ_ACT_SILU_REF)
+__host__ __device__ inline int act_kind(int act) { return act & 0xff; }
+inline SiluRef act_ref(int act) { return SiluRef{(act >> 8) & 0xff, (act >> 16) & 0x7fff}; }
+inline bool act_ok(int act) {
+  const int k = act_kind(act);
+  if (act < 0 || k < kActNone || k > kActSilu) return false;
+  if (k != kActSilu) return (act >> 8) == 0;
+  const int w = (act >> 8) & 0xff;
+  return w == 0 || w == 8 || w == 16 || w == 32 || w == 64;
+}
+inline SiluLay act_lay(int act, int64_t n) {
+  return act_kind(act) == kActSilu ? silu_lay(n, act_ref(act)) : SiluLay{};
+}
+
+// runtime act -> template dispatch (on the activation kind)
+#define VSIQ_ACT(ACTV, F, ...)                                                 \
+  (act_kind(ACTV) == kActRelu ? F<kActRelu>(__VA_ARGS__)                       \
+                              : act_kind(ACTV) == kActSilu ? F<kActSilu>(__VA_ARGS__) : F<kActNone>(__VA_ARGS__))
 
 // where qparams come from (one struct, passed by value -> kernarg / SGPRs)
 struct QPSrc {

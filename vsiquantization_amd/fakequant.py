@@ -115,6 +115,46 @@ def ste_backward(g: torch.Tensor, mask: torch.Tensor, scale, rowlen: int = 0, *,
     return gx
 
 
+# --------------------------------------------------------------------------- activation alone
+class ActivationFn(torch.autograd.Function):
+    """act(x) on its own (vsiq_act_fwd_f32 / vsiq_act_bwd_f32): the fused layers' F.silu
+    (modules/fused.py:133) where its output is not fake-quantized in the same pass
+    (calibration forwards), bit for bit as torch's CPU kernel computes it."""
+
+    @staticmethod
+    def forward(ctx, x, act):
+        x = H.require_device_f32(x)
+        code = H.act_code(act)
+        y = torch.empty_like(x)
+        H.check(H.lib().vsiq_act_fwd_f32(H.ptr(x), H.ptr(y), _i64(x.numel()), code, H.stream_of(x.device)),
+                "vsiq_act_fwd_f32")
+        ctx.code = code
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        g = H.require_device_f32(g, "grad_output")
+        gx = torch.empty_like(x)
+        H.check(H.lib().vsiq_act_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(x.numel()), ctx.code,
+                                         H.stream_of(x.device)), "vsiq_act_bwd_f32")
+        return gx, None
+
+
+def activation(x, act):
+    """The fused layers' F.relu / F.silu (modules/fused.py:133) as the reference computes
+    them: SiLU of a CUDA fp32 tensor through ActivationFn (torch's HIP silu uses another
+    exp); ReLU through torch (bitwise equal to its CPU kernel); anything else is torch's."""
+    if act == "relu":
+        return torch.nn.functional.relu(x)
+    if act == "silu":
+        if isinstance(x, torch.Tensor) and x.device.type == "cuda" and x.dtype == torch.float32:
+            return ActivationFn.apply(x, act)
+        return torch.nn.functional.silu(x)
+    raise ValueError(f"unsupported fused activation {act!r} ('relu' or 'silu')")
+
+
 class FakeQuantFixedFn(torch.autograd.Function):
     """Fixed-qparam fake quant with the reference's STE gradient (x only)."""
 

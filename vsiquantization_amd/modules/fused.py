@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..fakequant import activation
 from ..quantizers.fake_quantize import FakeQuantize
 
 
@@ -60,7 +61,7 @@ def bn_fold_device(weight, bias, bn):
 
 
 def _activation(x, is_relu):
-    return F.relu(x) if is_relu else F.silu(x)
+    return activation(x, "relu" if is_relu else "silu")   # SiLU: HIP, torch CPU's bits
 
 
 class _FusedActCore(FakeQuantize):

@@ -12,14 +12,13 @@ LSQFakeQuantize.calculate_grad_scale does (quantizers/lsq_module.py:326-330).
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from ..fakequant import PerChannelFQFn, PerChannelLearnFn, per_channel_fake_quant
+from ..fakequant import activation as _activation
 from ..utils.registry import register_class
 from .uniform import UniformQuantizer, _calib_factor
 
 
-_ACTS = {"relu": F.relu, "silu": F.silu}
 
 
 def _per_channel(v) -> bool:
@@ -34,7 +33,7 @@ class PerChannelUniformQuantizer(UniformQuantizer):
         if not (_per_channel(scale) or _per_channel(zero_point)):
             return super().quantize(x, scale, zero_point, is_learning_scale, act=act)
         if act is not None:   # per-channel activations: activation first (torch), then K3-fixed
-            x = _ACTS[act](x)
+            x = _activation(x, act)
         C = x.shape[0]
         if is_learning_scale:
             gscale = float((self.qmax * x.numel() / C) ** -0.5) * _calib_factor(self)

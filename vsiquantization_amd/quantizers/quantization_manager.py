@@ -24,10 +24,10 @@ import itertools
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import _hip as H
 from .. import observe_batch
+from ..fakequant import activation as _activation
 from ..fakequant import (observe_parts, observe_tensor, part_slot_doubles,
                          stats_from_row_sums)
 from ..observers.minmax import MinMaxObserver
@@ -36,7 +36,6 @@ from ..utils.registry import CLASS_REGISTRY
 from .per_channel import PerChannelUniformQuantizer
 
 _STAT_NAMES = ("mean_abs_x", "mean_x", "std")
-_ACTS = {"relu": F.relu, "silu": F.silu}
 
 # Calibration-time observer streams: an observe-only call (is_quantize False) has no
 # consumer until calibration ends, so its K2 pass is queued on a side stream and the
@@ -150,7 +149,7 @@ class QuantizationManager(nn.Module):
         if isinstance(x, torch.Tensor):
             self._x_device = x.device   # where this layer's tensors live (_home_device)
         if act is not None and not self._act_fusable(x):
-            x, act = _ACTS[act](x), None
+            x, act = _activation(x, act), None
         if (self.async_observer and not self.is_quantize and self._device_observer(x)
                 and not isinstance(self.observer, PerChannelMinMaxObserver)):
             # observe-only: queue on this manager's side stream, do not wait for it
@@ -249,7 +248,7 @@ class QuantizationManager(nn.Module):
         if self.is_quantize or self.is_learning_scale:
             self._join()
         if act is not None and not (self.is_quantize and self._act_fusable(x)):
-            x, act = _ACTS[act](x), None
+            x, act = _activation(x, act), None
         if act is None and (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
                 and isinstance(self.observer, PerChannelMinMaxObserver)
                 and isinstance(self.quantizer, PerChannelUniformQuantizer) and self._device_observer(x)):
