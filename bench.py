@@ -616,10 +616,11 @@ class ActQuant:
     quantizers in observe + quantize mode (calibrate, then
     activate_quantizer without learnable qparams) over a batch of 1024 images split
     across the ranks (1024/N per GPU: strong scaling).  Per layer and call: K2 observe
-    of relu(conv output) (4 B/elem) -> with N > 1 one RCCL all_gather of the 10-double
-    stats records + vsiq_observe_finalize_ranks (rank-order fold, running update, f64
-    qparams; QuantizationManager.dist_group, distributed.gather_finalize) -> K1 fused-ReLU fake quant
-    reading those qparams by pointer (8 B/elem).  Symmetric, observer 8-bit, quantizer
+    of relu(conv output) (4 B/elem) -> K1 fused-ReLU fake quant reading the qparams by
+    pointer (8 B/elem); with N > 1, between them one RCCL all_gather of the 10-double stats
+    records, folded (rank order, running update, f64 qparams) inside the fake-quant launch
+    (vsiq_act_fq_fwd_ranks_f32; QuantizationManager.dist_group,
+    distributed.observe_gather_fake_quant).  Symmetric, observer 8-bit, quantizer
     4-bit (the YAML default a4 and the observer quirk)."""
 
     key = "act"
@@ -655,34 +656,29 @@ class ActQuant:
             t["obs"] = (P["x"], n, H.ACT_RELU, P["st"], P["rmm"] if loc else None, P["qp"] if loc else None,
                         1, qd, 1e-8, P["ws"], H.c_i64(t["ws"].numel()), P["cnt"], st)
             t["gat"] = torch.empty(world * H.ST_LEN, dtype=torch.float64, device=dev)
-            t["fin"] = (H.ptr(t["gat"]), world, P["st"], P["rmm"], P["qp"], 1, qd, 1e-8, st)
             t["fq"] = (P["x"], P["y"], None, None, n, H.ACT_RELU, P["qp"], None, 0.0, None, 0.0, 0, 0,
                        self.qmin, self.qmax, st)
+            # N > 1: the gathered records folded inside the fake-quant launch (K1r)
+            t["rfq"] = (P["x"], P["y"], None, None, n, H.ACT_RELU, H.ptr(t["gat"]), world, P["st"], P["rmm"],
+                        P["qp"], 1, qd, 1e-8, self.qmin, self.qmax, st)
             self.L.append(t)
-        self.f_obs, self.f_fin, self.f_fq = (lib.vsiq_act_observe_f32, lib.vsiq_observe_finalize_ranks,
-                                             lib.vsiq_act_fq_fwd_f32)
+        self.f_obs, self.f_fq, self.f_rfq = (lib.vsiq_act_observe_f32, lib.vsiq_act_fq_fwd_f32,
+                                             lib.vsiq_act_fq_fwd_ranks_f32)
         self.n = sum(t["x"].numel() for t in self.L)
         self.slots = [None]
         self.kernels = {"observe_quant_all_layers": 12 * self.n}
-        # distributed.gather_stats with its per-call lookups (world size, backend, output
-        # views) done once: the step issues 27 of them, so at N = 8 their host cost counts
-        self.gather = None
-        if world > 1:
-            if dist.get_backend() == "gloo":   # CPU rehearsals: the list form
-                for t in self.L:
-                    t["gat_views"] = list(t["gat"].view(world, H.ST_LEN).unbind(0))
-                self.gather = lambda t: dist.all_gather(t["gat_views"], t["st"])
-            else:
-                self.gather = lambda t: dist.all_gather_into_tensor(t["gat"], t["st"])
 
     def launch(self, i):
         rc = 0
-        for t in self.L:
+        if self.world == 1:
+            for t in self.L:
+                rc |= self.f_obs(*t["obs"])
+                rc |= self.f_fq(*t["fq"])
+            return rc
+        for t in self.L:   # local K2 pass, ONE all_gather of the 10-double records, ONE fold + fq launch
             rc |= self.f_obs(*t["obs"])
-            if self.gather is not None:   # one all_gather of the 10-double records + one fold launch
-                self.gather(t)
-                rc |= self.f_fin(*t["fin"])
-            rc |= self.f_fq(*t["fq"])
+            dist.all_gather_into_tensor(t["gat"], t["st"])
+            rc |= self.f_rfq(*t["rfq"])
         return rc
 
     def launch_group(self, i0, cnt, ev):

@@ -201,6 +201,23 @@ int vsiq_observe_finalize_ranks(const double *gathered, int world, double *stats
                                 double *qp_out, int symmetric, double qden, double eps, void *stream);
 
 /*
+ * The per-call multi-GPU exchange's fold and the fake quant in ONE launch (K1r):
+ * `gathered` = the `world` ranks' stats records of this call (each from
+ * vsiq_act_observe_f32 over the rank's shard with run_minmax = qp_out = NULL; one
+ * all_gather in rank order).  Every workgroup folds them exactly as
+ * vsiq_observe_finalize_ranks does, applies the running update + f64 qparams and
+ * fake-quantizes its share of act(c) as vsiq_act_fq_fwd_f32 with those qparams;
+ * workgroup 0 writes run_minmax, qp_out and stats_out (nullable).  Bit for bit
+ * vsiq_observe_finalize_ranks followed by vsiq_act_fq_fwd_f32(qp_dev = qp_out).
+ * Replaces, per rank, minmax.py:42-74 + uniform.py:55,95 of a batch-sharded
+ * observe + quantize call (quantization_manager.py:73-90).
+ */
+int vsiq_act_fq_fwd_ranks_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                              const double *gathered, int world, double *stats_out, float *run_minmax,
+                              double *qp_out, int symmetric, double qden, double eps, int qmin, int qmax,
+                              void *stream);
+
+/*
  * Per-tensor observe + fake quant of a small tensor in ONE launch (K8): n <=
  * vsiq_observe_fq_max_elems() (65536).  Equal to vsiq_act_observe_f32(c, n, act,
  * stats_out, run_minmax, qp_out, ...) followed by vsiq_act_fq_fwd_f32(c, y, codes, mask,

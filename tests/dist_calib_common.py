@@ -28,7 +28,7 @@ class Config:
     def __init__(self, name):
         self.name = name
         if name == "small":
-            self.layers = [("relu", (8, 10, 10)), (None, (8, 10, 10)), ("relu", (8, 10, 10))]
+            self.layers = [("relu", (8, 10, 10)), (None, (8, 10, 10)), ("relu", (8, 10, 10)), ("silu", (8, 12, 10))]
             self.calls, self.batch, self.nan_at = 5, 4, (2, 1)
         elif name == "c5":
             self.layers = [("relu", (co, h, h)) for _, co, _, _, h in _backbone()]
@@ -44,7 +44,7 @@ def activations(cfg):
     out = []
     if cfg.name == "small":
         rng = np.random.default_rng(7)
-        scales = (1.0, 0.3, 4.0)
+        scales = (1.0, 0.3, 4.0, 2.0)
         for c in range(cfg.calls):
             row = []
             for li, (_, shp) in enumerate(cfg.layers):
@@ -83,6 +83,25 @@ def observe(cfg, mgrs, acts, shard=None):
             if shard is not None:
                 x = x.chunk(shard[1])[shard[0]]
             qm.quantize(x, act=act)
+
+
+def observe_quantize(cfg, mgrs, acts, shard=None):
+    """Observe + quantize mode (qm.py:73-90 with is_quantize): every call's
+    y and its straight-through gradient of a seeded upstream gradient, per (call, layer);
+    shard = (rank, world): that rank's part of each batch (and of each gradient)."""
+    out = {}
+    for c, row in enumerate(acts):
+        for li, (qm, x, (act, _)) in enumerate(zip(mgrs, row, cfg.layers)):
+            gen = torch.Generator(device=DEV).manual_seed(50_000 + 100 * c + li)
+            g = torch.randn(x.shape, device=DEV, generator=gen)
+            if shard is not None:
+                x, g = x.chunk(shard[1])[shard[0]], g.chunk(shard[1])[shard[0]]
+            xr = x.clone().requires_grad_(True)
+            y = qm.quantize(xr, act=act)
+            y.backward(g)
+            out[f"y{c}_{li}"] = y.detach().cpu().numpy()
+            out[f"g{c}_{li}"] = xr.grad.cpu().numpy()
+    return out
 
 
 def state(mgrs):

@@ -3,8 +3,10 @@
 argv: output path, configuration ("small" / "c5", tests/dist_calib_common.py).
 
 Every rank observes its half of every batch through QuantizationManager.quantize with
-the managers' dist_group set -- per-call all-reduce, or deferred K2p records + one
-sync_calibration -- and rank 0 writes the observer state as JSON to argv[1]."""
+the managers' dist_group set -- per-call all-gather, or deferred K2p records + one
+sync_calibration, and ("small") observe + quantize per call, whose y / gradients every
+rank saves to argv[1].oq<rank>.npz -- and rank 0 writes the observer state as JSON to
+argv[1]."""
 import json
 import os
 import sys
@@ -37,6 +39,15 @@ def main():
             for qm in mgrs:
                 qm.dist_defer = False
         res[mode] = state(mgrs)
+    if cfg.name == "small":   # observe + quantize per call: gather + fold inside the fake quant
+        import numpy as np
+        from tests.dist_calib_common import observe_quantize
+        mgrs = managers(cfg)
+        for qm in mgrs:
+            qm.dist_group = dist.group.WORLD
+            qm.is_quantize = True
+        np.savez(f"{out_path}.oq{rank}.npz", **observe_quantize(cfg, mgrs, acts, shard=(rank, world)))
+        res["observe_quantize"] = state(mgrs)
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)

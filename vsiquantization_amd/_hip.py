@@ -104,6 +104,8 @@ _SIGS = {
     "vsiq_observe_f32": ([c_p, c_i64, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p], c_int),
     "vsiq_observe_finalize": ([c_p, c_p, c_p, c_int, c_d, c_d, c_p], c_int),
     "vsiq_observe_finalize_ranks": ([c_p, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p], c_int),
+    "vsiq_act_fq_fwd_ranks_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_int, c_p, c_p, c_p, c_int, c_d, c_d,
+                                   c_int, c_int, c_p], c_int),
     "vsiq_pc_observe_fq_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_int, c_int,
                                 c_int, c_d, c_d, c_p], c_int),
     "vsiq_pc_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_p], c_int),

@@ -463,6 +463,79 @@ void launch_fold_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c,
 #undef K9
 }
 
+// ----------------------------------------------------------------------------
+// K1r: the per-call multi-GPU observer exchange's fold + fake quant in ONE launch.  The
+// ranks' stats records (one K2 pass over each rank's shard, then one all_gather, rank
+// order) are folded by EVERY workgroup in rank order -- min / max exact, counts and sums
+// in float64, the same bits on every rank and in every workgroup -- into the running
+// update and the f64 qparams (minmax.py:42-74), and the workgroup quantizes its share
+// (uniform.py:55,95).  K9's idempotent-update trick: workgroup 0 alone writes the
+// running state, the qparams record and the batch's stats record; a workgroup that reads
+// the state after that recomputes the same qparams.  Replaces k_observe_finalize_ranks
+// + K1 (two launches, the qparams through memory) of the round-2 exchange.
+// ----------------------------------------------------------------------------
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
+__global__ __launch_bounds__(kBlock) void k_ranks_fq_fwd(
+    const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
+    uint64_t *__restrict__ mask, int64_t n, const double *__restrict__ gathered, int world,
+    double *__restrict__ stats_out, float *__restrict__ run_minmax, double *__restrict__ qp_out, int sym,
+    double qden, double eps, float lo, float hi, SiluLay L) {
+  __shared__ double s_qp[2];
+  if (threadIdx.x == 0) {
+    double f[6] = {__builtin_inf(), -__builtin_inf(), 0.0, 0.0, 0.0, 0.0};
+    double nn = 0.0;
+    for (int r = 0; r < world; ++r) {   // rank order (k_observe_finalize_ranks' fold)
+      const double *g = gathered + (int64_t)r * VSIQ_ST_LEN;
+      f[0] = __builtin_fmin(f[0], g[VSIQ_ST_MIN]);
+      f[1] = __builtin_fmax(f[1], g[VSIQ_ST_MAX]);
+      f[2] += g[VSIQ_ST_NAN];
+      f[3] += g[VSIQ_ST_SUMABS];
+      f[4] += g[VSIQ_ST_SUM];
+      f[5] += g[VSIQ_ST_SUMSQ];
+      nn += g[VSIQ_ST_N];
+    }
+    float state[2] = {0.f, 0.f};
+    if (run_minmax) { state[0] = run_minmax[0]; state[1] = run_minmax[1]; }
+    const bool lead = blockIdx.x == 0;
+    observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax ? state : nullptr, lead ? qp_out : nullptr,
+                    sym, qden, eps, &s_qp[0], &s_qp[1]);
+    if (lead) {
+      if (run_minmax) { run_minmax[0] = state[0]; run_minmax[1] = state[1]; }
+      if (stats_out) write_stats(stats_out, f, (int64_t)nn);
+    }
+  }
+  __syncthreads();
+  QP p;
+  p.s = (float)s_qp[0];
+  p.z = (float)s_qp[1];
+  p.lo = lo;
+  p.hi = hi;
+  p.discrete = 0;
+  p.d = make_fastdiv(p.s);
+  p.fast = fq_fast_qp(p.s, p.z);
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, kFlatU>(x, y, codes, mask, n, p, blockIdx.x, GateClk{0}, 0u, L);
+}
+
+template <int ACT>
+void launch_ranks_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
+                         const double *gathered, int world, double *st, float *run, double *qp, int sym,
+                         double qden, double eps, float lo, float hi, const SiluLay &L, hipStream_t s) {
+  const dim3 grid((unsigned)oneshot_grid(cdiv(n, 4)));
+#define K1R(V, T, C, M)                                                                                    \
+  hipLaunchKernelGGL((k_ranks_fq_fwd<V, T, C, M, ACT>), grid, dim3(kBlock), 0, s, x, y, c, m, n, gathered, \
+                     world, st, run, qp, sym, qden, eps, lo, hi, L)
+#define K1RCM(V, T)                             \
+  if (c && m) { K1R(V, T, true, true); }        \
+  else if (c) { K1R(V, T, true, false); }       \
+  else if (m) { K1R(V, T, false, true); }       \
+  else { K1R(V, T, false, false); }
+  if (vec && nt) { K1RCM(true, true) }
+  else if (vec) { K1RCM(true, false) }
+  else { K1RCM(false, false) }
+#undef K1RCM
+#undef K1R
+}
+
 template <int ACT>
 void launch_observe_fq_small_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
                                  double *st, float *run, double *qp, int sym, double qden, double eps, float lo,
@@ -1000,6 +1073,20 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
   const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
   VSIQ_ACT(act, launch_fold_fq_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, ws,
            stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, act_lay(act, n),
+           (hipStream_t)stream);
+  return launch_rc();
+}
+
+int vsiq_act_fq_fwd_ranks_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                              const double *gathered, int world, double *stats_out, float *run_minmax,
+                              double *qp_out, int symmetric, double qden, double eps, int qmin, int qmax,
+                              void *stream) {
+  if (n <= 0 || !c || !y || !gathered || world <= 0 || qmin > qmax || !act_ok(act)) return VSIQ_E_ARG;
+  if (oneshot_grid(cdiv(n, 4)) > 0x7fffffffLL) return VSIQ_E_ARG;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
+  VSIQ_ACT(act, launch_ranks_fq_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, gathered,
+           world, stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, act_lay(act, n),
            (hipStream_t)stream);
   return launch_rc();
 }

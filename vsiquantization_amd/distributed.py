@@ -14,9 +14,10 @@ float64 summation order.
 
 Two modes:
 * per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): one tiny
-  all_gather of the stats records per observer call and one fold launch
-  (``gather_finalize``), needed when the same call also fake-quantizes
-  (observe+quantize mode, §3.4);
+  all_gather of the stats records per observer call; an observe+quantize call (§3.4)
+  then folds them inside its fake-quant launch (``observe_gather_fake_quant``: two
+  launches and one collective per call), an observe-only call in one fold launch
+  (``gather_finalize``);
 * deferred  (``dist_defer`` True, calibration): each rank only writes its local
   per-call partial records (K2p, no cross-workgroup fold, no atomics);
   ``sync_calibration(model)`` folds ALL calls of ALL layers in one launch,
@@ -62,25 +63,23 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
 
 def gather_stats(stats: torch.Tensor, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
     """One collective: every rank's stats record ``[ST_LEN]`` gathered in rank order into
-    ``[world * ST_LEN]`` (all_gather_into_tensor over RCCL; the list form on gloo)."""
+    ``[world * ST_LEN]`` (all_gather_into_tensor, on RCCL and on the gloo rehearsals
+    alike, so the tests run the branch the multi-GPU job runs)."""
     world = dist.get_world_size(group)
     if out is None:
         out = torch.empty(world * H.ST_LEN, dtype=stats.dtype, device=stats.device)
-    src = stats.contiguous()
-    if dist.get_backend(group) == "gloo":   # CPU rehearsals: the list form everywhere
-        dist.all_gather(list(out.view(world, H.ST_LEN).unbind(0)), src, group=group)
-    else:
-        dist.all_gather_into_tensor(out, src, group=group)
+    dist.all_gather_into_tensor(out, stats.contiguous(), group=group)
     return out
 
 
 def gather_finalize(stats: torch.Tensor, run_minmax: torch.Tensor, *, symmetric: bool, num_bits: int = 8,
                     eps: float = 1e-8, group=None):
-    """Per-call multi-GPU observer exchange: gather the ranks' stats records (one
-    collective), then ONE launch folds them in rank order (min / max exact, sums in float64
-    -- the same bits on every rank), writes the batch's stats record and applies the
-    running update + f64 qparams (vsiq_observe_finalize_ranks).  Returns (stats f64[ST_LEN],
-    qp f64[QP_LEN]); min/max/qparams bit-identical to one GPU over the whole batch."""
+    """Per-call multi-GPU observer exchange (observe only): gather the ranks' stats records
+    (one collective), then ONE launch folds them in rank order (min / max exact, sums in
+    float64 -- the same bits on every rank), writes the batch's stats record and applies
+    the running update + f64 qparams (vsiq_observe_finalize_ranks).  Returns (stats
+    f64[ST_LEN], qp f64[QP_LEN]); min/max/qparams bit-identical to one GPU over the whole
+    batch."""
     from .fakequant import qden
     gathered = gather_stats(stats, group)
     dev = stats.device
@@ -91,6 +90,57 @@ def gather_finalize(stats: torch.Tensor, run_minmax: torch.Tensor, *, symmetric:
                                              qden(symmetric, num_bits, eps), float(eps), H.stream_of(dev))
     H.check(rc, "vsiq_observe_finalize_ranks")
     return st, qp
+
+
+def observe_gather_fake_quant(x: torch.Tensor, run_minmax: torch.Tensor, *, symmetric: bool, num_bits: int = 8,
+                              eps: float = 1e-8, qmin: int, qmax: int, act=None, group=None,
+                              want_mask: bool = False):
+    """Per-call multi-GPU observe + fake quant of this rank's shard (observe+quantize mode,
+    quantization_manager.py:73-90 under DDP): the local K2 pass (stats record only), ONE
+    all_gather of the ranks' records, and ONE launch that folds them in rank order, applies
+    the running update + f64 qparams and fake-quantizes act(x) (vsiq_act_fq_fwd_ranks_f32).
+    Two launches and one collective per call; min / max / qparams / y bit-identical to one
+    GPU over the whole batch.  Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None)."""
+    from .fakequant import _i64, observe_tensor, qden
+    x = H.require_device_f32(x)
+    _, local = observe_tensor(x, symmetric=symmetric, num_bits=num_bits, eps=eps, run_minmax=None,
+                              want_qp=False, want_stats=True, act=act)
+    gathered = gather_stats(local, group)
+    dev = x.device
+    y = torch.empty_like(x)
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64, device=dev)
+    st = torch.empty(H.ST_LEN, dtype=torch.float64, device=dev)
+    mask = H.mask_buffer(1, x.numel(), dev) if want_mask else None
+    rc = H.lib().vsiq_act_fq_fwd_ranks_f32(H.ptr(x), H.ptr(y), None, H.ptr(mask), _i64(x.numel()), H.act_code(act),
+                                           H.ptr(gathered), int(dist.get_world_size(group)), H.ptr(st),
+                                           H.ptr(run_minmax), H.ptr(qp), int(bool(symmetric)),
+                                           qden(symmetric, num_bits, eps), float(eps), int(qmin), int(qmax),
+                                           H.stream_of(dev))
+    H.check(rc, "vsiq_act_fq_fwd_ranks_f32")
+    return y, qp, st, mask
+
+
+class ObserveGatherFakeQuantFn(torch.autograd.Function):
+    """observe_gather_fake_quant with the reference's STE gradient at fp32(scale) of this
+    call (FakeQuantFixedFn's backward; x only)."""
+
+    @staticmethod
+    def forward(ctx, x, run_minmax, symmetric, num_bits, eps, qmin, qmax, act, group):
+        y, qp, st, mask = observe_gather_fake_quant(x, run_minmax, symmetric=symmetric, num_bits=num_bits, eps=eps,
+                                                    qmin=qmin, qmax=qmax, act=act, group=group, want_mask=True)
+        ctx.act = act
+        ctx.save_for_backward(mask, x) if H.act_code(act) != H.ACT_NONE else ctx.save_for_backward(mask)
+        ctx.scale = qp[H.QP_SCALE:H.QP_SCALE + 1]
+        ctx.mark_non_differentiable(qp, st)
+        return y, qp, st
+
+    @staticmethod
+    def backward(ctx, gy, _gqp, _gst):
+        from .fakequant import ste_backward
+        saved = ctx.saved_tensors
+        pre = saved[1] if len(saved) > 1 else None
+        gx = ste_backward(gy.contiguous(), saved[0], ctx.scale, pre=pre, act=ctx.act)
+        return gx, None, None, None, None, None, None, None, None
 
 
 def replay_minmax(min_val, max_val, records):

@@ -258,7 +258,9 @@ class QuantizationManager(nn.Module):
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
             return y
         if act is None or self._act_fusable(x):
-            y = self._observe_quantize_small(x, act)
+            y = self._observe_quantize_ranks(x, act)
+            if y is None:
+                y = self._observe_quantize_small(x, act)
             if y is not None:
                 return y
         if self.is_learning_scale and self.is_quantize:
@@ -276,6 +278,38 @@ class QuantizationManager(nn.Module):
             return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale,
                                            act=act)
         return x
+
+    def _observe_quantize_ranks(self, x, act):
+        """Multi-GPU per-call observe + quantize (dist_group set, not deferred): the local
+        K2 pass, one all_gather of the ranks' stats records and ONE launch that folds them
+        and fake-quantizes (distributed.observe_gather_fake_quant); None when it does not
+        apply (then collect_qparameter + quantize below)."""
+        from ..distributed import ObserveGatherFakeQuantFn, observe_gather_fake_quant
+        from .uniform import UniformQuantizer
+        obs = self.observer
+        if not (self.dist_group is not None and not self.dist_defer and self.is_quantize
+                and not self.is_learning_scale and self.is_observer_qparam
+                and type(self.quantizer) is UniformQuantizer and isinstance(obs, MinMaxObserver)
+                and not isinstance(obs, PerChannelMinMaxObserver) and self._device_observer(x)
+                and x.dtype == torch.float32 and x.numel() > 0):
+            return None
+        self._join()
+        self._x_device = x.device
+        if obs._obs_stream is not None and obs._obs_stream != torch.cuda.current_stream(x.device):
+            obs._join()
+        state = obs.device_state(x.device)
+        q = self.quantizer
+        if x.requires_grad and torch.is_grad_enabled():
+            y, qp, st = ObserveGatherFakeQuantFn.apply(x, state, obs.symmetric, obs.num_bits, obs.eps, q.qmin,
+                                                       q.qmax, act, self.dist_group)
+        else:
+            y, qp, st, _ = observe_gather_fake_quant(x, state, symmetric=obs.symmetric, num_bits=obs.num_bits,
+                                                     eps=obs.eps, qmin=q.qmin, qmax=q.qmax, act=act,
+                                                     group=self.dist_group)
+        obs._dirty = True
+        self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+        self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
+        return y
 
     def _observe_quantize_small(self, x, act):
         """Observe + quantize of a small tensor in one call (K8 / K9) when this call is the
