@@ -787,6 +787,20 @@ def cpu_workload(workload, bits=(2, 4), frac=1):
                 E.lsq_step(c, g, scale=0.5, bits=bits[1], act="relu")
         return (fn, sum(t[0].numel() + t[2].numel() for t in tens),
                 f"{imgs} of the 256 images through all 27 backbone layers (+ weights), w{bits[0]}/a{bits[1]}, fwd+bwd")
+    if workload == "act":
+        from oracle.fakequant_np import minmax_qparams
+        imgs = 1024 // (64 * frac)
+        acts = [torch.randn(imgs, co, h, h, generator=gen) for _, co, _, _, h in yolov8n_backbone()]
+
+        def fn():   # per layer: relu, observer (2 .item()), 3 stats, qparams, fake quant (qm.py:55-90)
+            for c in acts:
+                a = torch.relu(c)
+                mn, mx = E.observe(a)
+                a.abs().mean().item(), a.mean().item(), a.std().item()
+                s, z = minmax_qparams(mn, mx, True, 8)
+                E.fake_quant(a, s, z, -8, 7)
+        return (fn, sum(t.numel() for t in acts),
+                f"{imgs} of the 1024 images through all 27 activation quantizers (observe + quantize per call)")
     raise ValueError(workload)
 
 
@@ -1179,8 +1193,7 @@ def main(argv=None):
         # CPU legs after every GPU measurement (host threads do not disturb the timed regions)
         out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds, bits)
         for key, e in extras.items():
-            if key != "act":
-                e["cpu_baseline"] = cpu_baseline(key, a.cpu_seconds, bits)
+            e["cpu_baseline"] = cpu_baseline(key, a.cpu_seconds, bits)
     if "act" in extras:
         out["batched_act_quant"] = extras.pop("act")
     if extras:
