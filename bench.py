@@ -865,11 +865,32 @@ def cpu_baseline(workload, seconds, bits=(2, 4)):
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:  # noqa: BLE001
         model = platform.processor()
-    return {"value": tried[th], "unit": "Melem/s", "cores": int(th), "kind": "port",
-            "sample": f"{desc}; min of {runs[th]} runs at {th} threads; torch {torch.__version__} CPU, {model}",
-            "threads_whole": {str(k): v for k, v in tried.items()},
-            "thread_probe_c1": {str(k): v for k, v in probe.items()},
-            "os_cpu_count": total, "usable_cpus": usable, "cpu_model": model}
+    out = {"value": tried[th], "unit": "Melem/s", "cores": int(th), "kind": "port",
+           "sample": f"{desc}; min of {runs[th]} runs at {th} threads; torch {torch.__version__} CPU, {model}",
+           "threads_whole": {str(k): v for k, v in tried.items()},
+           "thread_probe_c1": {str(k): v for k, v in probe.items()},
+           "os_cpu_count": total, "usable_cpus": usable, "cpu_model": model}
+    if workload == "c1":
+        out["product_host"] = host_product_baseline(seconds)
+    return out
+
+
+def host_product_baseline(seconds):
+    """BASELINE C1 through THIS package on CPU tensors: MinMaxObserver.forward +
+    UniformQuantizer.quantize take the native host loops (vsiquantization_amd/host.py,
+    csrc/k_host.hip), the same op sequence the reference runs -- reported beside the
+    reference's own timing, not used as the GPU's baseline."""
+    import vsiquantization_amd as V
+    from vsiquantization_amd import host
+    x = torch.randn(256, 256, generator=torch.Generator().manual_seed(0))
+    q = V.UniformQuantizer(8, True)
+
+    def fn():
+        s, z = V.MinMaxObserver(True).forward(x)
+        return q.quantize(x, s, z, False)
+    t, runs = _best_time(fn, seconds)
+    return {"value": x.numel() / t / 1e6, "unit": "Melem/s", "us_per_call": 1e6 * t, "host_threads": host.threads(),
+            "sample": f"the whole 256x256 C1 call (fresh observer, observe + fake quant), min of {runs} runs"}
 
 
 # --------------------------------------------------------------------------- measurement

@@ -271,6 +271,15 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
 int64_t vsiq_observe_part_records(int64_t n);
 int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts, int64_t parts_len,
                               void *stream);
+
+/*
+ * K2o: vsiq_act_observe_part_f32 that also writes y = act(c) (n floats): a calibration
+ * forward of a fused layer in one pass -- the activation the next layer consumes
+ * (modules/fused.py:133) and the deferred observer's records of it.  Records bit-identical
+ * to vsiq_act_observe_part_f32(c, n, act); y bit-identical to vsiq_act_fwd_f32.
+ */
+int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, double *parts, int64_t parts_len,
+                                  void *stream);
 int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride,
                             double *stats_out, void *stream);
 
@@ -507,6 +516,27 @@ int vsiq_pcm_lsq_bwd_arrive_f32(const float *g, const float *x, float *gx, int64
 int vsiq_bn_fold_f32(const float *w, const float *b, const float *gamma, const float *beta,
                      const float *running_mean, const float *running_var, float eps, float *w_out,
                      float *b_out, int64_t rows, int64_t rowlen, void *stream);
+
+/*
+ * Host path (CPU tensors; the reference's own environment, BASELINE C1): the same
+ * element arithmetic on HOST pointers, native C++ loops over fixed 64K-element chunks
+ * on up to VSIQ_HOST_THREADS threads (default: the CPUs this process may use); results
+ * do not depend on the thread count.  mask: one byte per element.
+ *   vsiq_host_observe_f32  = vsiq_act_observe_f32        (minmax.py:42-74, qm.py:66-68)
+ *   vsiq_host_fq_fwd_f32   = vsiq_act_fq_fwd_f32         (uniform.py:55,95; qp nullable)
+ *   vsiq_host_ste_bwd_f32  = vsiq_act_ste_bwd_f32        (autograd of uniform.py:55,95)
+ *   vsiq_host_lsq_bwd_f32  = vsiq_act_lsq_bwd_f32        (autograd of uniform.py:47-56)
+ */
+int vsiq_host_observe_f32(const float *x, int64_t n, int act, double *stats_out, float *run_minmax, double *qp_out,
+                          int symmetric, double qden, double eps);
+int vsiq_host_fq_fwd_f32(const float *x, float *y, uint8_t *codes, uint8_t *mask, int64_t n, int act,
+                         const double *qp, double scale, double zp, int zp_round, int discrete, int qmin,
+                         int qmax);
+int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre, float *gx, int64_t n, int act,
+                          double scale);
+int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, int act, double scale, double zp,
+                          int zp_learn, int qmin, int qmax, double gscale, double *grad_out);
+int vsiq_host_threads(void);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn as nn
 
-from vsiquantization_amd.modules.fused import ConvBnReLU
+from vsiquantization_amd.modules.fused import ConvBn, ConvBnReLU
 from vsiquantization_amd.utils.quantize_manager import calibrate_qat_model, data_calib
 
 pytestmark = pytest.mark.gpu
@@ -149,13 +149,14 @@ def test_observe_parts_multi_all_vector_batch_bitwise(act):
 
 
 def test_queued_deferred_calibration_equals_unqueued(monkeypatch):
-    """QuantizationManager's deferred calls queued and observed by K2m (default) give
-    the same running min/max, qparams and stats lists, bit for bit, as one K2p launch per
-    call (VSIQ_OBSERVE_BATCH=0)."""
+    """QuantizationManager's deferred calls queued and observed by K2m (opt-in,
+    VSIQ_OBSERVE_BATCH=1) give the same running min/max, qparams and stats lists, bit for
+    bit, as the default (fused layers: K2o, act + records in one pass; others: K2p)."""
     a = _model()
     b = copy.deepcopy(a)
+    monkeypatch.setenv("VSIQ_OBSERVE_BATCH", "1")
     calibrate_qat_model(a, _loader(), data_calib, DEV)
-    monkeypatch.setenv("VSIQ_OBSERVE_BATCH", "0")
+    monkeypatch.delenv("VSIQ_OBSERVE_BATCH")
     calibrate_qat_model(b, _loader(), data_calib, DEV)
     assert _state(a) == _state(b)
     from vsiquantization_amd import observe_batch
@@ -255,3 +256,53 @@ def test_manager_observe_quantize_mid_size_vs_oracle(shape, sym, bits):
         assert float(qm.scale) == s and float(qm.zero_point) == z
         assert np.array_equal(y.detach().cpu().numpy().view(np.uint32), yo.view(np.uint32))
         assert np.array_equal(xt.grad.cpu().numpy().view(np.uint32), gxo.view(np.uint32))
+
+
+class _Residual(nn.Module):
+    """Observed layers whose outputs user code modifies in place afterwards: a residual
+    ``+=`` on a ConvBn output (no activation: the observed tensor is the one handed back),
+    an in-place ReLU and an in-place scale on fused-ReLU outputs."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(2)
+        names = ("MinMaxObserver", "UniformQuantizer", "MinMaxObserver", "UniformQuantizer")
+
+        def bn(c):
+            b = nn.BatchNorm2d(c)
+            b.running_var.uniform_(0.5, 2.0)
+            return b
+        self.a = ConvBnReLU(nn.Conv2d(3, 16, 3, padding=1, bias=False), bn(16), nn.ReLU(), *names, True, True,
+                            True, 4, 4)
+        self.b = ConvBn(nn.Conv2d(16, 16, 3, padding=1, bias=False), bn(16), *names, True, True, True, 4, 4)
+        self.c = ConvBnReLU(nn.Conv2d(16, 16, 3, padding=1, bias=False), bn(16), nn.SiLU(), *names, True, True,
+                            True, 4, 4)
+        self.act = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        y = self.a(x)
+        z = self.b(y)
+        z += y              # residual, in place on an observed (handed back) tensor
+        z = self.act(z)     # in-place ReLU
+        w = self.c(z)
+        w.mul_(0.5)         # in place on a fused layer's calibration output
+        return w
+
+    def layers(self):
+        return [self.a, self.b, self.c]
+
+
+def test_deferred_calibration_with_in_place_ops_equals_sync():
+    """deferred calibration (the default) must observe each call before user
+    code can modify the tensor in place -- the result equals the per-call observers'."""
+    a = _Residual().to(DEV)
+    b = copy.deepcopy(a)
+    calibrate_qat_model(a, _loader(), data_calib, DEV)
+    calibrate_qat_model(b, _loader(), data_calib, DEV, defer_observers=False)
+    sa, sb = _state(a.layers()), _state(b.layers())
+    for x, y in zip(sa, sb):
+        assert (x[0], x[1]) == (y[0], y[1])
+        for i in (2, 3, 4):
+            np.testing.assert_allclose(x[i], y[i], rtol=1e-6, atol=1e-7)
+    from vsiquantization_amd import observe_batch
+    assert observe_batch.pending() == 0

@@ -190,3 +190,18 @@ def test_silu_act_code_layout():
         assert H.lib().vsiq_act_fwd_f32(H.ptr(x), H.ptr(y), H.c_i64(100), code, H.stream_of(torch.device(DEV))) == 0
     finally:
         H.set_silu_reference()
+
+
+@pytest.mark.parametrize("act", ["relu", "silu"])
+@pytest.mark.parametrize("n", [7, 4096, 100_003, 3 * 2**20 + 4])
+def test_observe_parts_out_equals_act_then_parts(n, act, pin):
+    """K2o (vsiq_act_observe_part_out_f32): y = act(c) and the deferred records in one
+    pass == the activation alone + K2p over c, bit for bit (records and y)."""
+    pin(32, 7)
+    c, _ = _inputs(n, n + 5)
+    x = cu(c)
+    y, parts = FQ.observe_parts_out(x, act)
+    want_parts = FQ.observe_parts(x, act=act)
+    assert torch.equal(parts.view(torch.int64), want_parts.view(torch.int64))
+    G.assert_bitwise_f32(npy(y), npy(FQ.activation(x, act)), "y")
+    G.assert_bitwise_f32(npy(y), O.act_forward(c, act, (32, 7)), "y vs oracle")

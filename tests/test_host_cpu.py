@@ -1,0 +1,166 @@
+"""The native host path (CPU tensors; csrc/k_host.hip through vsiquantization_amd/host.py)
+against the reference goldens, bit for bit: the reference's own environment
+(BASELINE C1: UniformQuantizer / MinMaxObserver on CPU tensors).  Runs without a GPU."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import vsiquantization_amd as V
+from vsiquantization_amd import _hip as H
+from vsiquantization_amd import host
+from oracle import fakequant_np as O
+from tests import goldens as G
+
+
+def t(a, grad=False):
+    x = torch.from_numpy(np.ascontiguousarray(a))
+    return x.requires_grad_(True) if grad else x
+
+
+def npy(x):
+    return x.detach().numpy()
+
+
+@pytest.mark.parametrize("case", G.cases("per_tensor_observe_fq"), ids=lambda c: c["key"])
+def test_golden_per_tensor_observe_fq(case):
+    x = t(G.arr(case["x"]))
+    obs = V.MinMaxObserver(case["sym"], case["obs_bits"])
+    if "raises" in case:
+        with pytest.raises(Exception) as ei:
+            obs.forward(x)
+        assert type(ei.value).__name__ == case["raises"]
+        return
+    s, z = obs.forward(x)
+    assert (s, z) == (case["scale"], case["zp"]) or (math.isnan(s) and math.isnan(case["scale"]))
+    assert (obs.min_val, obs.max_val) == (case["min_val"], case["max_val"])
+    q = V.UniformQuantizer(case["bits"], case["sym"])
+    xg = t(G.arr(case["x"]), grad=True)
+    y = q.quantize(xg, s, z, False)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    G.assert_bitwise_f32(npy(q.discreate_tensor(x, s, z, q.qmin, q.qmax)), G.arr(case["x_int"]), "x_int")
+    # the qparams record of the host pass, read as a tensor
+    obs2 = V.MinMaxObserver(case["sym"], case["obs_bits"])
+    qp, _ = obs2.observe_device(x)
+    assert qp[H.QP_SCALE].item() == case["scale"] and qp[H.QP_ZP].item() == case["zp"]
+    G.assert_bitwise_f32(npy(q.quantize(x, qp[H.QP_SCALE], qp[H.QP_ZP], False)), G.arr(case["y"]), "y(record)")
+
+
+@pytest.mark.parametrize("case", G.cases("fixed_fq"), ids=lambda c: c["key"])
+def test_golden_fixed_fq(case):
+    q = V.UniformQuantizer(case["bits"], case["sym"])
+    xg = t(G.arr(case["x"]), grad=True)
+    y = q.quantize(xg, case["scale"], case["zp"], False)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq"), ids=lambda c: c["key"])
+def test_golden_learnable(case):
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    q = (V.UniformQuantizer if case["sym"] else V.LSQQuantizer)(case["bits"], case["sym"])
+    scale = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64))
+    zp = 0 if case["sym"] else torch.nn.Parameter(torch.tensor(case["zp"], dtype=torch.float64))
+    xg = t(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=1e-9)
+    qmin, qmax = O.qrange(case["bits"], case["sym"])
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                              O.grad_scale(qmax, x.size), learn_zp=not case["sym"])
+    assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+    if not case["sym"]:
+        assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=1e-9)
+
+
+@pytest.mark.parametrize("case", G.cases("manager_sequence"), ids=lambda c: c["key"])
+def test_golden_manager_sequence(case):
+    """QuantizationManager on CPU tensors: calibrate (stats lists, running min/max,
+    qparams), observe + quantize, learn-init (qm.py:55-114)."""
+    bits, sym = case["bits"], case["sym"]
+    qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", bits, sym, is_learning_scale=False)
+    qm.is_observer_qparam, qm.is_quantize = True, False
+    for k in case["xs"]:
+        qm.quantize(t(G.arr(k)))
+    cal = case["calib"]
+    assert (qm.observer.min_val, qm.observer.max_val) == (cal["min_val"], cal["max_val"])
+    assert (qm.scale, qm.zero_point) == (cal["scale"], cal["zero_point"])
+    np.testing.assert_allclose(qm.mean_abs_x, cal["mean_abs_x"], rtol=1e-6)
+    np.testing.assert_allclose(qm.mean_x, cal["mean_x"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(qm.std, cal["std"], rtol=1e-6)
+    qm.is_quantize = True
+    y = qm.quantize(t(G.arr(case["x_oq"])))
+    assert qm.scale == case["observe_quantize"]["scale"]
+    G.assert_bitwise_f32(npy(y), G.arr(case["y_oq"]), "y_oq")
+
+
+@pytest.mark.parametrize("case", G.cases("act_fq"), ids=lambda c: c["key"])
+def test_golden_act_fq(case):
+    """Fused ReLU / SiLU + fake quant on the host (torch CPU's SiLU bits, this layout)."""
+    H.set_silu_reference(*G.GOLDEN_SILU_REF)
+    try:
+        q = V.UniformQuantizer(case["bits"], case["sym"])
+        c = t(G.arr(case["x"]), grad=True)
+        if case["mode"] == "observe":
+            qp, _ = host.observe_tensor(c.detach(), symmetric=case["sym"], act=case["act"])
+            assert (qp[H.QP_SCALE].item(), qp[H.QP_ZP].item()) == (case["scale"], case["zp"])
+            y = host.fake_quant_fixed(c, None, None, q.qmin, q.qmax, qp=qp, act=case["act"])
+        elif case["mode"] == "fixed":
+            y = q.quantize(c, case["scale"], case["zp"], False, act=case["act"])
+        else:
+            s = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64))
+            y = q.quantize(c, s, 0, True, act=case["act"])
+        y.backward(t(G.arr(case["g"])))
+        G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+        G.assert_bitwise_f32(npy(c.grad), G.arr(case["grad_x"]), "grad_c")
+    finally:
+        H.set_silu_reference()
+
+
+def test_c1_full_size_vs_oracle():
+    """BASELINE C1 (256x256 per-tensor symmetric int8) through the public classes on the
+    host, against the oracle: qparams exact, y / codes / grad bitwise."""
+    rng = np.random.default_rng(1)
+    w = (rng.standard_normal((256, 256)) * 0.05).astype(np.float32)
+    g = rng.standard_normal((256, 256)).astype(np.float32)
+    obs, q = V.MinMaxObserver(True), V.UniformQuantizer(8, True)
+    s, z = obs.forward(t(w))
+    mn, mx = O.observe_minmax(w)
+    assert (s, z) == O.minmax_qparams(mn, mx, True, 8)
+    xg = t(w, grad=True)
+    y = q.quantize(xg, s, z, False)
+    y.backward(t(g))
+    yo, qo, mo = O.fq_forward(w, s, z, -128, 127)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(xg.grad), O.fq_backward_fixed(g, mo, s), "grad")
+
+
+@pytest.mark.parametrize("n", [1, 5, 65_536 * 3 + 7])
+def test_host_stats_record_vs_oracle(n):
+    """mean|x| / mean / std of the host pass (f64 sums in fixed chunk order) vs the oracle;
+    min / max / NaN exact; a NaN call leaves the running state alone."""
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n) * 2).astype(np.float32)
+    run = torch.zeros(2)
+    qp, st = host.observe_tensor(t(x), symmetric=False, run_minmax=run)
+    mn, mx = O.observe_minmax(x)
+    assert (st[H.ST_MIN].item(), st[H.ST_MAX].item()) == (float(x.min()), float(x.max()))
+    assert (run[0].item(), run[1].item()) == (mn, mx)
+    ma, me, sd = O.collect_stats(x)
+    assert st[H.ST_MEANABS].item() == pytest.approx(ma, rel=1e-6)
+    if n > 1:
+        assert st[H.ST_STD].item() == pytest.approx(sd, rel=1e-6)
+    x[0] = np.nan
+    run2 = run.clone()
+    host.observe_tensor(t(x * 3), symmetric=False, run_minmax=run2)
+    assert torch.equal(run, run2)
+
+
+def test_host_threads_reported():
+    assert host.threads() >= 1

@@ -127,6 +127,7 @@ _SIGS = {
     "vsiq_observe_part_records": ([c_i64], c_i64),
     "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
     "vsiq_act_observe_part_multi_f32": ([c_p, c_int, c_int, c_p], c_int),
+    "vsiq_act_observe_part_out_f32": ([c_p, c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
     "vsiq_lsq_part_records": ([c_i64], c_i64),
     "vsiq_act_lsq_bwd_part_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_p, c_i64,
                                    c_p], c_int),
@@ -141,6 +142,11 @@ _SIGS = {
     "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
     "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),
     "vsiq_lsq_bwd_multi_f32": ([c_p, c_int, c_p, c_i64, c_p, c_p], c_int),
+    "vsiq_host_observe_f32": ([c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d], c_int),
+    "vsiq_host_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_d, c_int, c_int, c_int, c_int], c_int),
+    "vsiq_host_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_d], c_int),
+    "vsiq_host_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_d, c_d, c_int, c_int, c_int, c_d, c_p], c_int),
+    "vsiq_host_threads": ([], c_int),
     "vsiq_act_fwd_f32": ([c_p, c_p, c_i64, c_int, c_p], c_int),
     "vsiq_act_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p], c_int),
     "vsiq_selftest_exp_f32": ([c_p, c_p, c_p, c_i64, c_p], c_int),

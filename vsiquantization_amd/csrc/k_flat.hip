@@ -88,27 +88,6 @@ struct ObsFold {   // partial record {min, max, nan count, sum|x|, sum x, sum x^
   }
 };
 
-// The stats record (VSIQ_ST_*) of one call from its folded {min, max, nan count,
-// sum|x|, sum x, sum x^2}: quantization_manager.py:66-68's fp32 mean(|x|) / mean /
-// unbiased std, NaN when the call held a NaN (torch's fp32 reductions are NaN then).
-__device__ __forceinline__ void write_stats(double *__restrict__ st, const double (&f)[6], int64_t n) {
-  const double dn = (double)n;
-  const bool has_nan = f[2] > 0.0;
-  st[VSIQ_ST_MIN] = (double)(float)f[0];   // NaN-ignoring; see VSIQ_ST_NAN
-  st[VSIQ_ST_MAX] = (double)(float)f[1];
-  st[VSIQ_ST_NAN] = f[2];
-  st[VSIQ_ST_SUMABS] = f[3];
-  st[VSIQ_ST_SUM] = f[4];
-  st[VSIQ_ST_SUMSQ] = f[5];
-  st[VSIQ_ST_N] = dn;
-  const double mean = f[4] / dn;
-  const double var = (f[5] - f[4] * mean) / (dn - 1.0);
-  st[VSIQ_ST_MEANABS] = has_nan ? __builtin_nan("") : (double)(float)(f[3] / dn);
-  st[VSIQ_ST_MEAN] = has_nan ? __builtin_nan("") : (double)(float)mean;
-  st[VSIQ_ST_STD] = (has_nan || n < 2) ? __builtin_nan("")
-                                       : (double)(float)__builtin_sqrt(var > 0.0 ? var : 0.0);
-}
-
 // Block partial -> workspace record; the workgroup holding the fold of every record
 // writes the stats record and applies the running update.
 __device__ __forceinline__ void observe_epilogue(ObsAcc &a, int64_t n, double *__restrict__ stats_out,
@@ -260,6 +239,42 @@ __global__ __launch_bounds__(kBlock) void k_observe_part(const float *__restrict
                                                           double *__restrict__ parts, SiluLay L) {
   ObsAcc a;
   observe_stride<VEC, NT, ACT, U>(x, n, a, L);
+  store_part_record(a, parts, blockIdx.x, gridDim.x, n);
+}
+
+// ----------------------------------------------------------------------------
+// K2o: a calibration forward of a fused layer in ONE pass -- y = act(c), the tensor the
+// next layer consumes (modules/fused.py:133), and the deferred observer's K2p records of
+// act(c) (minmax.py:42-43 + qm.py:66-68) -- instead of an activation pass that writes y
+// and an observer pass that reads it again (8 instead of 12 B per element) and with
+// nothing queued that user code could modify before it is observed.  Same grid, groups
+// per lane and accumulation order as k_observe_part, so the records are the same bits.
+// ----------------------------------------------------------------------------
+template <bool VEC, bool NT, int ACT, int U>
+__global__ __launch_bounds__(kBlock) void k_observe_part_out(const float *__restrict__ x, float *__restrict__ y,
+                                                              int64_t n, double *__restrict__ parts, SiluLay L) {
+  ObsAcc a;
+  obs_init(a);
+  const int64_t ng = cdiv(n, 4);
+  const int64_t nfull = n / 4;
+  const int64_t step = (int64_t)gridDim.x * kBlock * U;
+  for (int64_t b = (int64_t)blockIdx.x * kBlock * U; b < ng; b += step) {
+    f4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = load_group_c<VEC, NT>(x, b + threadIdx.x + k * kBlock, ng, n);
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = b + threadIdx.x + k * kBlock;
+      v[k] = act_fwd4_at<ACT>(v[k], 4 * i, L);
+      if (i < nfull) obs_add4(a, v[k], 4);
+      else if (i < ng) obs_add4(a, v[k], valid_in_group(i, n));
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = b + threadIdx.x + k * kBlock;
+      if (i < ng) store_group<VEC, NT>(y, i, n, v[k]);
+    }
+  }
   store_part_record(a, parts, blockIdx.x, gridDim.x, n);
 }
 
@@ -1011,6 +1026,35 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
   const bool vec = aligned16(c) && n % 4 == 0;
   VSIQ_ACT(act, launch_observe_part, vec, g_tune.nontemporal != 0, c, n, parts, grid, act_lay(act, n),
            (hipStream_t)stream);
+  return launch_rc();
+}
+
+int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, double *parts, int64_t parts_len,
+                                  void *stream) {
+  if (n <= 0 || !c || !y || !parts || !act_ok(act)) return VSIQ_E_ARG;
+  const int64_t grid = observe_part_grid(n);
+  if (parts_len < grid * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
+  const bool vec = aligned16(c) && aligned16(y) && n % 4 == 0;
+  const bool nt = g_tune.nontemporal != 0;
+  const int u = observe_part_u(n);
+  const SiluLay L = act_lay(act, n);
+  const hipStream_t st = (hipStream_t)stream;
+#define K2O(A, U_)                                                                                              \
+  if (vec && nt) hipLaunchKernelGGL((k_observe_part_out<true, true, A, U_>), dim3((unsigned)grid), dim3(kBlock), 0, \
+                                    st, c, y, n, parts, L);                                                     \
+  else if (vec) hipLaunchKernelGGL((k_observe_part_out<true, false, A, U_>), dim3((unsigned)grid), dim3(kBlock), 0, \
+                                   st, c, y, n, parts, L);                                                      \
+  else hipLaunchKernelGGL((k_observe_part_out<false, false, A, U_>), dim3((unsigned)grid), dim3(kBlock), 0, st, c,  \
+                          y, n, parts, L);
+#define K2OU(A)                     \
+  if (u == 8) { K2O(A, 8) }         \
+  else if (u == 4) { K2O(A, 4) }    \
+  else { K2O(A, 2) }
+  if (act_kind(act) == kActRelu) { K2OU(kActRelu) }
+  else if (act_kind(act) == kActSilu) { K2OU(kActSilu) }
+  else { K2OU(kActNone) }
+#undef K2OU
+#undef K2O
   return launch_rc();
 }
 

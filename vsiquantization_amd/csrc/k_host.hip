@@ -1,0 +1,221 @@
+// k_host.hip — the fake-quant path on the HOST, for CPU tensors: the reference's own
+// environment (it runs UniformQuantizer / MinMaxObserver on CPU tensors, BASELINE C1).
+// Native C++ loops with the kernels' element arithmetic (vsiq_common.cuh): IEEE fp32
+// division, rint (half to even), the NaN-propagating clamp that keeps -0.0, f64 qparams
+// with Python round()'s NaN-for-raise convention, and the SiLU exp split of torch's CPU
+// kernel.  Work is cut into fixed 64K-element chunks folded in chunk order, so every
+// result is independent of the number of host threads (VSIQ_HOST_THREADS, default the
+// CPUs this process may run on).  No device memory, no HIP calls.
+#include <sched.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "vsiq_common.cuh"
+
+namespace vsiq {
+namespace host {
+
+constexpr int64_t kChunk = 1 << 16;
+
+inline int usable_cpus() {
+  static const int n = [] {
+    if (const char *e = std::getenv("VSIQ_HOST_THREADS")) {
+      const int v = std::atoi(e);
+      if (v > 0) return v;
+    }
+    cpu_set_t s;
+    if (sched_getaffinity(0, sizeof s, &s) == 0) return CPU_COUNT(&s);
+    const int h = (int)std::thread::hardware_concurrency();
+    return h > 0 ? h : 1;
+  }();
+  return n;
+}
+
+// f(chunk, begin, end) over the fixed chunks of [0, n), on up to usable_cpus() threads
+template <class F>
+void for_chunks(int64_t n, F &&f) {
+  const int64_t nc = cdiv(n, kChunk);
+  const int t = (int)std::min<int64_t>(usable_cpus(), nc);
+  auto run = [&](int64_t c) { f(c, c * kChunk, std::min<int64_t>(n, (c + 1) * kChunk)); };
+  if (t <= 1) {
+    for (int64_t c = 0; c < nc; ++c) run(c);
+    return;
+  }
+  std::atomic<int64_t> next{0};
+  std::vector<std::thread> th;
+  th.reserve(t);
+  for (int i = 0; i < t; ++i)
+    th.emplace_back([&] {
+      for (int64_t c; (c = next.fetch_add(1)) < nc;) run(c);
+    });
+  for (auto &x : th) x.join();
+}
+
+inline float act_at(float c, int kind, int64_t e, const SiluLay &L) {
+  if (kind == kActRelu) return c < 0.0f ? 0.0f : c;
+  if (kind == kActSilu) return (L.on && (silu_scalar4(e, L) & 1u)) ? silu_fwd<true>(c) : silu_fwd<false>(c);
+  return c;
+}
+
+inline float act_bwd_at(float g, float c, int kind, int64_t e, const SiluLay &L) {
+  if (kind == kActRelu) return c <= 0.0f ? 0.0f : g;
+  if (kind == kActSilu) return (L.on && (silu_scalar4(e, L) & 1u)) ? silu_bwd<true>(g, c) : silu_bwd<false>(g, c);
+  return g;
+}
+
+struct HQP {
+  float s, z, lo, hi;
+};
+
+// uniform.py:98-102 for a learned zero point: clamp(round(zp), qmin, qmax) in f64
+inline HQP make_hqp(double s, double z, int zround, int qmin, int qmax) {
+  if (zround) {
+    const double zr = __builtin_rint(z);
+    z = zr < (double)qmin ? (double)qmin : (zr > (double)qmax ? (double)qmax : zr);
+  }
+  return HQP{(float)s, (float)z, (float)qmin, (float)qmax};
+}
+
+// uniform.py:55,95: r = rint(x / s + zp); q = clamp(r); y = (q - zp) * s
+inline float fq(float x, const HQP &p, int discrete, bool *m, uint8_t *code) {
+  float u = x / p.s;
+  u = u + p.z;
+  const float r = __builtin_rintf(u);
+  const float q = r < p.lo ? p.lo : (r > p.hi ? p.hi : r);
+  *m = r >= p.lo && r <= p.hi;
+  *code = q == q ? (uint8_t)((int)q & 0xff) : 0;
+  return discrete ? q : (q - p.z) * p.s;
+}
+
+}  // namespace host
+}  // namespace vsiq
+
+using namespace vsiq;
+using namespace vsiq::host;
+
+extern "C" {
+
+int vsiq_host_observe_f32(const float *x, int64_t n, int act, double *stats_out, float *run_minmax, double *qp_out,
+                          int symmetric, double qden, double eps) {
+  if (n <= 0 || !x || !act_ok(act)) return VSIQ_E_ARG;
+  const int kind = act_kind(act);
+  const SiluLay L = act_lay(act, n);
+  const int64_t nc = cdiv(n, kChunk);
+  std::vector<double> part((size_t)nc * 6);
+  for_chunks(n, [&](int64_t c, int64_t b, int64_t e) {
+    float mn = __builtin_inff(), mx = -__builtin_inff();
+    double nan = 0.0, sa = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int64_t i = b; i < e; ++i) {
+      const float v = act_at(x[i], kind, i, L);
+      if (v != v) {
+        nan += 1.0;
+      } else {
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+      }
+      const double d = (double)v;
+      sa += __builtin_fabs(d);
+      s1 += d;
+      s2 += d * d;
+    }
+    double *p = &part[(size_t)c * 6];
+    p[0] = mn; p[1] = mx; p[2] = nan; p[3] = sa; p[4] = s1; p[5] = s2;
+  });
+  double f[6] = {__builtin_inf(), -__builtin_inf(), 0.0, 0.0, 0.0, 0.0};
+  for (int64_t c = 0; c < nc; ++c) {   // chunk order: independent of the thread count
+    const double *p = &part[(size_t)c * 6];
+    f[0] = p[0] < f[0] ? p[0] : f[0];
+    f[1] = p[1] > f[1] ? p[1] : f[1];
+    f[2] += p[2]; f[3] += p[3]; f[4] += p[4]; f[5] += p[5];
+  }
+  if (stats_out) write_stats(stats_out, f, n);
+  observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax, qp_out, symmetric, qden, eps);
+  return 0;
+}
+
+int vsiq_host_fq_fwd_f32(const float *x, float *y, uint8_t *codes, uint8_t *mask, int64_t n, int act,
+                         const double *qp, double scale, double zp, int zp_round, int discrete, int qmin,
+                         int qmax) {
+  if (n < 0 || qmin > qmax || (n > 0 && (!x || !y)) || !act_ok(act)) return VSIQ_E_ARG;
+  const HQP p = qp ? make_hqp(qp[VSIQ_QP_SCALE], qp[VSIQ_QP_ZP], 0, qmin, qmax)
+                   : make_hqp(scale, zp, zp_round, qmin, qmax);
+  const int kind = act_kind(act);
+  const SiluLay L = act_lay(act, n);
+  for_chunks(n, [&](int64_t, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      bool m;
+      uint8_t c;
+      y[i] = fq(act_at(x[i], kind, i, L), p, discrete, &m, &c);
+      if (mask) mask[i] = m;
+      if (codes) codes[i] = c;
+    }
+  });
+  return 0;
+}
+
+int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre, float *gx, int64_t n, int act,
+                          double scale) {
+  if (n < 0 || (n > 0 && (!g || !mask || !gx)) || !act_ok(act) || (act_kind(act) != kActNone && !pre))
+    return VSIQ_E_ARG;
+  const float s = (float)scale;
+  const int kind = act_kind(act);
+  const SiluLay L = act_lay(act, n);
+  for_chunks(n, [&](int64_t, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      const float o = (mask[i] ? g[i] * s : 0.0f) / s;   // MulBackward0, ClampBackward1, DivBackward0
+      gx[i] = kind == kActNone ? o : act_bwd_at(o, pre[i], kind, i, L);
+    }
+  });
+  return 0;
+}
+
+int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, int act, double scale, double zp,
+                          int zp_learn, int qmin, int qmax, double gscale, double *grad_out) {
+  if (n <= 0 || !g || !x || !gx || !grad_out || qmin > qmax || !act_ok(act)) return VSIQ_E_ARG;
+  const HQP p = make_hqp(scale, zp, zp_learn, qmin, qmax);
+  const int kind = act_kind(act);
+  const SiluLay L = act_lay(act, n);
+  const int64_t nc = cdiv(n, kChunk);
+  std::vector<double> part((size_t)nc * 2);
+  for_chunks(n, [&](int64_t c, int64_t b, int64_t e) {
+    double st = 0.0, sz = 0.0;
+    for (int64_t i = b; i < e; ++i) {   // autograd of uniform.py:47-56, term by term (k_body.cuh lsq_elem)
+      const float xa = act_at(x[i], kind, i, L);
+      const float u = xa / p.s;
+      const float r = __builtin_rintf(u + p.z);
+      const float q = r < p.lo ? p.lo : (r > p.hi ? p.hi : r);
+      const bool m = r >= p.lo && r <= p.hi;
+      const float gq = g[i] * p.s;
+      const float gm = m ? gq : 0.0f;
+      const float t1 = g[i] * (q - p.z);
+      const float xs = u / p.s;
+      const float t2 = (-gm) * xs;
+      st += (double)t1 + (double)t2;
+      if (zp_learn) sz += (double)gm + (double)(-gq);
+      const float o = gm / p.s;
+      gx[i] = kind == kActNone ? o : act_bwd_at(o, x[i], kind, i, L);
+    }
+    part[(size_t)c * 2] = st;
+    part[(size_t)c * 2 + 1] = sz;
+  });
+  double t = 0.0, z = 0.0;
+  for (int64_t c = 0; c < nc; ++c) {
+    t += part[(size_t)c * 2];
+    z += part[(size_t)c * 2 + 1];
+  }
+  grad_out[0] = t * gscale;
+  if (zp_learn) {   // ClampBackward of zero_point_rounding: the in-range test on round(zp)
+    const double zr = __builtin_rint(zp);
+    grad_out[1] = (zr >= (double)qmin && zr <= (double)qmax) ? z * gscale : 0.0;
+  } else {
+    grad_out[1] = 0.0;
+  }
+  return 0;
+}
+
+int vsiq_host_threads(void) { return usable_cpus(); }
+
+}  // extern "C"

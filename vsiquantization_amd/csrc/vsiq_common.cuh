@@ -1174,8 +1174,8 @@ __device__ __forceinline__ bool wave_arrive(double *ws, uint32_t first, uint32_t
 
 // f64 qparams from the running min/max (observers/minmax.py:49-74).
 // min_val <= 0 <= max_val always holds (state starts at 0/0, minmax.py:28-29).
-__device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, double qden,
-                                               double eps, double *scale, double *zp) {
+__host__ __device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, double qden,
+                                                        double eps, double *scale, double *zp) {
   if (sym) {
     const double a = __builtin_fabs(mn), b = __builtin_fabs(mx);
     const double max_abs = b > a ? b : a;   // Python max(): first unless strictly greater
@@ -1192,13 +1192,34 @@ __device__ __forceinline__ void minmax_qparams(double mn, double mx, int sym, do
   }
 }
 
+// The stats record (VSIQ_ST_*) of one call from its folded {min, max, nan count,
+// sum|x|, sum x, sum x^2}: quantization_manager.py:66-68's fp32 mean(|x|) / mean /
+// unbiased std, NaN when the call held a NaN (torch's fp32 reductions are NaN then).
+__host__ __device__ __forceinline__ void write_stats(double *__restrict__ st, const double (&f)[6], int64_t n) {
+  const double dn = (double)n;
+  const bool has_nan = f[2] > 0.0;
+  st[VSIQ_ST_MIN] = (double)(float)f[0];   // NaN-ignoring; see VSIQ_ST_NAN
+  st[VSIQ_ST_MAX] = (double)(float)f[1];
+  st[VSIQ_ST_NAN] = f[2];
+  st[VSIQ_ST_SUMABS] = f[3];
+  st[VSIQ_ST_SUM] = f[4];
+  st[VSIQ_ST_SUMSQ] = f[5];
+  st[VSIQ_ST_N] = dn;
+  const double mean = f[4] / dn;
+  const double var = (f[5] - f[4] * mean) / (dn - 1.0);
+  st[VSIQ_ST_MEANABS] = has_nan ? __builtin_nan("") : (double)(float)(f[3] / dn);
+  st[VSIQ_ST_MEAN] = has_nan ? __builtin_nan("") : (double)(float)mean;
+  st[VSIQ_ST_STD] = (has_nan || n < 2) ? __builtin_nan("")
+                                       : (double)(float)__builtin_sqrt(var > 0.0 ? var : 0.0);
+}
+
 // Running-state update + qparams (observers/minmax.py:42-47 then :49-74).  A call
 // whose tensor holds a NaN changes nothing: `nan < v` is False in Python.
 // Returns the f64 (scale, zp) in *s_out / *z_out when those are given.
-__device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_nan,
-                                                float *run_minmax, double *qp_out, int sym,
-                                                double qden, double eps, double *s_out = nullptr,
-                                                double *z_out = nullptr) {
+__host__ __device__ __forceinline__ void observer_update(float cmn, float cmx, bool has_nan,
+                                                         float *run_minmax, double *qp_out, int sym,
+                                                         double qden, double eps, double *s_out = nullptr,
+                                                         double *z_out = nullptr) {
   float mn = 0.f, mx = 0.f;
   if (run_minmax) { mn = run_minmax[0]; mx = run_minmax[1]; }
   if (!has_nan) {

@@ -1,4 +1,5 @@
-"""torch-facing fake-quant ops over the HIP C ABI (no CPU path).
+"""torch-facing fake-quant ops over the HIP C ABI (CPU tensors: the native host loops of
+host.py, never the oracle).
 
 Each op here is one (or two) kernel launches on the tensor's current HIP
 stream, no host synchronisation, and is the MI355X replacement of one chain of
@@ -11,6 +12,7 @@ eager torch ops in the reference:
   FakeQuantLearnFn         autograd of uniform.py:47-56 (LSQ: ScaleGradient, STE) (K4)
   FakeQuantLearnMultiFn    FakeQuantLearnFn over many tensors in one launch each way
   observe_parts/fold_parts deferred-calibration observer (K2p) and its one-launch fold
+  observe_parts_out        K2p that also writes act(x): a fused layer's calibration forward (K2o)
 
 Every op takes an optional ``act`` ("relu" / "silu", K5): the op is then applied
 to act(x) without materializing it -- the fused layers' F.relu / F.silu before
@@ -26,6 +28,7 @@ import numpy as np
 import torch
 
 from . import _hip as H
+from . import host as _host
 
 
 # --------------------------------------------------------------------------- scalars
@@ -71,7 +74,11 @@ def fake_quant(x: torch.Tensor, scale, zero_point, qmin: int, qmax: int, *, zp_r
 
     qp: optional observer record (f64[QP_LEN] on x.device) used instead of scale/zero_point.
     discrete: return the integer-valued fp32 codes in y instead (discreate_tensor).
-    Returns (y, mask|None, codes|None); codes int8 (qmin<0) or uint8."""
+    Returns (y, mask|None, codes|None); codes int8 (qmin<0) or uint8.  A CPU tensor takes
+    the native host path (host.py; its mask is one byte per element)."""
+    if _host.is_host(x):
+        return _host.fake_quant(x, scale, zero_point, qmin, qmax, zp_round=zp_round, qp=qp, want_mask=want_mask,
+                                want_codes=want_codes, discrete=discrete, act=act)
     x = H.require_device_f32(x)
     dev = x.device
     y = torch.empty_like(x)
@@ -144,15 +151,14 @@ class ActivationFn(torch.autograd.Function):
 
 def activation(x, act):
     """The fused layers' F.relu / F.silu (modules/fused.py:133) as the reference computes
-    them: SiLU of a CUDA fp32 tensor through ActivationFn (torch's HIP silu uses another
-    exp); ReLU through torch (bitwise equal to its CPU kernel); anything else is torch's."""
-    if act == "relu":
-        return torch.nn.functional.relu(x)
-    if act == "silu":
-        if isinstance(x, torch.Tensor) and x.device.type == "cuda" and x.dtype == torch.float32:
-            return ActivationFn.apply(x, act)
-        return torch.nn.functional.silu(x)
-    raise ValueError(f"unsupported fused activation {act!r} ('relu' or 'silu')")
+    them on its CPU tensors: a CUDA fp32 tensor goes through ActivationFn (torch's HIP silu
+    uses another exp, and its HIP relu turns -0.0 into +0.0 where the CPU kernel keeps
+    -0.0); anything else is torch's own CPU op, i.e. the reference's."""
+    if act not in ("relu", "silu"):
+        raise ValueError(f"unsupported fused activation {act!r} ('relu' or 'silu')")
+    if isinstance(x, torch.Tensor) and x.device.type == "cuda" and x.dtype == torch.float32:
+        return ActivationFn.apply(x, act)
+    return torch.nn.functional.relu(x) if act == "relu" else torch.nn.functional.silu(x)
 
 
 class FakeQuantFixedFn(torch.autograd.Function):
@@ -193,7 +199,10 @@ def _qarg(v):
 
 def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None, act=None):
     """Fixed-qparam fake quant; with a gradient-requiring x, the STE backward is attached
-    (C++ node of _vsiq_torch.so, or FakeQuantFixedFn with VSIQ_TORCH_EXT=0)."""
+    (C++ node of _vsiq_torch.so, or FakeQuantFixedFn with VSIQ_TORCH_EXT=0).  CPU tensors:
+    the native host path (host.py)."""
+    if _host.is_host(x):
+        return _host.fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=qp, act=act)
     if x.requires_grad and torch.is_grad_enabled():
         if H.torch_ext_enabled():
             x = H.require_device_f32(x)
@@ -207,7 +216,9 @@ def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None, act=None):
 def fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
     """Learnable fake quant (uniform.py:47-56): K1/K5 forward, K4 backward with the
     ScaleGradient factor ``gscale`` (C++ node of _vsiq_torch.so, or FakeQuantLearnFn
-    with VSIQ_TORCH_EXT=0)."""
+    with VSIQ_TORCH_EXT=0).  CPU tensors: the native host path (host.py)."""
+    if _host.is_host(x):
+        return _host.fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
     if H.torch_ext_enabled():
         x = H.require_device_f32(x)
         st, sh = _qarg(scale)
@@ -369,7 +380,11 @@ def observe_tensor(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, eps: 
                    want_stats: bool = True, act=None):
     """One pass over x: min/max/NaN/sums -> running state update -> f64 qparams (no sync).
 
-    Returns (qp f64[QP_LEN] | None, stats f64[ST_LEN] | None)."""
+    Returns (qp f64[QP_LEN] | None, stats f64[ST_LEN] | None).  CPU tensors: the native
+    host path (host.py; run_minmax a CPU fp32[2])."""
+    if _host.is_host(x):
+        return _host.observe_tensor(x, symmetric=symmetric, num_bits=num_bits, eps=eps, run_minmax=run_minmax,
+                                    want_qp=want_qp, want_stats=want_stats, act=act)
     x = H.require_device_f32(x)
     if x.numel() == 0:
         raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
@@ -487,6 +502,25 @@ def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) ->
                                            _i64(out.numel()), H.stream_of(x.device))
     H.check(rc, "vsiq_act_observe_part_f32")
     return out
+
+
+def observe_parts_out(x: torch.Tensor, act, out: torch.Tensor | None = None):
+    """K2o: y = act(x) and the deferred observer records of act(x) (observe_parts) in ONE
+    pass -- a fused layer's calibration forward (modules/fused.py:133 + minmax.py:42-43).
+    Returns (y, out)."""
+    x = H.require_device_f32(x)
+    if x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    need = part_slot_doubles(x.numel())
+    if out is None:
+        out = torch.empty(need, dtype=torch.float64, device=x.device)
+    elif out.dtype != torch.float64 or out.device != x.device or not out.is_contiguous() or out.numel() < need:
+        raise ValueError("observe_parts_out: out must be a contiguous float64 tensor on x's device")
+    y = torch.empty_like(x)
+    rc = H.lib().vsiq_act_observe_part_out_f32(H.ptr(x), H.ptr(y), _i64(x.numel()), H.act_code(act), H.ptr(out),
+                                               _i64(out.numel()), H.stream_of(x.device))
+    H.check(rc, "vsiq_act_observe_part_out_f32")
+    return y, out
 
 
 def observe_parts_multi(xs, outs, act=None) -> list:

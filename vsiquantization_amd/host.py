@@ -1,0 +1,150 @@
+"""The fake-quant path for CPU tensors: native host loops in the same library
+(csrc/k_host.hip, vsiq_host_* in include/vsiq.h) -- the reference's own environment
+(BASELINE C1: UniformQuantizer / MinMaxObserver on CPU tensors).  Same arithmetic as
+the HIP kernels, bit for bit (IEEE fp32 division, rint, NaN-propagating clamp, f64
+qparams, torch CPU's SiLU); multi-threaded over fixed chunks, results independent of
+the thread count.  This is not a fallback for CUDA tensors: a CUDA tensor never comes
+here, and a missing library raises like every other op.
+"""
+from __future__ import annotations
+
+import numbers
+
+import numpy as np
+import torch
+
+from . import _hip as H
+
+
+def is_host(x) -> bool:
+    """A CPU float32 tensor (the host path's input)."""
+    return isinstance(x, torch.Tensor) and x.device.type == "cpu" and x.dtype == torch.float32
+
+
+def _i64(n):
+    return H.c_i64(int(n))
+
+
+def _num(v) -> float:
+    if isinstance(v, torch.Tensor):
+        if v.numel() != 1:
+            raise ValueError(f"expected a scalar qparam, got shape {tuple(v.shape)}")
+        return float(v.detach().reshape(()).item())
+    if isinstance(v, (numbers.Real, np.floating, np.integer)):
+        return float(v)
+    raise TypeError(f"unsupported qparam type {type(v).__name__}")
+
+
+def _f32(x, what="x"):
+    if x.dtype != torch.float32:
+        raise TypeError(f"{what}: only float32 is supported by the fake-quant path, got {x.dtype}")
+    return x.contiguous()
+
+
+def fake_quant(x, scale, zero_point, qmin, qmax, *, zp_round=False, qp=None, want_mask=False, want_codes=False,
+               discrete=False, act=None):
+    """Host counterpart of fakequant.fake_quant: (y, mask uint8 | None, codes | None)."""
+    x = _f32(x)
+    y = torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.uint8) if want_mask else None
+    codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8) if want_codes else None
+    if qp is not None:
+        qp = qp.detach().to("cpu", torch.float64).contiguous()
+        s = z = 0.0
+    else:
+        s, z = _num(scale), _num(zero_point)
+    rc = H.lib().vsiq_host_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(x.numel()), H.act_code(act),
+                                      H.ptr(qp), s, z, int(bool(zp_round)), int(bool(discrete)), int(qmin), int(qmax))
+    H.check(rc, "vsiq_host_fq_fwd_f32")
+    return y, mask, codes
+
+
+class FixedFn(torch.autograd.Function):
+    """Fixed-qparam fake quant with the reference's STE gradient, on the host."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, qp, act=None):
+        y, mask, _ = fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, want_mask=True, act=act)
+        ctx.code = H.act_code(act)
+        ctx.save_for_backward(mask, x.contiguous())
+        ctx.scale = float(qp[H.QP_SCALE]) if qp is not None else _num(scale)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        mask, x = ctx.saved_tensors
+        g = _f32(gy, "grad_output")
+        gx = torch.empty_like(g)
+        rc = H.lib().vsiq_host_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(x), H.ptr(gx), _i64(g.numel()), ctx.code,
+                                           ctx.scale)
+        H.check(rc, "vsiq_host_ste_bwd_f32")
+        return gx, None, None, None, None, None, None
+
+
+class LearnFn(torch.autograd.Function):
+    """Learnable fake quant (uniform.py:47-56) on the host: forward as fake_quant with the
+    (rounded, clamped) zero point, backward grad_x + the f64 closed-form scale / zero-point
+    gradients times the ScaleGradient factor."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
+        x = _f32(x)
+        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, act=act)
+        ctx.save_for_backward(x)
+        ctx.scale, ctx.zp = scale, zero_point
+        ctx.args = (int(qmin), int(qmax), float(gscale), bool(learn_zp), H.act_code(act))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        qmin, qmax, gscale, learn_zp, code = ctx.args
+        s, z = ctx.scale, ctx.zp
+        g = _f32(gy, "grad_output")
+        gx = torch.empty_like(g)
+        grads = torch.empty(2, dtype=torch.float64)
+        rc = H.lib().vsiq_host_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), code, _num(s), _num(z),
+                                           int(learn_zp), qmin, qmax, gscale, H.ptr(grads))
+        H.check(rc, "vsiq_host_lsq_bwd_f32")
+        gs = gz = None
+        if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
+            gs = grads[0].to(device=s.device, dtype=s.dtype).reshape(s.shape)
+        if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
+            gz = grads[1].to(device=z.device, dtype=z.dtype).reshape(z.shape)
+        return gx, gs, gz, None, None, None, None, None
+
+
+def fake_quant_fixed(x, scale, zero_point, qmin, qmax, qp=None, act=None):
+    if x.requires_grad and torch.is_grad_enabled():
+        return FixedFn.apply(x, scale, zero_point, qmin, qmax, qp, act)
+    return fake_quant(x, scale, zero_point, qmin, qmax, qp=qp, act=act)[0]
+
+
+def fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
+    return LearnFn.apply(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
+
+
+def observe_tensor(x, *, symmetric, num_bits=8, eps=1e-8, run_minmax=None, want_qp=True, want_stats=True,
+                   act=None):
+    """Host counterpart of fakequant.observe_tensor: one pass -> running update (fp32[2]
+    CPU state) -> f64 qparams record, stats record."""
+    from .fakequant import qden
+    x = _f32(x)
+    if x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    qp = torch.empty(H.QP_LEN, dtype=torch.float64) if want_qp else None
+    st = torch.empty(H.ST_LEN, dtype=torch.float64) if want_stats else None
+    if run_minmax is not None and (run_minmax.device.type != "cpu" or run_minmax.dtype != torch.float32):
+        raise ValueError("host observe: the running state must be a CPU float32 tensor")
+    rc = H.lib().vsiq_host_observe_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), H.ptr(st), H.ptr(run_minmax),
+                                       H.ptr(qp), int(bool(symmetric)), qden(symmetric, num_bits, eps), float(eps))
+    H.check(rc, "vsiq_host_observe_f32")
+    return qp, st
+
+
+def threads() -> int:
+    """Host threads the CPU path uses (VSIQ_HOST_THREADS, else the CPUs this process may use)."""
+    return int(H.lib().vsiq_host_threads())
+
+
+__all__ = ["is_host", "fake_quant", "fake_quant_fixed", "fake_quant_learn", "observe_tensor", "threads"]

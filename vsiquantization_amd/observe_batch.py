@@ -10,8 +10,11 @@ when it holds 32 calls or ``VSIQ_OBSERVE_BATCH_BYTES`` of tensors (default 4 GiB
 the 288 GB HBM), when a call comes from another stream, and before anything reads the
 records (``flush``; ``distributed.sync_calibration`` calls it).
 
-A queued tensor must not be modified in place before the flush: its version counter is
-checked and a change raises (set ``VSIQ_OBSERVE_BATCH=0`` to observe every call at once).
+OPT-IN (``VSIQ_OBSERVE_BATCH=1``): a queued tensor is the one the manager hands back to
+the model, and it must not be modified in place before the flush (its version counter is
+checked and a change raises; a write through ``.data`` is not seen).  By default every
+deferred call is observed at once: a fused layer's call in one pass that also writes
+the activation (K2o, ``fakequant.observe_parts_out``), any other call by K2p.
 """
 from __future__ import annotations
 
@@ -23,7 +26,7 @@ MAX_CALLS = 32
 
 
 def enabled() -> bool:
-    return os.environ.get("VSIQ_OBSERVE_BATCH", "1") != "0"
+    return os.environ.get("VSIQ_OBSERVE_BATCH", "0") == "1"
 
 
 def _budget() -> int:
@@ -69,19 +72,25 @@ def _flush(q: _Queue):
         for act in dict.fromkeys(a for _, a, _, _ in ok):
             sel = [(x, s) for x, a, s, _ in ok if a == act]
             observe_parts_multi([x for x, _ in sel], [s for _, s in sel], act=act)
+        for x, _, _, _ in ok:   # x may come from another stream's pool: keep it until K2m ran
+            x.record_stream(q.stream)
         for _, _, slot, _ in changed:   # record count 0: a later fold reads nothing from it
             slot.zero_()
     if changed:
         raise RuntimeError(f"{len(changed)} tensor(s) queued for a deferred observer were modified in place "
-                           "before the observer ran (their calls recorded nothing); set "
-                           "VSIQ_OBSERVE_BATCH=0 to observe each call at once")
+                           "before the observer ran (their calls recorded nothing); unset "
+                           "VSIQ_OBSERVE_BATCH to observe each call at once")
 
 
 def flush(device=None):
-    """Observe every queued call (of ``device``, or of all devices) now."""
+    """Observe every queued call (of ``device``, or of all devices) now; the current stream
+    of each device then waits for its queue's launches (a later fold reads the records)."""
     for dev, q in list(_QUEUES.items()):
         if device is None or torch.device(device) == dev:
+            st = q.stream
             _flush(q)
+            if st is not None and st != torch.cuda.current_stream(dev):
+                torch.cuda.current_stream(dev).wait_stream(st)
 
 
 def pending(device=None) -> int:

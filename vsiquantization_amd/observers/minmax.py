@@ -11,6 +11,9 @@ exact: every value it can hold is an element of an fp32 tensor or the initial 0.
 ``min_val``/``max_val`` read it back lazily (one sync), returning the int ``0``
 the reference starts with until a strictly smaller/larger value arrives.
 
+A CPU tensor takes the same single pass in native host code (host.py; the state is then
+a CPU fp32[2]).
+
 ``get_scale_zero_point``/``forward`` keep the reference's host semantics (Python
 float scale, int zero point, ValueError/OverflowError from ``round`` on a
 non-finite value).  ``observe_device`` is the sync-free path used by
@@ -21,6 +24,7 @@ from __future__ import annotations
 import torch
 
 from .. import _hip as H
+from .. import host
 from ..fakequant import observe_tensor
 from ..utils.registry import register_class
 from .base import BaseObserver
@@ -99,9 +103,12 @@ class MinMaxObserver(BaseObserver):
     def observe_device(self, x, want_stats=True, want_qp=True, act=None):
         """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device.
         ``act``: observe act(x) (fused ReLU/SiLU, K5) without materializing it."""
-        dev = H.require_device_f32(x).device
-        if self._obs_stream is not None and self._obs_stream != torch.cuda.current_stream(dev):
-            self._join()
+        if host.is_host(x):   # CPU tensor: the native host pass (host.py), CPU fp32[2] state
+            dev = x.device
+        else:
+            dev = H.require_device_f32(x).device
+            if self._obs_stream is not None and self._obs_stream != torch.cuda.current_stream(dev):
+                self._join()
         state = self.device_state(dev)
         qp, st = observe_tensor(x, symmetric=self.symmetric, num_bits=self.num_bits, eps=self.eps,
                                 run_minmax=state, want_qp=want_qp, want_stats=want_stats, act=act)

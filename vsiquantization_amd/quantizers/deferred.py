@@ -40,10 +40,15 @@ from .uniform import UniformQuantizer
 # per quantizer of the model).
 _PENDING = {}
 _PENDING_MAX = 1 << 14
+# forward generation (bundle_qparams): a pending entry is consumed by the bundle within
+# the backward pass that created it, so entries older than the previous generation are
+# orphans of a backward that never reached the bundle and are dropped at the next forward
+# (one generation of slack: a checkpointed layer re-runs its forward inside the backward)
+_GEN = [0]
 
 
 class _Fold:
-    __slots__ = ("records", "nrec", "zd", "zh", "gscale", "qmin", "qmax", "learn_zp", "out", "keep")
+    __slots__ = ("records", "nrec", "zd", "zh", "gscale", "qmin", "qmax", "learn_zp", "out", "keep", "gen")
 
 
 def lsq_backward_part(g, x, scale, zero_point, qmin, qmax, learn_zp, act, records):
@@ -98,6 +103,7 @@ class DeferredLearnFn(torch.autograd.Function):
         e.gscale, e.qmin, e.qmax, e.learn_zp = float(gscale), int(qmin), int(qmax), bool(learn_zp)
         e.out = torch.empty(2, dtype=torch.float64, device=dev)
         e.keep = (s, z)
+        e.gen = _GEN[0]
         _PENDING[e.out.data_ptr()] = e
         while len(_PENDING) > _PENDING_MAX:
             _PENDING.pop(next(iter(_PENDING)))
@@ -155,6 +161,10 @@ def _eligible(qm) -> bool:
 
 def bundle_qparams(managers) -> int:
     """Route the eligible managers' next learnable call through one QParamBundleFn node."""
+    _GEN[0] += 1
+    stale = [k for k, e in _PENDING.items() if e.gen < _GEN[0] - 1]
+    for k in stale:
+        del _PENDING[k]
     picked = [qm for qm in managers if _eligible(qm)]
     if not picked or not torch.is_grad_enabled():
         return 0

@@ -178,6 +178,16 @@ class QuantizationManager(nn.Module):
             self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
 
     def _observe_host(self, x):
+        from .. import host
+        obs = self.observer
+        if host.is_host(x) and isinstance(obs, MinMaxObserver) and not isinstance(obs, PerChannelMinMaxObserver):
+            # CPU tensor, this package's observer: one native host pass (host.py) for the
+            # running state and the mean|x| / mean / std record; qparams as the
+            # reference's host numbers (minmax.py:49-74)
+            _, st = obs.observe_device(x.detach(), want_qp=False)
+            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+            self.scale, self.zero_point = obs.get_scale_zero_point()
+            return
         # third-party observer: the reference's host path
         xd = x.detach()
         self._materialize_stats()
@@ -199,7 +209,7 @@ class QuantizationManager(nn.Module):
             if not self._pending_records:
                 self._calib_init = (obs.min_val, obs.max_val)
             slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
-            if observe_batch.enabled():   # queued: one K2m launch per up to 32 calls
+            if observe_batch.enabled():   # opt-in queue: one K2m launch per up to 32 calls
                 observe_batch.add(x, act, slot)
                 self._pending_records.append(slot)
             else:
@@ -247,6 +257,10 @@ class QuantizationManager(nn.Module):
         this package's kernels it is fused into the observer and the fake quant (K5)."""
         if self.is_quantize or self.is_learning_scale:
             self._join()
+        if (act is not None and not self.is_quantize and self.dist_defer and not self.is_learning_scale
+                and self.is_observer_qparam and self._act_fusable(x)
+                and not (x.requires_grad and torch.is_grad_enabled())):
+            return self._observe_deferred_act(x, act)
         if act is not None and not (self.is_quantize and self._act_fusable(x)):
             x, act = _activation(x, act), None
         if act is None and (self.is_quantize and not self.is_learning_scale and self.is_observer_qparam
@@ -278,6 +292,22 @@ class QuantizationManager(nn.Module):
             return self.quantizer.quantize(x, self.scale, self.zero_point, self.is_learning_scale,
                                            act=act)
         return x
+
+    def _observe_deferred_act(self, x, act):
+        """A fused layer's deferred calibration call (calibrate_qat_model's default mode):
+        y = act(x), which the next layer consumes, and this call's K2p records of act(x) in
+        ONE pass (K2o, fakequant.observe_parts_out).  Nothing is queued, so user code may
+        modify y in place (ReLU(inplace=True), a residual +=) before calibration ends."""
+        from ..fakequant import observe_parts_out
+        self._join()
+        self._x_device = x.device
+        obs = self.observer
+        if not self._pending_records:
+            self._calib_init = (obs.min_val, obs.max_val)
+        slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
+        y, _ = observe_parts_out(x, act, out=slot)
+        self._pending_records.append(slot)
+        return y
 
     def _observe_quantize_ranks(self, x, act):
         """Multi-GPU per-call observe + quantize (dist_group set, not deferred): the local

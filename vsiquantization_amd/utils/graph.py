@@ -23,6 +23,16 @@ import torch
 from .. import _hip as H
 
 
+def _detached(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach()
+    if isinstance(v, (list, tuple)):
+        return type(v)(_detached(u) for u in v)
+    if isinstance(v, dict):
+        return {k: _detached(u) for k, u in v.items()}
+    return v
+
+
 class GraphedStep:
     """Capture ``fn`` (no arguments; reads and writes persistent tensors) into a HIP graph.
 
@@ -59,8 +69,17 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(side)
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
+        before = set(H._WS)
         with torch.cuda.graph(self.graph):
-            self.out = fn()
+            out = fn()
+        # keep the outputs' storage (every replay rewrites it), not their autograd graph:
+        # a live graph would keep the parameters' AccumulateGrad nodes of the capture
+        # stream alive into later eager steps (torch's stream-mismatch warning)
+        self.out = _detached(out)
+        del out
+        # the capture's own reduction workspaces / counters (one per capture, from the
+        # graph's pool): released with this object, not kept by _hip's table forever
+        self._ws_keys = [k for k in H._WS if k not in before]
 
     def _pending(self) -> int:
         n = H.gate_tuning_pending()
@@ -82,3 +101,18 @@ class GraphedStep:
     def __call__(self):
         self.graph.replay()
         return self.out
+
+    def release(self):
+        """Drop the graph and the workspaces its capture allocated."""
+        for k in getattr(self, "_ws_keys", ()):
+            H._WS.pop(k, None)
+        self._ws_keys = []
+        self.graph = None
+        self.out = None
+
+    def __del__(self):
+        try:
+            for k in getattr(self, "_ws_keys", ()):
+                H._WS.pop(k, None)
+        except Exception:   # interpreter shutdown
+            pass
