@@ -451,6 +451,14 @@ def test_tail_groups_and_mask_bits_per_tensor():
         G.assert_bitwise_f32(npy(gx), O.fq_backward_fixed(g, mo, 0.4), "gx")
 
 
-def test_cpu_tensor_fails_loudly():
+def test_cpu_tensor_takes_the_host_path():
+    """A CPU tensor is computed by the native host loops (vsiquantization_amd/host.py),
+    stays on the CPU and equals the oracle; a CUDA op handed a CPU operand still raises."""
+    x = np.random.default_rng(3).standard_normal(1000).astype(np.float32)
+    y = V.UniformQuantizer(8, True).quantize(torch.from_numpy(x), 0.1, 0, False)
+    assert y.device.type == "cpu"
+    G.assert_bitwise_f32(y.numpy(), O.fq_forward(x, 0.1, 0, -128, 127)[0], "host y")
+    g = torch.randn(64, device=DEV)
+    _, mask, _ = FQ.fake_quant(g, 0.1, 0, -128, 127, want_mask=True)
     with pytest.raises(H.VsiqError):
-        V.UniformQuantizer(8, True).quantize(torch.randn(8), 0.1, 0, False)
+        FQ.ste_backward(g, mask, 0.1, pre=torch.randn(64), act="relu")
