@@ -399,12 +399,13 @@ int vsiq_lsq_bwd_multi_f32(const vsiq_lsq_tensor *tensors, int count, double *ws
  * last-block fold (3-5 us of every K4 launch at 2-26M elements).  vsiq_lsq_fold_multi
  * then folds `count` such calls (each its own records) into grad_out[2] = {grad_scale,
  * grad_zp} exactly as vsiq_act_lsq_bwd_f32 defines them (to float64 summation order), 64
- * calls per launch.  The activation quantizers of a QAT model (quantize_out of every fused
+ * calls per launch pair (chunk folds, then the per-call folds); the fold uses the records
+ * as its scratch (their contents are overwritten).  The activation quantizers of a QAT model (quantize_out of every fused
  * layer, fake_quantize.py:49-50 -> uniform.py:47-56) are folded in one launch when
  * autograd has been through all of them (quantizers/deferred.py).
  */
 typedef struct vsiq_lsq_fold {
-  const double *records;   /* the call's records, nrec x {sum t, sum z} */
+  double *records;         /* the call's records, nrec x {sum t, sum z} (overwritten) */
   int64_t nrec;            /* vsiq_lsq_part_records(n) of the call */
   const double *zp_dev;    /* the zero point the forward used (NULL: zp_host) */
   double zp_host;

@@ -66,11 +66,21 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
                        gx, n, src, gscale, L, grad_out, ws, counter);
 }
 
+// Records-only K4 (K4d): groups per lane 2.  Without an arrival chain more, smaller
+// workgroups cost nothing and stream better at every C4 size (MI355X kernel trace, 3.3M
+// -> 105M elements: 9.8 / 16.1 / 27.7 / 51.1 / 100.1 / 204.5 us at 2 per lane against
+// 10.9 / 16.4 / 28.3 / 53.6 / 102.6 / 207.1 us at K4's 4 / 8, profiles/r03g_c4_groups.txt);
+// the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
+inline int lsq_part_groups_per_lane() {
+  const int g = g_tune.lsq_groups;
+  return g > 0 ? g : 2;
+}
+
 template <int ACT, bool VEC, bool NT>
 void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
                     double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                     const SiluLay &L, hipStream_t st) {
-  const int per_lane = lsq_groups_per_lane(cdiv(n, 4));
+  const int per_lane = counter ? lsq_groups_per_lane(cdiv(n, 4)) : lsq_part_groups_per_lane();
   if (per_lane == kLsqGroups)
     launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 8)
@@ -116,7 +126,7 @@ int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, 
   if (n <= 0 || !g || !x || !gx || !records || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
-  const int64_t grid = lsq_grid(cdiv(n, 4));
+  const int64_t grid = lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane());
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (records_len < 2 * grid) return VSIQ_E_WS;
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
@@ -127,15 +137,24 @@ int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, 
 }
 
 // ----------------------------------------------------------------------------
-// Fold of records-only K4 calls: workgroup t folds call t's block records (thread j
-// sums records j, j + 256, ... in order, then the fixed block tree) -> grad_out[t] =
-// {sum t * gscale, ClampBackward of the rounded zp ? sum z * gscale : 0}
-// (quantizers/uniform.py:47-56 + ScaleGradient :242-255, zero_point_rounding :98-102).
+// Fold of records-only K4 calls, two launches (quantizers/uniform.py:47-56 + ScaleGradient
+// :242-255, zero_point_rounding :98-102):
+//   k_lsq_fold_chunks  one workgroup per chunk of kFoldChunk records of a call: every
+//                      thread issues its 4 record loads at once, adds them in order, the
+//                      fixed block tree sums the workgroup; the chunk's {sum t, sum z}
+//                      replaces the chunk's first record (the records are scratch);
+//   k_lsq_fold_multi   workgroup t folds call t's chunk sums in chunk order -> grad_out[t]
+//                      = {sum t * gscale, ClampBackward of round(zp) ? sum z * gscale : 0}.
+// Deterministic (fixed chunks, fixed trees).  Round 2's single launch walked a call's
+// records with one dependent load round trip per 256 records (14.6 us at C4, 54.6 us
+// with the 4x record count of 2 groups per lane, profiles/r03g_c4_groups.txt).
 // ----------------------------------------------------------------------------
-constexpr int kFoldMulti = 64;   // calls per launch (descriptor table in the kernel arguments)
+constexpr int kFoldMulti = 64;    // calls per launch pair (descriptor table in the kernel arguments)
+constexpr int kFoldPer = 4;       // records per thread of a chunk workgroup
+constexpr int64_t kFoldChunk = (int64_t)kBlock * kFoldPer;
 
 struct FCall {
-  const double *rec;
+  double *rec;
   const double *zdev;
   double *out;
   int64_t nrec;
@@ -146,15 +165,44 @@ struct FCall {
 
 struct FBatch {
   FCall t[kFoldMulti];
+  uint32_t c0[kFoldMulti + 1];   // first chunk workgroup of each call
   int count;
 };
 
+__global__ __launch_bounds__(kBlock) void k_lsq_fold_chunks(const FBatch b) {
+  int t = 0;
+  const uint32_t blk = blockIdx.x;
+  while (t + 1 < b.count && blk >= b.c0[t + 1]) ++t;   // scalar: c0 is a kernel argument
+  const FCall &T = b.t[t];
+  const int64_t r0 = (int64_t)(blk - b.c0[t]) * kFoldChunk;
+  double2 v[kFoldPer];
+#pragma unroll
+  for (int k = 0; k < kFoldPer; ++k) {
+    const int64_t i = r0 + threadIdx.x + (int64_t)k * kBlock;
+    v[k] = i < T.nrec ? *reinterpret_cast<const double2 *>(T.rec + 2 * i) : double2{0.0, 0.0};
+  }
+  LsqAcc acc{0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < kFoldPer; ++k) {
+    if (r0 + threadIdx.x + (int64_t)k * kBlock < T.nrec) {
+      acc.t += v[k].x;
+      acc.z += v[k].y;
+    }
+  }
+  lsq_block_reduce(acc);   // every thread's loads were consumed before its first barrier
+  if (threadIdx.x == 0) {
+    T.rec[2 * r0] = acc.t;
+    T.rec[2 * r0 + 1] = acc.z;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_lsq_fold_multi(const FBatch b) {
   const FCall &T = b.t[blockIdx.x];
+  const int64_t nch = cdiv(T.nrec, kFoldChunk);
   LsqAcc acc{0.0, 0.0};
-  for (int64_t i = threadIdx.x; i < T.nrec; i += kBlock) {
-    acc.t += T.rec[2 * i];
-    acc.z += T.rec[2 * i + 1];
+  for (int64_t c = threadIdx.x; c < nch; c += kBlock) {
+    acc.t += T.rec[2 * c * kFoldChunk];
+    acc.z += T.rec[2 * c * kFoldChunk + 1];
   }
   lsq_block_reduce(acc);
   if (threadIdx.x == 0) {
@@ -584,7 +632,7 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
 
 int64_t vsiq_lsq_part_records(int64_t n) {
   if (n <= 0) return VSIQ_E_ARG;
-  return lsq_grid(cdiv(n, 4));
+  return lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane());
 }
 
 int vsiq_act_lsq_bwd_part_f32(const float *g, const float *c, float *gc, int64_t n, int act,
@@ -603,13 +651,20 @@ int vsiq_lsq_fold_multi(const vsiq_lsq_fold *folds, int count, void *stream) {
   for (int i0 = 0; i0 < count; i0 += kFoldMulti) {
     FBatch b{};
     b.count = std::min(kFoldMulti, count - i0);
+    uint32_t chunks = 0;
     for (int k = 0; k < b.count; ++k) {
       const vsiq_lsq_fold &F = folds[i0 + k];
       b.t[k] = FCall{F.records, F.zp_dev, F.grad_out, F.nrec, F.zp_host, F.gscale, (float)F.qmin, (float)F.qmax,
                      F.zp_learn};
+      b.c0[k] = chunks;
+      chunks += (uint32_t)cdiv(F.nrec, kFoldChunk);
     }
+    b.c0[b.count] = chunks;
+    hipLaunchKernelGGL(k_lsq_fold_chunks, dim3(chunks), dim3(kBlock), 0, (hipStream_t)stream, b);
+    int rc = launch_rc();
+    if (rc) return rc;
     hipLaunchKernelGGL(k_lsq_fold_multi, dim3((unsigned)b.count), dim3(kBlock), 0, (hipStream_t)stream, b);
-    const int rc = launch_rc();
+    rc = launch_rc();
     if (rc) return rc;
   }
   return 0;

@@ -9,29 +9,41 @@
 // the engine runs without the GIL.  Numerics are the kernels' own: every result is
 // bit-identical to the ctypes path (tests/test_gpu_torch_ext.py).
 //
+// Round 3: the nodes are plain torch::autograd::Node subclasses wired by hand (the way
+// torch's generated ops are), not torch::autograd::Function<>: no IValue-keyed
+// saved_data dictionary, no output wrapping of the non-differentiable qparam outputs
+// (they are ordinary tensors without history), one SavedVariable where a version check
+// is needed.  The learnable node also takes its reduction workspace from a per-(device,
+// stream | capture) cache here instead of from Python.
+//
 // Each node mirrors one Python autograd.Function of vsiquantization_amd/fakequant.py:
-//   PcObserveFq   PerChannelObserveFQFn  (K3 forward, STE backward from the 1-bit mask)
-//   FqFixed       FakeQuantFixedFn       (K1 / K5 forward, STE backward)
-//   FqLearn       FakeQuantLearnFn       (K1 / K5 forward, K4 backward: grad_x, d scale, d zp)
+//   PcObserveFqBackward  PerChannelObserveFQFn  (K3 forward, STE backward from the 1-bit mask)
+//   FqFixedBackward      FakeQuantFixedFn       (K1 / K5 forward, STE backward)
+//   FqLearnBackward      FakeQuantLearnFn       (K1 / K5 forward, K4 backward: grad_x, d scale, d zp)
 // Inputs are validated on the Python side (CUDA, float32, contiguous); the library
 // never allocates: every buffer here comes from torch's caching allocator, every
 // launch goes to torch's current HIP stream of the tensor's device.
 #include <torch/extension.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/functions/utils.h>
+#include <torch/csrc/autograd/saved_variable.h>
 #include <c10/hip/HIPStream.h>
 
+#include <map>
+#include <mutex>
 #include <optional>
+#include <tuple>
 
 #include "vsiq.h"
 
 namespace {
 
-using torch::autograd::AutogradContext;
+using torch::autograd::Node;
+using torch::autograd::SavedVariable;
 using torch::autograd::variable_list;
 using at::Tensor;
 
-void *stream_of(const Tensor &t) {
-  return (void *)c10::hip::getCurrentHIPStream(t.device().index()).stream();
-}
+hipStream_t stream_of(const Tensor &t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 void check(int rc, const char *what) {
   TORCH_CHECK(rc == 0, what, " failed (", rc, "): ", vsiq_error_string(rc));
@@ -59,164 +71,229 @@ Tensor mask_buffer(int64_t rows, int64_t rowlen, const Tensor &like) {
   return at::empty({std::max<int64_t>(words, 1)}, like.options().dtype(at::kLong));
 }
 
-// --------------------------------------------------------------------------- K3 + STE
-struct PcObserveFq : public torch::autograd::Function<PcObserveFq> {
-  static variable_list forward(AutogradContext *ctx, Tensor x, Tensor run_min, Tensor run_max,
-                               bool sym, int64_t qmin, int64_t qmax, double qden, double eps,
-                               bool want_row_stats) {
-    const int64_t C = x.dim() > 0 ? x.size(0) : 1;
-    const int64_t rowlen = C > 0 ? x.numel() / C : 0;
-    Tensor y = at::empty_like(x);
-    // separate buffers, not rows of one: view outputs cost the engine extra bookkeeping
-    Tensor scale = at::empty({C}, x.options().dtype(at::kDouble));
-    Tensor zp = at::empty({C}, x.options().dtype(at::kDouble));
-    Tensor mask = mask_buffer(C, rowlen, x);
-    Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble))
-                               : at::empty({0}, x.options().dtype(at::kDouble));
-    check(vsiq_pc_observe_fq_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), C, rowlen,
-                                 ptr<float>(run_min), ptr<float>(run_max), ptr<double>(scale),
-                                 ptr<double>(zp), want_row_stats ? ptr<double>(rs) : nullptr, sym ? 1 : 0,
-                                 (int)qmin, (int)qmax, qden, eps, stream_of(x)),
-          "vsiq_pc_observe_fq_f32");
-    ctx->save_for_backward({mask, scale});
-    ctx->mark_non_differentiable({scale, zp, rs});
-    // the engine would otherwise materialize zero gradients for the three
-    // non-differentiable outputs (two allocations + fill launches per backward)
-    ctx->set_materialize_grads(false);
-    return {y, scale, zp, rs};
-  }
+bool needs_grad(const Tensor &t) { return t.defined() && t.requires_grad(); }
 
-  static variable_list backward(AutogradContext *ctx, variable_list grads) {
-    if (!grads[0].defined())
-      return {Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
-    const auto saved = ctx->get_saved_variables();
+// Reduction workspace + self-resetting arrival counter per (device, stream), or per HIP
+// graph capture (every graph its own, from that graph's pool: graphs replayed
+// concurrently on two streams never share a counter) -- _hip.workspace's C++ twin.
+struct Ws {
+  Tensor ws, counter;
+};
+std::mutex g_ws_mu;
+std::map<std::tuple<int, void *, unsigned long long>, Ws> g_ws;
+
+Ws &workspace(const Tensor &like, int64_t n) {
+  const int dev = like.device().index();
+  const hipStream_t st = stream_of(like);
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(st, &status, &cid) != hipSuccess || status != hipStreamCaptureStatusActive) cid = 0;
+  const auto key = std::make_tuple(dev, cid ? nullptr : (void *)st, cid);
+  const int64_t need = vsiq_workspace_doubles(n);
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  Ws &w = g_ws[key];
+  if (!w.counter.defined()) w.counter = at::zeros({VSIQ_COUNTER_WORDS}, like.options().dtype(at::kInt));
+  if (!w.ws.defined() || w.ws.numel() < need) w.ws = at::empty({need}, like.options().dtype(at::kDouble));
+  return w;
+}
+
+// drop the workspaces of finished captures (utils.graph.GraphedStep.release)
+void release_captures(const std::vector<int64_t> &ids) {
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  for (auto it = g_ws.begin(); it != g_ws.end();) {
+    bool drop = false;
+    for (int64_t id : ids) drop = drop || std::get<2>(it->first) == (unsigned long long)id;
+    it = drop ? g_ws.erase(it) : std::next(it);
+  }
+}
+
+int64_t capture_workspaces() {
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  int64_t n = 0;
+  for (auto &kv : g_ws) n += std::get<2>(kv.first) != 0;
+  return n;
+}
+
+// --------------------------------------------------------------------------- K3 + STE
+struct PcObserveFqBackward : public Node {
+  Tensor mask, scale;   // internal buffers: no version check needed
+  std::string name() const override { return "PcObserveFqBackward"; }
+  void release_variables() override {
+    mask.reset();
+    scale.reset();
+  }
+  variable_list apply(variable_list &&grads) override {
+    TORCH_CHECK(mask.defined(), "PcObserveFqBackward: backward through the graph a second time");
+    if (!grads[0].defined()) return {Tensor()};
     const Tensor g = grads[0].contiguous();
     Tensor gx = at::empty_like(g);
-    const int64_t C = saved[1].numel();   // one scale per row
+    const int64_t C = scale.numel();   // one scale per row
     const int64_t rowlen = C > 0 ? g.numel() / C : 0;
-    check(vsiq_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(saved[0]), ptr<float>(gx), g.numel(),
-                           ptr<double>(saved[1]), rowlen, 0.0, stream_of(g)),
+    check(vsiq_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(mask), ptr<float>(gx), g.numel(), ptr<double>(scale), rowlen,
+                           0.0, stream_of(g)),
           "vsiq_ste_bwd_f32");
-    return {gx, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+    return {gx};
   }
 };
 
-std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool sym, int64_t qmin,
-                                  int64_t qmax, double qden, double eps, bool want_row_stats) {
-  return PcObserveFq::apply(x, run_min, run_max, sym, qmin, qmax, qden, eps, want_row_stats);
+std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool sym, int64_t qmin, int64_t qmax,
+                                  double qden, double eps, bool want_row_stats) {
+  const int64_t C = x.dim() > 0 ? x.size(0) : 1;
+  const int64_t rowlen = C > 0 ? x.numel() / C : 0;
+  Tensor y = at::empty_like(x);
+  Tensor scale = at::empty({C}, x.options().dtype(at::kDouble));
+  Tensor zp = at::empty({C}, x.options().dtype(at::kDouble));
+  const bool grad = torch::autograd::compute_requires_grad(x);
+  Tensor mask = grad ? mask_buffer(C, rowlen, x) : Tensor();
+  Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble))
+                             : at::empty({0}, x.options().dtype(at::kDouble));
+  check(vsiq_pc_observe_fq_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), C, rowlen,
+                               ptr<float>(run_min), ptr<float>(run_max), ptr<double>(scale), ptr<double>(zp),
+                               want_row_stats ? ptr<double>(rs) : nullptr, sym ? 1 : 0, (int)qmin, (int)qmax, qden,
+                               eps, stream_of(x)),
+        "vsiq_pc_observe_fq_f32");
+  if (grad) {
+    auto node = std::shared_ptr<PcObserveFqBackward>(new PcObserveFqBackward(), torch::autograd::deleteNode);
+    node->set_next_edges(torch::autograd::collect_next_edges(x));
+    node->mask = mask;
+    node->scale = scale;
+    torch::autograd::set_history(y, node);
+  }
+  return {y, scale, zp, rs};
 }
 
 // --------------------------------------------------------------------------- K1/K5 + STE
-struct FqFixed : public torch::autograd::Function<FqFixed> {
-  static Tensor forward(AutogradContext *ctx, Tensor x, std::optional<Tensor> scale, double scale_host,
-                        std::optional<Tensor> zp, double zp_host, int64_t qmin, int64_t qmax,
-                        std::optional<Tensor> qp, int64_t act) {
-    Tensor y = at::empty_like(x);
-    Tensor mask = mask_buffer(1, x.numel(), x);
-    Tensor qpt = qp.has_value() ? *qp : Tensor();
-    Tensor sd = qpt.defined() ? Tensor() : f64_on(scale, x);
-    Tensor zd = qpt.defined() ? Tensor() : f64_on(zp, x);
-    check(vsiq_act_fq_fwd_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), x.numel(), (int)act,
-                              ptr<double>(qpt), ptr<double>(sd), scale_host, ptr<double>(zd), zp_host, 0, 0,
-                              (int)qmin, (int)qmax, stream_of(x)),
-          "vsiq_act_fq_fwd_f32");
-    // backward scale: the qparams record's scale entry, the device scale, or the host value
-    // (held outside save_for_backward, like the Python Function's ctx.scale: an in-place
-    // update of a scale tensor between forward and backward is not a version error)
-    Tensor sb = qpt.defined() ? qpt.narrow(0, VSIQ_QP_SCALE, 1) : sd;
-    ctx->save_for_backward({mask, act != VSIQ_ACT_NONE ? x : Tensor()});
-    ctx->saved_data["has_sb"] = sb.defined();
-    if (sb.defined()) ctx->saved_data["sb"] = sb;
-    ctx->saved_data["scale_host"] = scale_host;
-    ctx->saved_data["act"] = act;
-    return y;
+struct FqFixedBackward : public Node {
+  Tensor mask, sb;      // internal mask; scale for the backward (record entry / device copy)
+  SavedVariable pre;    // the pre-activation (act != NONE): version-checked like an input
+  double scale_host = 0.0;
+  int act = VSIQ_ACT_NONE;
+  std::string name() const override { return "FqFixedBackward"; }
+  void release_variables() override {
+    mask.reset();
+    sb.reset();
+    pre.reset_data();
   }
-
-  static variable_list backward(AutogradContext *ctx, variable_list grads) {
-    const auto saved = ctx->get_saved_variables();
+  variable_list apply(variable_list &&grads) override {
+    TORCH_CHECK(mask.defined(), "FqFixedBackward: backward through the graph a second time");
+    if (!grads[0].defined()) return {Tensor()};
     const Tensor g = grads[0].contiguous();
     Tensor gx = at::empty_like(g);
-    const int act = (int)ctx->saved_data["act"].toInt();
-    const Tensor sb = ctx->saved_data["has_sb"].toBool() ? ctx->saved_data["sb"].toTensor() : Tensor();
-    check(vsiq_act_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(saved[0]), act ? ptr<float>(saved[1]) : nullptr,
-                               ptr<float>(gx), g.numel(), act, ptr<double>(sb), 0,
-                               ctx->saved_data["scale_host"].toDouble(), stream_of(g)),
+    const Tensor c = act != VSIQ_ACT_NONE ? pre.unpack() : Tensor();
+    check(vsiq_act_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(mask), ptr<float>(c), ptr<float>(gx), g.numel(), act,
+                               ptr<double>(sb), 0, scale_host, stream_of(g)),
           "vsiq_act_ste_bwd_f32");
-    return {gx, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+    return {gx};
   }
 };
 
-Tensor fq_fixed(Tensor x, std::optional<Tensor> scale, double scale_host, std::optional<Tensor> zp,
-                double zp_host, int64_t qmin, int64_t qmax, std::optional<Tensor> qp, int64_t act) {
-  return FqFixed::apply(x, scale, scale_host, zp, zp_host, qmin, qmax, qp, act);
+Tensor fq_fixed(Tensor x, std::optional<Tensor> scale, double scale_host, std::optional<Tensor> zp, double zp_host,
+                int64_t qmin, int64_t qmax, std::optional<Tensor> qp, int64_t act) {
+  Tensor y = at::empty_like(x);
+  const bool grad = torch::autograd::compute_requires_grad(x);
+  Tensor mask = grad ? mask_buffer(1, x.numel(), x) : Tensor();
+  Tensor qpt = qp.has_value() ? *qp : Tensor();
+  Tensor sd = qpt.defined() ? Tensor() : f64_on(scale, x);
+  Tensor zd = qpt.defined() ? Tensor() : f64_on(zp, x);
+  check(vsiq_act_fq_fwd_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), x.numel(), (int)act,
+                            ptr<double>(qpt), ptr<double>(sd), scale_host, ptr<double>(zd), zp_host, 0, 0, (int)qmin,
+                            (int)qmax, stream_of(x)),
+        "vsiq_act_fq_fwd_f32");
+  if (grad) {
+    auto node = std::shared_ptr<FqFixedBackward>(new FqFixedBackward(), torch::autograd::deleteNode);
+    node->set_next_edges(torch::autograd::collect_next_edges(x));
+    node->mask = mask;
+    // backward scale: the qparams record's scale entry, the device scale, or the host value
+    // (not version-checked, like the Python Function's ctx.scale: an in-place update of a
+    // scale tensor between forward and backward is not an error)
+    node->sb = qpt.defined() ? qpt.narrow(0, VSIQ_QP_SCALE, 1) : sd;
+    node->scale_host = scale_host;
+    node->act = (int)act;
+    if (act != VSIQ_ACT_NONE) node->pre = SavedVariable(x, false);
+    torch::autograd::set_history(y, node);
+  }
+  return y;
 }
 
 // --------------------------------------------------------------------------- K1/K5 + K4
-struct FqLearn : public torch::autograd::Function<FqLearn> {
-  static Tensor forward(AutogradContext *ctx, Tensor x, std::optional<Tensor> scale, double scale_host,
-                        std::optional<Tensor> zp, double zp_host, int64_t qmin, int64_t qmax, double gscale,
-                        bool learn_zp, int64_t act, Tensor ws, Tensor counter) {
-    Tensor y = at::empty_like(x);
-    Tensor sd = f64_on(scale, x), zd = f64_on(zp, x);
-    check(vsiq_act_fq_fwd_f32(ptr<float>(x), ptr<float>(y), nullptr, nullptr, x.numel(), (int)act, nullptr,
-                              ptr<double>(sd), scale_host, ptr<double>(zd), zp_host, learn_zp ? 1 : 0, 0,
-                              (int)qmin, (int)qmax, stream_of(x)),
-          "vsiq_act_fq_fwd_f32");
-    ctx->save_for_backward({x, ws, counter});
-    ctx->saved_data["has_sd"] = sd.defined();
-    ctx->saved_data["has_zd"] = zd.defined();
-    if (sd.defined()) ctx->saved_data["sd"] = sd;
-    if (zd.defined()) ctx->saved_data["zd"] = zd;
-    ctx->saved_data["scale_host"] = scale_host;
-    ctx->saved_data["zp_host"] = zp_host;
-    ctx->saved_data["qmin"] = qmin;
-    ctx->saved_data["qmax"] = qmax;
-    ctx->saved_data["gscale"] = gscale;
-    ctx->saved_data["learn_zp"] = learn_zp;
-    ctx->saved_data["act"] = act;
-    // gradient targets: the learnable tensors as given (shape / dtype / device of each)
-    // (needs_input_grad counts Variable inputs only, whose positions move with the optional
-    // tensors, so requires_grad is recorded here instead)
-    ctx->saved_data["has_scale_t"] = scale.has_value() && scale->defined() && scale->requires_grad();
-    ctx->saved_data["has_zp_t"] = zp.has_value() && zp->defined() && zp->requires_grad();
-    if (scale.has_value() && scale->defined()) ctx->saved_data["scale_t"] = scale->detach();
-    if (zp.has_value() && zp->defined()) ctx->saved_data["zp_t"] = zp->detach();
-    return y;
-  }
+// a 0-dim f64 gradient value as the gradient of a parameter of the given shape / options
+Tensor as_param(Tensor v, const std::vector<int64_t> &sizes, const at::TensorOptions &o) {
+  if (v.device() != o.device() || v.scalar_type() != o.dtype().toScalarType()) v = v.to(o.device(), o.dtype().toScalarType());
+  return sizes.empty() ? v : v.reshape(sizes);
+}
 
-  static variable_list backward(AutogradContext *ctx, variable_list grads) {
-    const auto saved = ctx->get_saved_variables();
-    const Tensor &x = saved[0], &ws = saved[1], &counter = saved[2];
+struct FqLearnBackward : public Node {
+  SavedVariable x;
+  Tensor sd, zd;                 // the qparams the forward read (device f64 copies) or undefined
+  std::vector<int64_t> s_sizes, z_sizes;   // the learnable tensors as given: gradient shape,
+  at::TensorOptions s_opts, z_opts;        // dtype and device
+  double scale_host = 0.0, zp_host = 0.0, gscale = 0.0;
+  int qmin = 0, qmax = 0, act = VSIQ_ACT_NONE;
+  bool learn_zp = false, grad_s = false, grad_z = false;
+  std::string name() const override { return "FqLearnBackward"; }
+  void release_variables() override {
+    x.reset_data();
+    sd.reset();
+    zd.reset();
+  }
+  variable_list apply(variable_list &&grads) override {
+    if (!grads[0].defined()) return {Tensor(), Tensor(), Tensor()};
+    const Tensor xv = x.unpack();
     const Tensor g = grads[0].contiguous();
     Tensor gx = at::empty_like(g);
     Tensor go = at::empty({2}, g.options().dtype(at::kDouble));
-    auto &d = ctx->saved_data;
-    const Tensor sd = d["has_sd"].toBool() ? d["sd"].toTensor() : Tensor();
-    const Tensor zd = d["has_zd"].toBool() ? d["zd"].toTensor() : Tensor();
-    const bool learn_zp = d["learn_zp"].toBool();
-    check(vsiq_act_lsq_bwd_f32(ptr<float>(g), ptr<float>(x), ptr<float>(gx), g.numel(), (int)d["act"].toInt(),
-                               ptr<double>(sd), d["scale_host"].toDouble(), ptr<double>(zd),
-                               d["zp_host"].toDouble(), learn_zp ? 1 : 0, (int)d["qmin"].toInt(),
-                               (int)d["qmax"].toInt(), d["gscale"].toDouble(), ptr<double>(go),
-                               ptr<double>(ws), ws.numel(), ptr<uint32_t>(counter), stream_of(g)),
+    Ws &w = workspace(g, g.numel());
+    check(vsiq_act_lsq_bwd_f32(ptr<float>(g), ptr<float>(xv), ptr<float>(gx), g.numel(), act, ptr<double>(sd),
+                               scale_host, ptr<double>(zd), zp_host, learn_zp ? 1 : 0, qmin, qmax, gscale,
+                               ptr<double>(go), ptr<double>(w.ws), w.ws.numel(), ptr<uint32_t>(w.counter),
+                               stream_of(g)),
           "vsiq_act_lsq_bwd_f32");
     Tensor gs, gz;
-    if (d["has_scale_t"].toBool()) {
-      const Tensor p = d["scale_t"].toTensor();
-      gs = go.narrow(0, 0, 1).to(p.device(), p.scalar_type()).reshape(p.sizes());
-    }
-    if (learn_zp && d["has_zp_t"].toBool()) {
-      const Tensor p = d["zp_t"].toTensor();
-      gz = go.narrow(0, 1, 1).to(p.device(), p.scalar_type()).reshape(p.sizes());
-    }
-    return {gx, gs, Tensor(), gz, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+    if (grad_s) gs = as_param(go.select(0, 0), s_sizes, s_opts);
+    if (learn_zp && grad_z) gz = as_param(go.select(0, 1), z_sizes, z_opts);
+    return {gx, gs, gz};
   }
 };
 
-Tensor fq_learn(Tensor x, std::optional<Tensor> scale, double scale_host, std::optional<Tensor> zp,
-                double zp_host, int64_t qmin, int64_t qmax, double gscale, bool learn_zp, int64_t act,
-                Tensor ws, Tensor counter) {
-  return FqLearn::apply(x, scale, scale_host, zp, zp_host, qmin, qmax, gscale, learn_zp, act, ws, counter);
+// ws / counter: accepted for signature compatibility (the node takes its workspace from
+// the C++ cache above when its backward runs)
+Tensor fq_learn(Tensor x, std::optional<Tensor> scale, double scale_host, std::optional<Tensor> zp, double zp_host,
+                int64_t qmin, int64_t qmax, double gscale, bool learn_zp, int64_t act, std::optional<Tensor> /*ws*/,
+                std::optional<Tensor> /*counter*/) {
+  Tensor y = at::empty_like(x);
+  Tensor sd = f64_on(scale, x), zd = f64_on(zp, x);
+  check(vsiq_act_fq_fwd_f32(ptr<float>(x), ptr<float>(y), nullptr, nullptr, x.numel(), (int)act, nullptr,
+                            ptr<double>(sd), scale_host, ptr<double>(zd), zp_host, learn_zp ? 1 : 0, 0, (int)qmin,
+                            (int)qmax, stream_of(x)),
+        "vsiq_act_fq_fwd_f32");
+  const Tensor st = scale.has_value() ? *scale : Tensor();
+  const Tensor zt = zp.has_value() ? *zp : Tensor();
+  if (torch::autograd::compute_requires_grad(x, st, zt)) {
+    auto node = std::shared_ptr<FqLearnBackward>(new FqLearnBackward(), torch::autograd::deleteNode);
+    node->set_next_edges(torch::autograd::collect_next_edges(x, st, zt));
+    node->x = SavedVariable(x, false);
+    node->sd = sd;
+    node->zd = zd;
+    node->scale_host = scale_host;
+    node->zp_host = zp_host;
+    node->gscale = gscale;
+    node->qmin = (int)qmin;
+    node->qmax = (int)qmax;
+    node->act = (int)act;
+    node->learn_zp = learn_zp;
+    node->grad_s = needs_grad(st);
+    node->grad_z = needs_grad(zt);
+    if (node->grad_s) {
+      node->s_sizes = st.sizes().vec();
+      node->s_opts = st.options();
+    }
+    if (node->grad_z) {
+      node->z_sizes = zt.sizes().vec();
+      node->z_opts = zt.options();
+    }
+    torch::autograd::set_history(y, node);
+  }
+  return y;
 }
 
 }  // namespace
@@ -226,5 +303,10 @@ PYBIND11_MODULE(_vsiq_torch, m) {
   m.def("abi_version", []() { return vsiq_abi_version(); });
   m.def("pc_observe_fq", &pc_observe_fq, "K3 per-channel observe + fake quant; STE backward");
   m.def("fq_fixed", &fq_fixed, "K1/K5 fake quant with fixed qparams; STE backward");
-  m.def("fq_learn", &fq_learn, "K1/K5 learnable fake quant; K4 backward");
+  m.def("fq_learn", &fq_learn, "K1/K5 learnable fake quant; K4 backward", pybind11::arg("x"), pybind11::arg("scale"),
+        pybind11::arg("scale_host"), pybind11::arg("zp"), pybind11::arg("zp_host"), pybind11::arg("qmin"),
+        pybind11::arg("qmax"), pybind11::arg("gscale"), pybind11::arg("learn_zp"), pybind11::arg("act"),
+        pybind11::arg("ws") = pybind11::none(), pybind11::arg("counter") = pybind11::none());
+  m.def("release_captures", &release_captures, "drop the C++ workspaces of the given HIP graph capture ids");
+  m.def("capture_workspaces", &capture_workspaces, "number of capture-owned C++ workspaces held");
 }

@@ -219,13 +219,12 @@ def fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=Non
     with VSIQ_TORCH_EXT=0).  CPU tensors: the native host path (host.py)."""
     if _host.is_host(x):
         return _host.fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
-    if H.torch_ext_enabled():
+    if H.torch_ext_enabled():   # the C++ node takes its K4 workspace from its own cache
         x = H.require_device_f32(x)
         st, sh = _qarg(scale)
         zt, zh = _qarg(zero_point)
-        w = H.workspace(x.device, x.numel())
         return H.torch_ext().fq_learn(x, st, sh, zt, zh, int(qmin), int(qmax), float(gscale), bool(learn_zp),
-                                      H.act_code(act), w.ws, w.counter)
+                                      H.act_code(act))
     return FakeQuantLearnFn.apply(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
 
 

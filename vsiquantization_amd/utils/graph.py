@@ -71,6 +71,7 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         before = set(H._WS)
         with torch.cuda.graph(self.graph):
+            self._cids = [H._capture_id(H.stream_of(torch.cuda.current_device()))]
             out = fn()
         # keep the outputs' storage (every replay rewrites it), not their autograd graph:
         # a live graph would keep the parameters' AccumulateGrad nodes of the capture
@@ -102,17 +103,23 @@ class GraphedStep:
         self.graph.replay()
         return self.out
 
-    def release(self):
-        """Drop the graph and the workspaces its capture allocated."""
+    def _drop_workspaces(self):
         for k in getattr(self, "_ws_keys", ()):
             H._WS.pop(k, None)
         self._ws_keys = []
+        cids = [c for c in getattr(self, "_cids", ()) if c is not None]
+        self._cids = []
+        if cids and H._EXT is not None:   # the C++ nodes' capture workspaces
+            H._EXT.release_captures(cids)
+
+    def release(self):
+        """Drop the graph and the workspaces its capture allocated."""
+        self._drop_workspaces()
         self.graph = None
         self.out = None
 
     def __del__(self):
         try:
-            for k in getattr(self, "_ws_keys", ()):
-                H._WS.pop(k, None)
+            self._drop_workspaces()
         except Exception:   # interpreter shutdown
             pass
