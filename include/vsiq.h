@@ -122,6 +122,11 @@ int vsiq_set_tuning(int key, int value);
 int vsiq_gate_tuning_pending(void);
 int64_t vsiq_gate_report(char *buf, int64_t len);
 int vsiq_gate_reset(void);
+/* Re-tune every store-gate launch site from its next launches on (e.g. once a training
+ * loop runs under its real load); returns the number of sites.  A tuned site also
+ * re-tunes by itself when the median time of its chosen gate drifts by more than 15 %
+ * (one launch in 128 is timed).  Results never depend on the gate. */
+int vsiq_gate_retune(void);
 
 /*
  * Self-test of the kernels' correctly rounded division x / s (reciprocal +

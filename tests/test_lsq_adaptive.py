@@ -1,0 +1,62 @@
+"""LSQFakeQuantize's adaptive rounding (flag_adaptive, h(theta) offset:
+reference quantizers/lsq_module.py:293-300, 239-241) against vectors the reference itself
+produced (tests/golden/gen_adaptive.py).  The adaptive path is an experiment of the
+reference and stays eager torch here: bit-exact on CPU tensors (the
+reference's own device); on the GPU torch's HIP tanh may differ by an ulp, so y and the
+gradients are checked to 1e-6 / 1e-5 relative there."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from vsiquantization_amd.quantizers.lsq_module import LSQFakeQuantize
+
+GOLD = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lsq_adaptive.npz"))
+
+
+def _module(case, device):
+    per_channel = bool(GOLD[f"a{case}_per_channel"])
+    kw = dict(quant_min=0, quant_max=15, dtype=torch.quint8, reduce_range=False)
+    if per_channel:
+        fq = LSQFakeQuantize(learn_scale=True, config_act=False,
+                             observer=torch.quantization.MovingAveragePerChannelMinMaxObserver,
+                             qscheme=torch.per_channel_affine, averaging_constant=0.01, ch_axis=1, **kw)
+    else:
+        fq = LSQFakeQuantize(learn_scale=True, config_act=False,
+                             observer=torch.quantization.MovingAverageMinMaxObserver,
+                             qscheme=torch.per_tensor_affine, **kw)
+    fq = fq.to(device)
+    x = torch.from_numpy(GOLD[f"a{case}_x"]).to(device)
+    fq(x)   # creates scale_param / zero_point_param_float / theta (lsq_module.py:134-143)
+    fq.disable_observer()
+    fq.flag_adaptive = True
+    with torch.no_grad():
+        fq.scale_param.copy_(torch.from_numpy(GOLD[f"a{case}_scale"]))
+        fq.zero_point_param_float.copy_(torch.from_numpy(GOLD[f"a{case}_zp"]))
+        fq.theta.copy_(torch.from_numpy(GOLD[f"a{case}_theta"]))
+    return fq, x
+
+
+def _run(case, device):
+    fq, x = _module(case, device)
+    y = fq(x.clone())
+    y.backward(torch.from_numpy(GOLD[f"a{case}_g"]).to(device))
+    return (y.detach().cpu().numpy(), fq.scale_param.grad.cpu().numpy(), fq.zero_point_param_float.grad.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", [0, 1], ids=["per_tensor", "per_channel"])
+def test_adaptive_rounding_cpu_bitwise(case):
+    y, gs, gz = _run(case, "cpu")
+    assert np.array_equal(y.view(np.uint32), GOLD[f"a{case}_y"].view(np.uint32))
+    np.testing.assert_allclose(gs, GOLD[f"a{case}_sgrad"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(gz, GOLD[f"a{case}_zgrad"], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [0, 1], ids=["per_tensor", "per_channel"])
+def test_adaptive_rounding_gpu(case):
+    y, gs, gz = _run(case, "cuda:0")
+    np.testing.assert_allclose(y, GOLD[f"a{case}_y"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(gs, GOLD[f"a{case}_sgrad"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(gz, GOLD[f"a{case}_zgrad"], rtol=1e-5, atol=1e-7)

@@ -97,6 +97,7 @@ _SIGS = {
     "vsiq_gate_tuning_pending": ([], c_int),
     "vsiq_gate_report": ([ctypes.c_char_p, c_i64], c_i64),
     "vsiq_gate_reset": ([], c_int),
+    "vsiq_gate_retune": ([], c_int),
     "vsiq_selftest_div": ([c_p, c_int, c_p, c_p], c_int),
     "vsiq_selftest_fq": ([c_int, c_p, c_p, c_int, ctypes.c_float, ctypes.c_float, c_p, c_p], c_int),
     "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
@@ -269,6 +270,11 @@ def set_tuning(key: int, value: int):
 def gate_tuning_pending() -> int:
     """Store-gate launch sites still tuning (vsiq_gate_tuning_pending)."""
     return int(lib().vsiq_gate_tuning_pending())
+
+
+def gate_retune() -> int:
+    """Re-tune every store-gate launch site (vsiq_gate_retune); returns the site count."""
+    return int(lib().vsiq_gate_retune())
 
 
 def gate_report() -> str:

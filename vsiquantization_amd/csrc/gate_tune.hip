@@ -8,6 +8,13 @@
 // smallest median wins and is used from then on.  All state is behind one mutex
 // (autograd's backward thread launches too); launches under HIP-graph capture take the
 // current choice and are never timed.
+//
+// Drift (round 3): a tuned site keeps timing one launch in kWatchEvery; when the median of
+// kWatch such samples moves more than kDrift from the winner's tuned median (the load
+// around the launches changed: RCCL or conv kernels overlapping the quantizers in a real
+// step, a different clock state), the site tunes again.  vsiq_gate_retune() re-tunes
+// every site on demand (e.g. once a training loop is warm).  The gate is a delay only:
+// results are bit-identical whatever it is.
 #include "vsiq_common.cuh"
 
 #include <algorithm>
@@ -26,6 +33,9 @@ constexpr int kCand = sizeof(kFactors) / sizeof(kFactors[0]);
 constexpr int kSamples = 8;        // timed launches per candidate
 constexpr double kDefault = 1.05;  // before (or without) tuning
 constexpr double kCapUs = 40.0;
+constexpr int kWatchEvery = 128;   // a tuned site times one launch in this many
+constexpr int kWatch = 8;          // samples per drift check
+constexpr double kDrift = 0.15;    // relative change of the median that triggers re-tuning
 
 struct Site {
   std::string label;
@@ -38,13 +48,17 @@ struct Site {
   int rr = 0;
   bool done = false;
   uint32_t best = 0;
+  float best_ms = 0.0f;             // the winner's median when tuned
+  std::vector<float> watch;         // drift samples of the chosen gate
+  int since_watch = 0;
+  int retunes = 0;
   uint64_t last_sel = 0;            // g_sel when this site was last launched
 };
 
 struct Sample {
   hipEvent_t a = nullptr, b = nullptr;
   Site *site = nullptr;
-  int cand = 0;
+  int cand = 0;   // -1: a drift sample of the tuned gate
   int dev = 0;
 };
 
@@ -79,7 +93,31 @@ void finish_if_complete(Site &s) {
     if (m < bm) { bm = m; bc = c; }
   }
   s.best = s.ticks[bc];
+  s.best_ms = bm;
   s.done = true;
+  s.watch.clear();
+  s.since_watch = 0;
+}
+
+void retune(Site &s) {
+  for (int c = 0; c < kCand; ++c) {
+    s.ms[c].clear();
+    s.issued[c] = 0;
+  }
+  s.rr = 0;
+  s.done = false;
+  s.watch.clear();
+  s.since_watch = 0;
+  ++s.retunes;
+}
+
+void watch_sample(Site &s, float ms) {
+  if (!s.done) return;   // re-tuning already
+  s.watch.push_back(ms);
+  if ((int)s.watch.size() < kWatch) return;
+  const float m = median(s.watch);
+  s.watch.clear();
+  if (s.best_ms > 0.0f && (m > (1.0 + kDrift) * s.best_ms || m < (1.0 - kDrift) * s.best_ms)) retune(s);
 }
 
 // caller holds g_mu
@@ -94,11 +132,15 @@ void harvest_locked() {
     }
     float ms = 0.0f;
     if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f) {
-      p->site->ms[p->cand].push_back(ms);
-      finish_if_complete(*p->site);
+      if (p->cand < 0) {
+        watch_sample(*p->site, ms);
+      } else if (!p->site->done) {
+        p->site->ms[p->cand].push_back(ms);
+        finish_if_complete(*p->site);
+      }
       g_pool[p->dev].emplace_back(p->a, p->b);
     } else {
-      p->site->issued[p->cand]--;   // lost sample: issue again
+      if (p->cand >= 0 && !p->site->done) p->site->issued[p->cand]--;   // lost sample: issue again
       (void)hipGetLastError();
     }
     delete p;
@@ -140,11 +182,15 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     s.est = est;
     for (int c = 0; c < kCand; ++c) s.ticks[c] = clamp_ticks(kFactors[c] * est, khz);
   }
+  int cand = -2;
   if (s.done) {
     sel.gate = s.best;
-    return sel;
+    if (++s.since_watch < kWatchEvery) return sel;
+    s.since_watch = 0;
+    cand = -1;   // time this launch: a drift sample
+  } else {
+    sel.gate = clamp_ticks(kDefault * est, khz);
   }
-  sel.gate = clamp_ticks(kDefault * est, khz);
   // under capture: no event work at all (queries are not allowed in global capture mode)
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
@@ -152,17 +198,21 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     return sel;
   }
   if (!g_pending.empty()) harvest_locked();
-  if (s.done) {
-    sel.gate = s.best;
-    return sel;
+  int c = cand;
+  if (c == -2) {
+    if (s.done) {
+      sel.gate = s.best;
+      return sel;
+    }
+    for (int k = 0; k < kCand; ++k) {
+      const int j = (s.rr + k) % kCand;
+      if (s.issued[j] < kSamples) { c = j; break; }
+    }
+    if (c < 0) return sel;   // every sample issued, results still in flight
+    s.rr = (c + 1) % kCand;
+  } else if (!s.done) {
+    return sel;   // the harvest above started a re-tune: plain launch this time
   }
-  int c = -1;
-  for (int k = 0; k < kCand; ++k) {
-    const int j = (s.rr + k) % kCand;
-    if (s.issued[j] < kSamples) { c = j; break; }
-  }
-  if (c < 0) return sel;   // every sample issued, results still in flight
-  s.rr = (c + 1) % kCand;
   auto &pool = g_pool[dev];
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
   if (!pool.empty()) {
@@ -183,8 +233,10 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   p->site = &s;
   p->cand = c;
   p->dev = dev;
-  s.issued[c]++;
-  sel.gate = s.ticks[c];
+  if (c >= 0) {
+    s.issued[c]++;
+    sel.gate = s.ticks[c];
+  }
   sel.timing = p;
   return sel;
 }
@@ -196,7 +248,7 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (hipEventRecord(p->b, st) != hipSuccess) {
     (void)hipGetLastError();
-    p->site->issued[p->cand]--;
+    if (p->cand >= 0) p->site->issued[p->cand]--;
     g_pool[p->dev].emplace_back(p->a, p->b);
     delete p;
     return;
@@ -221,9 +273,9 @@ int64_t gate_report(char *buf, int64_t len) {
   char line[512];
   for (auto &kv : g_sites) {
     const Site &s = kv.second;
-    std::snprintf(line, sizeof line, "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u",
+    std::snprintf(line, sizeof line, "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u retunes=%d",
                   s.label.c_str(), s.dev, (long long)s.grid, (long long)s.bytes, s.est, s.done ? 1 : 0,
-                  s.best);
+                  s.best, s.retunes);
     out += line;
     for (int c = 0; c < kCand; ++c) {
       if (s.ms[c].empty()) continue;
@@ -238,6 +290,17 @@ int64_t gate_report(char *buf, int64_t len) {
     buf[n] = '\0';
   }
   return (int64_t)out.size();
+}
+
+int gate_retune() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  harvest_locked();
+  int n = 0;
+  for (auto &kv : g_sites) {
+    retune(kv.second);
+    ++n;
+  }
+  return n;
 }
 
 int gate_reset() {
@@ -259,5 +322,7 @@ int vsiq_gate_tuning_pending(void) { return gate_sites_tuning(); }
 int64_t vsiq_gate_report(char *buf, int64_t len) { return gate_report(buf, len); }
 
 int vsiq_gate_reset(void) { return gate_reset(); }
+
+int vsiq_gate_retune(void) { return gate_retune(); }
 
 }  // extern "C"

@@ -116,7 +116,7 @@ class LSQFakeQuantize(FakeQuantize):
                     return self._adaptive_reference(X, grad_scale, qmin, qmax)
                 return self._learnable(X, grad_scale, qmin, qmax)
             scale, zero_point = self.scale, self.zero_point
-            if self.flag_adaptive:
+            if self.flag_adaptive or (self.is_per_channel and X.device.type == "cpu"):
                 if self.is_per_channel:
                     view = [1] + [-1] + [1] * (len(X.shape) - 2)
                     scale, zero_point = scale.view(view), zero_point.view(view)
@@ -135,6 +135,8 @@ class LSQFakeQuantize(FakeQuantize):
 
     def _learnable(self, X, grad_scale, qmin, qmax):
         s, z = self.scale_param, self.zero_point_param_float
+        if self.is_per_channel and X.device.type == "cpu":   # no per-channel host loops: torch's CPU ops
+            return self._adaptive_reference(X, grad_scale, qmin, qmax)
         if self.is_per_channel:
             self._check_channels(X, s)
             return PerChannelLearnFn.apply(X, s, z, qmin, qmax, float(grad_scale), True, 1)
