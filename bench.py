@@ -944,29 +944,144 @@ def settle_gates(W, cap=4000, world=1):
     return n, sites
 
 
-def measure(W, steps, warmup, world):
+class _PhaseMark:
+    """Stands in for the timing event k of a launch group while the group is captured:
+    event 0 opens the first phase's HIP graph, event k closes phase k-1 and opens phase
+    k, the last one closes the last phase (each phase of each group one graph)."""
+
+    def __init__(self, cap, k, last):
+        self.cap, self.k, self.last = cap, k, last
+
+    def record(self, *_):
+        cap = self.cap
+        if self.k > 0:
+            cap.ctx.__exit__(None, None, None)
+            cap.graphs.append(cap.cur)
+        if not self.last:
+            cap.cur = torch.cuda.CUDAGraph()
+            cap.ctx = torch.cuda.graph(cap.cur, stream=cap.stream)
+            cap.ctx.__enter__()
+
+
+class _GroupCapture:
+    def __init__(self, stream):
+        self.stream, self.graphs, self.cur, self.ctx = stream, [], None, None
+
+
+def capture_groups(W, groups, nphase):
+    """Every launch group of the timed region, phase by phase, as HIP graphs (the same
+    launches, replayed without host work between the kernels).  None when a workload's
+    launches cannot be captured (then the timed region launches directly)."""
+    stream = torch.cuda.current_stream()
+    out = []
+    try:
+        for g0, cnt in groups:
+            cap = _GroupCapture(stream)
+            rc = W.launch_group(g0, cnt, [_PhaseMark(cap, k, k == nphase) for k in range(nphase + 1)])
+            if rc != 0 or len(cap.graphs) != nphase:
+                return None
+            out.append(cap.graphs)
+    except Exception as e:  # noqa: BLE001
+        progress(f"graph capture not used: {type(e).__name__}: {e}")
+        torch.cuda.synchronize()
+        return None
+    torch.cuda.synchronize()
+    return out
+
+
+def measure(W, steps, warmup, world, graphs=None):
     """W untimed warmup steps, self-check, then exactly `steps` timed steps between
     barrier + synchronize on both sides; the max over ranks of the wall time; per-phase
-    HIP-event durations (rank-local) -> roofline of the dominant phase."""
+    HIP-event durations (rank-local) -> roofline of the dominant phase.
+
+    Launch mode (one rank; graphs None = VSIQ_BENCH_GRAPH, default on): the timed launch
+    groups are also captured as HIP graphs (after the warm-up and the store-gate settling,
+    capture_groups).  Replaying them removes the host's per-launch cost (ctypes +
+    hipLaunchKernel, 5-10 us on a slow host, comparable to a C2 kernel) from between the
+    kernels, but a graph's kernel nodes dispatch a little slower than direct launches on a
+    fast host (measured: C2 29.7 vs 28.2 us/step).  So an untimed trial (the first group,
+    3 times each way, median wall time) picks the mode for the timed region, and the same
+    `steps` are then timed the other way too and reported as "alt_launch"."""
     for i in range(warmup):
         assert W.launch(i) == 0
     settle, gate_sites = settle_gates(W, world=world)
     names = list(W.kernels)
     ns = W.group
     groups = [(g0, min(ns, steps - g0)) for g0 in range(0, steps, ns)]
+    if graphs is None:
+        graphs = os.environ.get("VSIQ_BENCH_GRAPH", "1") == "1"
+    captured = capture_groups(W, groups, len(names)) if graphs and world == 1 else None
+    use_graph, trial = False, None
+    if captured is not None:
+        use_graph, trial = _pick_launch(W, groups[0], captured[0])
+    dt, evs = _timed(W, groups, names, steps, world, captured if use_graph else None)
+    alt = _timed(W, groups, names, steps, world, None if use_graph else captured) if captured is not None else None
+    out = _report(W, steps, world, dt, _durations(evs, names, steps), names, settle, gate_sites)
+    out["launch"] = "hip graph per phase and group" if use_graph else "direct"
+    if alt is not None:
+        adt, aevs = alt
+        ar = _report(W, steps, world, adt, _durations(aevs, names, steps), names, settle, gate_sites)
+        out["alt_launch"] = {"launch": "direct" if use_graph else "hip graph per phase and group",
+                             "value": ar["value"], "ms_per_step": ar["ms_per_step"],
+                             "frac": ar["roofline"]["frac"],
+                             "kernels_us": {k: v["avg_us"] for k, v in ar["kernels"].items()},
+                             "trial_ms_per_group": trial}
+    return out
+
+
+def _durations(evs, names, steps):
+    return {k: sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps * 1e-3 for i, k in enumerate(names)}
+
+
+class _NoEvent:
+    def record(self, *_):
+        pass
+
+
+def _pick_launch(W, group, graphs, reps=3):
+    """Untimed trial of one launch group each way: (graph faster?, {mode: median ms})."""
+    g0, cnt = group
+    t = {"direct": [], "graph": []}
+    for _ in range(reps):
+        for mode in ("direct", "graph"):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if mode == "graph":
+                for g in graphs:
+                    g.replay()
+            else:
+                assert W.launch_group(g0, cnt, [_NoEvent()] * (len(graphs) + 1)) == 0
+            torch.cuda.synchronize()
+            t[mode].append((time.perf_counter() - t0) * 1e3)
+    med = {k: sorted(v)[reps // 2] for k, v in t.items()}
+    return med["graph"] < med["direct"], med
+
+
+def _timed(W, groups, names, steps, world, captured):
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in groups]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rc = 0
-    for (g0, cnt), ev in zip(groups, evs):
-        rc |= W.launch_group(g0, cnt, ev)
+    if captured is None:
+        for (g0, cnt), ev in zip(groups, evs):
+            rc |= W.launch_group(g0, cnt, ev)
+    else:
+        for gr, ev in zip(captured, evs):
+            ev[0].record()
+            for k, g in enumerate(gr):
+                g.replay()
+                ev[k + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     assert rc == 0, f"kernel launch failed rc={rc}"
+    return dt, evs
+
+
+def _report(W, steps, world, dt, dur, names, settle, gate_sites):
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=torch.cuda.current_device())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -978,7 +1093,6 @@ def measure(W, steps, warmup, world):
         t = torch.tensor([int(ok)], device=torch.cuda.current_device())
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         ok = bool(t.item())
-    dur = {k: sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps * 1e-3 for i, k in enumerate(names)}
     dom = max((k for k in names if W.kernels[k] > 0), key=dur.get)
     achieved = W.kernels[dom] / dur[dom] / 1e9
     per_kernel = {k: {"avg_us": dur[k] * 1e6, "alg_bytes": W.kernels[k],
@@ -1144,6 +1258,9 @@ def main(argv=None):
     backend = os.environ.get("VSIQ_BENCH_BACKEND", "nccl")
     dev = torch.device("cuda", local if backend == "nccl" else local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    # every launch of the run on one non-default stream (HIP graphs of the timed groups are
+    # captured on it: measure / capture_groups)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -1181,7 +1298,10 @@ def main(argv=None):
         "roofline": r["roofline"],
         "kernels": r["kernels"],
         "store_gate": r["store_gate"],
+        "launch": r["launch"],
     }
+    if "alt_launch" in r:
+        out["alt_launch"] = r["alt_launch"]
     if a.tune:
         out["config"]["tuning"] = a.tune
     if a.workload == "c2":
@@ -1207,7 +1327,9 @@ def main(argv=None):
                        "ms_per_step": rx["ms_per_step"], "steps": steps, "warmup": warm,
                        "scaling": "strong" if key == "act" else "weak",
                        "config": dict(describe(Wx, key, a, world), self_check=rx["self_check"]),
-                       "roofline": rx["roofline"], "kernels": rx["kernels"]}
+                       "roofline": rx["roofline"], "kernels": rx["kernels"], "launch": rx["launch"]}
+        if "alt_launch" in rx:
+            extras[key]["alt_launch"] = rx["alt_launch"]
         del Wx
         torch.cuda.empty_cache()
     if cpu:
