@@ -13,8 +13,11 @@
 // kWatch such samples moves more than kDrift from the winner's tuned median (the load
 // around the launches changed: RCCL or conv kernels overlapping the quantizers in a real
 // step, a different clock state), the site tunes again.  vsiq_gate_retune() re-tunes
-// every site on demand (e.g. once a training loop is warm).  The gate is a delay only:
-// results are bit-identical whatever it is.
+// every site on demand (e.g. once a training loop is warm).  A re-tune needs two drifting
+// checks in a row, and one that lands on the gate the site had already doubles that
+// site's watch interval (up to kWatchMax): a site whose launches simply vary with the
+// caller's pace (isolated per-call launches vs back-to-back ones) stops paying for timing
+// and re-tuning.  The gate is a delay only: results are bit-identical whatever it is.
 #include "vsiq_common.cuh"
 
 #include <algorithm>
@@ -34,6 +37,7 @@ constexpr int kSamples = 8;        // timed launches per candidate
 constexpr double kDefault = 1.05;  // before (or without) tuning
 constexpr double kCapUs = 40.0;
 constexpr int kWatchEvery = 128;   // a tuned site times one launch in this many
+constexpr int kWatchMax = 128 * 64;
 constexpr int kWatch = 8;          // samples per drift check
 constexpr double kDrift = 0.15;    // relative change of the median that triggers re-tuning
 
@@ -51,6 +55,9 @@ struct Site {
   float best_ms = 0.0f;             // the winner's median when tuned
   std::vector<float> watch;         // drift samples of the chosen gate
   int since_watch = 0;
+  int watch_every = kWatchEvery;
+  int drifting = 0;                 // consecutive drifting checks
+  uint32_t prev_best = 0;           // the gate before the running re-tune
   int retunes = 0;
   uint64_t last_sel = 0;            // g_sel when this site was last launched
 };
@@ -97,6 +104,8 @@ void finish_if_complete(Site &s) {
   s.done = true;
   s.watch.clear();
   s.since_watch = 0;
+  s.drifting = 0;
+  if (s.retunes > 0 && s.best == s.prev_best) s.watch_every = std::min(2 * s.watch_every, kWatchMax);
 }
 
 void retune(Site &s) {
@@ -105,9 +114,11 @@ void retune(Site &s) {
     s.issued[c] = 0;
   }
   s.rr = 0;
+  s.prev_best = s.best;
   s.done = false;
   s.watch.clear();
   s.since_watch = 0;
+  s.drifting = 0;
   ++s.retunes;
 }
 
@@ -117,7 +128,9 @@ void watch_sample(Site &s, float ms) {
   if ((int)s.watch.size() < kWatch) return;
   const float m = median(s.watch);
   s.watch.clear();
-  if (s.best_ms > 0.0f && (m > (1.0 + kDrift) * s.best_ms || m < (1.0 - kDrift) * s.best_ms)) retune(s);
+  const bool drift = s.best_ms > 0.0f && (m > (1.0 + kDrift) * s.best_ms || m < (1.0 - kDrift) * s.best_ms);
+  s.drifting = drift ? s.drifting + 1 : 0;
+  if (s.drifting >= 2) retune(s);
 }
 
 // caller holds g_mu
@@ -185,7 +198,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   int cand = -2;
   if (s.done) {
     sel.gate = s.best;
-    if (++s.since_watch < kWatchEvery) return sel;
+    if (++s.since_watch < s.watch_every) return sel;
     s.since_watch = 0;
     cand = -1;   // time this launch: a drift sample
   } else {
@@ -273,9 +286,10 @@ int64_t gate_report(char *buf, int64_t len) {
   char line[512];
   for (auto &kv : g_sites) {
     const Site &s = kv.second;
-    std::snprintf(line, sizeof line, "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u retunes=%d",
+    std::snprintf(line, sizeof line,
+                  "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u retunes=%d watch=%d",
                   s.label.c_str(), s.dev, (long long)s.grid, (long long)s.bytes, s.est, s.done ? 1 : 0,
-                  s.best, s.retunes);
+                  s.best, s.retunes, s.watch_every);
     out += line;
     for (int c = 0; c < kCand; ++c) {
       if (s.ms[c].empty()) continue;

@@ -68,8 +68,8 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
 
 // Records-only K4 (K4d): groups per lane 2.  Without an arrival chain more, smaller
 // workgroups cost nothing and stream better at every C4 size (MI355X kernel trace, 3.3M
-// -> 105M elements: 9.8 / 16.1 / 27.7 / 51.1 / 100.1 / 204.5 us at 2 per lane against
-// 10.9 / 16.4 / 28.3 / 53.6 / 102.6 / 207.1 us at K4's 4 / 8, profiles/r03g_c4_groups.txt);
+// -> 105M elements: 9.9 / 16.2 / 28.0 / 51.7 / 101.0 / 205.3 us at 2 per lane against
+// 11.1 / 16.6 / 28.4 / 54.2 / 103.2 / 207.9 us at K4's 4 / 8, profiles/r03g_c4_groups.txt);
 // the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
 inline int lsq_part_groups_per_lane() {
   const int g = g_tune.lsq_groups;
