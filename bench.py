@@ -29,6 +29,7 @@ its return code.  Under torchrun, WORLD_SIZE must equal --gpus.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -95,6 +96,64 @@ def launch_ranks(a, argv) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
     return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+# --------------------------------------------------------------------------- timing events
+class HipEvent:
+    """A HIP timing event created with hipEventDisableSystemFence (hip_runtime_api.h: for
+    events "only being used to measure timing"; "on some AMD GPU devices this can improve
+    the accuracy of timing measurements by avoiding the cost of cache writeback and
+    invalidation, and the performance impact of those actions on the execution of following
+    work").  torch.cuda.Event records with the default system-scope release, so every
+    event between two launch phases wrote the L2 back and invalidated it in the middle of
+    the timed region.  Same interface as torch.cuda.Event (record / elapsed_time) on the
+    current stream.  VSIQ_BENCH_EVENTS=torch uses torch's events instead."""
+
+    FLAG = 0x20000000   # hipEventDisableSystemFence
+    _rt = None
+
+    @classmethod
+    def rt(cls):
+        if cls._rt is None:
+            rt = ctypes.CDLL("libamdhip64.so.7")   # torch's already-mapped HIP runtime
+            rt.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            rt.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._rt = rt
+        return cls._rt
+
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        rc = self.rt().hipEventCreateWithFlags(ctypes.byref(self.h), self.FLAG)
+        assert rc == 0, f"hipEventCreateWithFlags rc={rc}"
+
+    def record(self, stream=None):
+        st = (stream or torch.cuda.current_stream()).cuda_stream
+        rc = self.rt().hipEventRecord(self.h, ctypes.c_void_p(st))
+        assert rc == 0, f"hipEventRecord rc={rc}"
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        rc = self.rt().hipEventElapsedTime(ctypes.byref(ms), self.h, end.h)
+        assert rc == 0, f"hipEventElapsedTime rc={rc}"
+        return ms.value
+
+    def __del__(self):
+        if self.h and self._rt is not None:
+            self._rt.hipEventDestroy(self.h)
+            self.h = ctypes.c_void_p()
+
+
+def timing_event():
+    if os.environ.get("VSIQ_BENCH_EVENTS", "hip") == "torch":
+        return torch.cuda.Event(enable_timing=True)
+    return HipEvent()
+
+
+def timing_events_kind():
+    return ("torch.cuda.Event (system-scope release)" if os.environ.get("VSIQ_BENCH_EVENTS", "hip") == "torch"
+            else "HIP events with hipEventDisableSystemFence")
 
 
 # --------------------------------------------------------------------------- workloads
@@ -176,7 +235,7 @@ class C2PerChannel:
                 torch.cuda.synchronize()
                 if H.gate_tuning_pending() == 0:
                     break
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
+        evs = [(timing_event(), timing_event()) for _ in range(groups)]
         for e0, e1 in evs:
             e0.record()
             for a in args:
@@ -1058,7 +1117,7 @@ def _pick_launch(W, group, graphs, reps=3):
 
 
 def _timed(W, groups, names, steps, world, captured):
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in groups]
+    evs = [[timing_event() for _ in range(len(names) + 1)] for _ in groups]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1305,6 +1364,7 @@ def main(argv=None):
         "kernels": r["kernels"],
         "store_gate": r["store_gate"],
         "launch": r["launch"],
+        "timing_events": timing_events_kind(),
     }
     if "alt_launch" in r:
         out["alt_launch"] = r["alt_launch"]

@@ -4,7 +4,9 @@
 // A launch site is (kernel, grid, read bytes, device).  Its first launches cycle
 // through candidate gates f x (read bytes at 7.5 TB/s), and no gate, each bracketed by
 // a pair of HIP events on the launch stream; later calls harvest finished pairs
-// (hipEventQuery, never a host sync), and once every candidate has kSamples times the
+// (hipEventQuery, never a host sync; the events skip the system-scope fence, so timing a
+// launch neither writes back / invalidates the caches nor slows the launches after it),
+// and once every candidate has kSamples times the
 // smallest median wins and is used from then on.  All state is behind one mutex
 // (autograd's backward thread launches too); launches under HIP-graph capture take the
 // current choice and are never timed.
@@ -231,7 +233,8 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   if (!pool.empty()) {
     ev = pool.back();
     pool.pop_back();
-  } else if (hipEventCreate(&ev.first) != hipSuccess || hipEventCreate(&ev.second) != hipSuccess) {
+  } else if (hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence) != hipSuccess ||
+             hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence) != hipSuccess) {
     (void)hipGetLastError();
     return sel;
   }
