@@ -20,7 +20,10 @@ KERNEL_KEYS = {
     # C1_K2K1=1 runs K2 + K1 ("observe", "fq_fwd")
     "c1": [("k_observe_part<", "observe_fq", 1), ("k_fold_fq_fwd<", "observe_fq", 1),
            ("k_observe_loop<", "observe", 1), ("k_fq_fwd<", "fq_fwd", 1)],
-    "c2": [("k_pc_observe_fq<", "pc_observe_fq_fwd", 1), ("k_ste_bwd<", "ste_bwd", 1)],
+    # C2: the mask-only K3 instance (MASK true, CODES false); the run also launches the
+    # codes variant (9 B/elem, bench's pc_observe_fq_fwd_with_codes), which must not be
+    # averaged in (round 2's 1.07x "write excess" was exactly that mix)
+    "c2": [(("k_pc_observe_fq<", ", true, false, 256, 1>"), "pc_observe_fq_fwd", 1), ("k_ste_bwd<", "ste_bwd", 1)],
     "c3": [("k_fq_fwd<", "fq_fwd", 1), ("k_lsq_bwd<", "lsq_bwd", 1)],
     # C4: per step 27 fused-ReLU activation launches each way + ONE multi-tensor launch
     # each way for the 27 weights
@@ -40,7 +43,8 @@ def per_kernel(d, counter, keys):
             if r["Counter_Name"] != counter:
                 continue
             for frag, _, _ in keys:
-                if frag in r["Kernel_Name"]:
+                parts = frag if isinstance(frag, tuple) else (frag,)
+                if all(p in r["Kernel_Name"] for p in parts):
                     acc[frag].append(float(r["Counter_Value"]))
     out = collections.defaultdict(float)
     for frag, label, mult in keys:
