@@ -61,14 +61,18 @@ def _same(got, want, what):
             np.testing.assert_allclose(g[k], w[k], rtol=1e-6, atol=atol, err_msg=f"{what} layer {i} {k}")
 
 
-@pytest.mark.parametrize("name", ["small", "c5"])
-def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name):
+@pytest.mark.parametrize("name,backend,ranks", [("small", "gloo", 2), ("c5", "gloo", 2), ("small", "nccl", 1)])
+def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name, backend, ranks):
+    """gloo: 2 ranks sharing cuda:0.  nccl: ONE rank over RCCL (two ranks cannot share a
+    GPU under RCCL): the RCCL all_gather_into_tensor / all_reduce branches and a
+    GraphedStep capture of the per-call observe+quantize step holding an RCCL all_gather."""
     cfg = Config(name)
     out = tmp_path / "rank0.json"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "dist_calib_worker.py"), str(out), name]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    env = dict(os.environ, VSIQ_DIST_BACKEND=backend)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = json.loads(out.read_text())
     acts = activations(cfg)
@@ -78,7 +82,9 @@ def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name):
     assert len(one[0]["mean_abs"]) == cfg.calls and len(one) == len(cfg.layers)
     _same(one, _oracle(cfg, acts), "1 GPU vs oracle")
     for mode in ("per_call", "deferred"):
-        _same(got[mode], one, f"2 ranks {mode} vs 1 GPU")
+        _same(got[mode], one, f"{ranks} ranks ({backend}) {mode} vs 1 GPU")
+    if backend == "nccl":
+        assert got["graph"]["replays_equal_eager"], got["graph"]
     if name == "small":
         # observe + quantize per call: the 2 ranks' y / straight-through gradients are the
         # 1-GPU run's halves bit for bit, the observer state identical (one all_gather
@@ -89,10 +95,10 @@ def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name):
             qm.is_quantize = True
         full = observe_quantize(cfg, mgrs, acts)
         _same(got["observe_quantize"], state(mgrs), "2 ranks observe+quantize vs 1 GPU")
-        for r in range(2):
+        for r in range(ranks):
             part = np.load(f"{out}.oq{r}.npz")
             for k, v in full.items():
-                want = np.array_split(v, 2, axis=0)[r]
+                want = np.array_split(v, ranks, axis=0)[r]
                 assert np.array_equal(part[k].view(np.uint32), want.view(np.uint32)), (r, k)
 
 

@@ -2,15 +2,14 @@
 
 The fake-quant itself is elementwise and needs no communication.  The only
 exchange is the per-tensor observer's statistics: every rank
-runs the K2 pass over its shard, then
-
-    all_reduce(MAX)  over [-min, max]                         (exact, order-free)
-    all_reduce(SUM)  over [nan_count, sum|x|, sum x, sum x^2, n]
-
-after which every rank holds the statistics of the whole batch and applies the
-reference's running update (observers/minmax.py:42-47) identically.  min/max and
-the qparams are therefore bit-identical to a 1-GPU run; the sums differ only in
-float64 summation order.
+runs the observer pass over its shard and writes its stats record(s); ONE
+all_gather of the records (``all_gather_into_tensor`` on every backend), then a
+fold in rank order on every rank -- min / max exact, the sums in float64 in a fixed
+order, so every rank holds the same bits -- followed by the reference's running
+update (observers/minmax.py:42-47) and the f64 qparams.  min/max and the qparams are
+bit-identical to a 1-GPU run; the sums differ only in float64 summation order.
+(``allreduce_stats`` -- MAX over [-min, max], SUM over the sums -- is what the
+deferred sync uses over all records of all layers at once.)
 
 Two modes:
 * per call  (``QuantizationManager.dist_group`` set, ``dist_defer`` False): one tiny
