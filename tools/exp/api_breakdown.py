@@ -50,6 +50,32 @@ def empty():
     torch.empty_like(x)
 
 
+from vsiquantization_amd import _hip as H  # noqa: E402
+from vsiquantization_amd.fakequant import qden  # noqa: E402
+ext = H.torch_ext()
+mn, mx = obs._state(x)
+qd = qden(False, 8, 1e-8)
+
+
+def ext_fwd():
+    ext.pc_observe_fq(x, mn, mx, False, 0, 255, qd, 1e-8, False)
+
+
+def ext_step():
+    x.grad = None
+    y = ext.pc_observe_fq(x, mn, mx, False, 0, 255, qd, 1e-8, False)[0]
+    y.backward(g)
+
+
+def py_wrapper_only():
+    H.require_device_f32(x)
+    obs._state(x)
+    H.torch_ext_enabled()
+    qden(False, 8, 1e-8)
+
+
 for name, fn in (("fwd (no grad)", fwd), ("fwd (autograd node)", fwd_graph), ("fwd + bwd", step),
-                 ("torch x*1 fwd + bwd", trivial), ("torch.empty_like", empty)):
+                 ("torch x*1 fwd + bwd", trivial), ("torch.empty_like", empty),
+                 ("ext fwd (direct)", ext_fwd), ("ext fwd + bwd (direct)", ext_step),
+                 ("python wrapper only", py_wrapper_only)):
     print(f"{name:22s} {t(fn):8.1f} us", flush=True)

@@ -10,7 +10,8 @@ Importing the package registers the quantizer/observer classes by name in
 
 plus ``LSQFakeQuantize`` (quantizers/lsq_module.py, the torch.ao-based LSQ module).
 All fake-quant arithmetic runs in the HIP kernels of ``csrc/`` through the C ABI of
-``include/vsiq.h``; there is no CPU path.
+``include/vsiq.h``; CPU float32 tensors of the per-tensor classes run the same
+library's native host loops (``host.py``, ``vsiq_host_*``), never the test oracle.
 """
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 

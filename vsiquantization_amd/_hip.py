@@ -250,8 +250,10 @@ def require_device_f32(x: torch.Tensor, what: str = "x") -> torch.Tensor:
         raise TypeError(f"{what} must be a torch.Tensor, got {type(x).__name__}")
     if x.device.type != "cuda":
         raise VsiqError(
-            f"vsiquantization_amd runs on MI355X (HIP) only; {what} is on {x.device}. "
-            "There is no CPU path: move the model/tensors to the GPU.")
+            f"{what} is on {x.device}: this operation runs on MI355X (HIP) only. CPU float32 "
+            "tensors are served by the native host path of the reference's per-tensor classes "
+            "(UniformQuantizer, LSQQuantizer, MinMaxObserver, QuantizationManager, FakeQuantize); "
+            "the per-channel, multi-tensor and fused-layer kernels need the GPU.")
     if x.dtype != torch.float32:
         raise TypeError(f"{what}: only float32 is supported by the HIP fake-quant path, got {x.dtype}")
     return x.contiguous()
