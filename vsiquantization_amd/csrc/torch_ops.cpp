@@ -145,8 +145,7 @@ std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool
   Tensor zp = at::empty({C}, x.options().dtype(at::kDouble));
   const bool grad = torch::autograd::compute_requires_grad(x);
   Tensor mask = grad ? mask_buffer(C, rowlen, x) : Tensor();
-  Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble))
-                             : at::empty({0}, x.options().dtype(at::kDouble));
+  Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble)) : Tensor();   // None
   check(vsiq_pc_observe_fq_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), C, rowlen,
                                ptr<float>(run_min), ptr<float>(run_max), ptr<double>(scale), ptr<double>(zp),
                                want_row_stats ? ptr<double>(rs) : nullptr, sym ? 1 : 0, (int)qmin, (int)qmax, qden,
