@@ -1058,8 +1058,9 @@ def measure(W, steps, warmup, world, graphs=None):
     capture_groups).  Replaying them removes the host's per-launch cost (ctypes +
     hipLaunchKernel, 5-10 us on a slow host, comparable to a C2 kernel) from between the
     kernels, but a graph's kernel nodes dispatch a little slower than direct launches on a
-    fast host (measured: C2 29.7 vs 28.2 us/step).  So an untimed trial (the first group,
-    3 times each way, median wall time) picks the mode for the timed region, and the same
+    fast host (measured: C2 29.7 vs 28.2 us/step).  So an untimed trial (up to 4 groups,
+    5 rounds each way, median wall time; graph only if >1 % faster) picks the mode for the
+    timed region, and the same
     `steps` are then timed the other way too and reported as "alt_launch"."""
     for i in range(warmup):
         assert W.launch(i) == 0
@@ -1072,7 +1073,7 @@ def measure(W, steps, warmup, world, graphs=None):
     captured = capture_groups(W, groups, len(names)) if graphs and world == 1 else None
     use_graph, trial = False, None
     if captured is not None:
-        use_graph, trial = _pick_launch(W, groups[0], captured[0])
+        use_graph, trial = _pick_launch(W, groups, captured)
     dt, evs = _timed(W, groups, names, steps, world, captured if use_graph else None)
     alt = _timed(W, groups, names, steps, world, None if use_graph else captured) if captured is not None else None
     out = _report(W, steps, world, dt, _durations(evs, names, steps), names, settle, gate_sites)
@@ -1084,7 +1085,7 @@ def measure(W, steps, warmup, world, graphs=None):
                              "value": ar["value"], "ms_per_step": ar["ms_per_step"],
                              "frac": ar["roofline"]["frac"],
                              "kernels_us": {k: v["avg_us"] for k, v in ar["kernels"].items()},
-                             "trial_ms_per_group": trial}
+                             "trial_ms": trial}
     return out
 
 
@@ -1097,23 +1098,27 @@ class _NoEvent:
         pass
 
 
-def _pick_launch(W, group, graphs, reps=3):
-    """Untimed trial of one launch group each way: (graph faster?, {mode: median ms})."""
-    g0, cnt = group
+def _pick_launch(W, groups, graphs, reps=5, margin=0.01):
+    """Untimed trial: up to 4 launch groups each way, `reps` rounds, median wall time per
+    mode; graph replay is chosen only when it is faster by more than `margin` (direct
+    launches are the default).  Returns (use graph?, {mode: median ms})."""
+    sel = list(range(min(4, len(groups))))
     t = {"direct": [], "graph": []}
     for _ in range(reps):
         for mode in ("direct", "graph"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            if mode == "graph":
-                for g in graphs:
-                    g.replay()
-            else:
-                assert W.launch_group(g0, cnt, [_NoEvent()] * (len(graphs) + 1)) == 0
+            for j in sel:
+                if mode == "graph":
+                    for g in graphs[j]:
+                        g.replay()
+                else:
+                    g0, cnt = groups[j]
+                    assert W.launch_group(g0, cnt, [_NoEvent()] * (len(graphs[j]) + 1)) == 0
             torch.cuda.synchronize()
             t[mode].append((time.perf_counter() - t0) * 1e3)
     med = {k: sorted(v)[reps // 2] for k, v in t.items()}
-    return med["graph"] < med["direct"], med
+    return med["graph"] < (1.0 - margin) * med["direct"], med
 
 
 def _timed(W, groups, names, steps, world, captured):
