@@ -62,6 +62,9 @@ def parse(argv=None):
     p.add_argument("--per-call-grads", action="store_true",
                    help="C4: fold each activation scale gradient inside its K4 launch (round 1) instead of "
                         "records-only K4 + one fold launch (enable_deferred_qparam_grads)")
+    p.add_argument("--asym", action="store_true",
+                   help="C3: the asymmetric variant (uint8 [0, 255], learnable zero point 3.0: LSQQuantizer, "
+                        "SURVEY §8d) instead of symmetric int8")
     p.add_argument("--slots", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-api", action="store_true", help="skip the public-API C2 timing")
@@ -352,7 +355,9 @@ class C3Lsq(C2PerChannel):
     shape = (512, 3, 224, 224)
     scale0 = 0.03
 
-    def __init__(self, dev, slots, seed_base):
+    zp0 = 3.0
+
+    def __init__(self, dev, slots, seed_base, asym=False):
         from vsiquantization_amd import _hip as H
         self.H = H
         n = 1
@@ -364,7 +369,11 @@ class C3Lsq(C2PerChannel):
         w = H.workspace(dev, n)
         self.ws = w
         self.slots = []
-        self.gscale = (127 * n) ** -0.5
+        self.asym = asym
+        self.qmin, self.qmax = (0, 255) if asym else (-128, 127)
+        if asym:
+            self.name = "C3 LSQ learnable-scale asym uint8 (learnable zero point 3.0) fwd + STE/scale/zp-grad bwd"
+        self.gscale = (self.qmax * n) ** -0.5
         for i in range(min(slots, 2)):   # 2 slots x 1.2 GB already defeat the MALL
             gen = torch.Generator(device=dev).manual_seed(seed_base + 2 * i)
             x = torch.randn(self.shape, device=dev, generator=gen)
@@ -372,11 +381,13 @@ class C3Lsq(C2PerChannel):
             g = torch.randn(self.shape, device=dev, generator=gen)
             s = dict(x=x, g=g, y=torch.empty_like(x), gx=torch.empty_like(x),
                      scale=torch.tensor(self.scale0, dtype=torch.float64, device=dev),
+                     zp=torch.tensor(self.zp0, dtype=torch.float64, device=dev),
                      grads=torch.empty(2, dtype=torch.float64, device=dev))
             P = {k: H.ptr(v) for k, v in s.items()}
-            s["fwd"] = (P["x"], P["y"], None, None, H.c_i64(n), None, P["scale"], 0.0, None, 0.0, 0, 0,
-                        -128, 127, st)
-            s["bwd"] = (P["g"], P["x"], P["gx"], H.c_i64(n), P["scale"], 0.0, None, 0.0, 0, -128, 127,
+            zp, za = (P["zp"], 1) if asym else (None, 0)   # zero_point_rounding (uniform.py:98-102)
+            s["fwd"] = (P["x"], P["y"], None, None, H.c_i64(n), None, P["scale"], 0.0, zp, 0.0, za, 0,
+                        self.qmin, self.qmax, st)
+            s["bwd"] = (P["g"], P["x"], P["gx"], H.c_i64(n), P["scale"], 0.0, zp, 0.0, za, self.qmin, self.qmax,
                         self.gscale, P["grads"], H.ptr(w.ws), H.c_i64(w.ws_len), H.ptr(w.counter), st)
             self.slots.append(s)
         self.f_fwd = lib.vsiq_fq_fwd_f32
@@ -392,17 +403,19 @@ class C3Lsq(C2PerChannel):
         s = self.slots[0]
         k = 1 << 21
         s32 = torch.tensor(self.scale0, dtype=torch.float64).float()
+        z32 = torch.tensor(self.zp0 if self.asym else 0.0, dtype=torch.float32)
+        lo, hi = self.qmin, self.qmax
         acc, ok = 0.0, True
         for i0 in range(0, self.n, 1 << 23):
             x = s["x"].reshape(-1)[i0:i0 + (1 << 23)].cpu()
             g = s["g"].reshape(-1)[i0:i0 + (1 << 23)].cpu()
-            r = torch.round(x / s32)
-            q = torch.clamp(r, -128, 127)
-            m = (r >= -128) & (r <= 127)
+            r = torch.round(x / s32 + z32) if self.asym else torch.round(x / s32)
+            q = torch.clamp(r, lo, hi)
+            m = (r >= lo) & (r <= hi)
             gm = torch.where(m, g * s32, torch.zeros_like(g))
-            acc += float((g * q).double().sum()) + float(((-gm) * ((x / s32) / s32)).double().sum())
+            acc += float((g * (q - z32)).double().sum()) + float(((-gm) * ((x / s32) / s32)).double().sum())
             if i0 == 0:
-                y, gx = q * s32, gm / s32
+                y, gx = (q - z32) * s32, gm / s32
                 ok = (torch.equal(y[:k].view(torch.int32), s["y"].reshape(-1)[:k].cpu().view(torch.int32))
                       and torch.equal(gx[:k].view(torch.int32), s["gx"].reshape(-1)[:k].cpu().view(torch.int32)))
         want = acc * self.gscale
@@ -815,11 +828,14 @@ def cpu_workload(workload, bits=(2, 4), frac=1):
         return ((lambda: E.per_channel_step(w, g, symmetric=False, bits=8)), w.numel(),
                 f"{rows} of the 1024 out-channels of the 1024x1024x3x3 weight, reference classes looped "
                 "over the out-channels, fwd+bwd")
-    if workload == "c3":
+    if workload in ("c3", "c3asym"):
         imgs = 512 // frac
         x = torch.randn(imgs, 3, 224, 224, generator=gen)
         g = torch.randn(imgs, 3, 224, 224, generator=gen)
-        return (lambda: E.lsq_step(x, g)), x.numel(), f"{imgs} of the 512 images of the 512x3x224x224 activation, fwd+bwd"
+        zp = C3Lsq.zp0 if workload == "c3asym" else None
+        return ((lambda: E.lsq_step(x, g, zero_point=zp)), x.numel(),
+                f"{imgs} of the 512 images of the 512x3x224x224 activation, fwd+bwd"
+                + (" (asymmetric, learnable zero point)" if zp is not None else ""))
     if workload == "c5":
         imgs = 128 // frac
         acts = [torch.randn(imgs, co, h, h, generator=gen) for _, co, _, _, h in yolov8n_backbone()]
@@ -1261,7 +1277,9 @@ def build_workload(key, a, dev, rank, world):
         return C5Calibration(dev, a.slots, 1000 * rank, batch=128, steps=16)
     if key == "act":
         return ActQuant(dev, world, rank)
-    return {"c1": C1PerTensor, "c2": C2PerChannel, "c3": C3Lsq}[key](dev, a.slots, 1000 * rank)
+    if key == "c3":
+        return C3Lsq(dev, a.slots, 1000 * rank, asym=a.asym)
+    return {"c1": C1PerTensor, "c2": C2PerChannel}[key](dev, a.slots, 1000 * rank)
 
 
 def describe(W, key, a, world):
@@ -1407,9 +1425,10 @@ def main(argv=None):
         torch.cuda.empty_cache()
     if cpu:
         # CPU legs after every GPU measurement (host threads do not disturb the timed regions)
-        out["cpu_baseline"] = cpu_baseline(a.workload, a.cpu_seconds, bits)
+        cpu_key = lambda k: "c3asym" if k == "c3" and a.asym else k   # noqa: E731
+        out["cpu_baseline"] = cpu_baseline(cpu_key(a.workload), a.cpu_seconds, bits)
         for key, e in extras.items():
-            e["cpu_baseline"] = cpu_baseline(key, a.cpu_seconds, bits)
+            e["cpu_baseline"] = cpu_baseline(cpu_key(key), a.cpu_seconds, bits)
     if "act" in extras:
         out["batched_act_quant"] = extras.pop("act")
     if extras:

@@ -53,10 +53,14 @@ def per_channel_step(w, g, symmetric=False, bits=8):
     return w.grad
 
 
-def lsq_step(x, g, scale=0.03, bits=8, act=None):
-    """Learnable symmetric fake-quant fwd + bwd (uniform.py:47-56 with ScaleGradient);
-    act="relu"/"silu": the fused layers' activation first (modules/fused.py:133)."""
-    qmin, qmax = qrange(bits, True)
+def lsq_step(x, g, scale=0.03, bits=8, act=None, zero_point=None):
+    """Learnable fake-quant fwd + bwd (uniform.py:47-56 with ScaleGradient); symmetric, or
+    with ``zero_point`` (a float) the asymmetric LSQQuantizer variant: a learnable f64 zero
+    point through zero_point_rounding (uniform.py:98-102, round STE + clamp) and its own
+    ScaleGradient (:51-52).  act="relu"/"silu": the fused layers' activation first
+    (modules/fused.py:133).  Returns (grad_x, grad_scale) (+ grad_zp when asymmetric)."""
+    asym = zero_point is not None
+    qmin, qmax = qrange(bits, not asym)
     s = torch.nn.Parameter(torch.tensor(scale, dtype=torch.float64))
     gscale = (qmax * x.numel()) ** -0.5
     x0 = x.detach().requires_grad_(True)
@@ -75,6 +79,12 @@ def lsq_step(x, g, scale=0.03, bits=8, act=None):
         def backward(ctx, gv):
             return gv * gscale
 
-    y = fake_quant(x, _ScaleGrad.apply(s), 0, qmin, qmax)
+    if not asym:
+        y = fake_quant(x, _ScaleGrad.apply(s), 0, qmin, qmax)
+        y.backward(g)
+        return x0.grad, s.grad
+    z = torch.nn.Parameter(torch.tensor(zero_point, dtype=torch.float64))
+    zr = _ScaleGrad.apply(torch.clamp(_RoundSTE.apply(z), qmin, qmax))
+    y = fake_quant(x, _ScaleGrad.apply(s), zr, qmin, qmax)
     y.backward(g)
-    return x0.grad, s.grad
+    return x0.grad, s.grad, z.grad

@@ -46,3 +46,22 @@ def test_eager_lsq(c):
     gx, gs = E.lsq_step(x, torch.from_numpy(arr(c["g"])), scale=c["scale"], bits=c["bits"])
     assert_bitwise_f32(gx.numpy(), arr(c["grad_x"]), "grad_x")
     assert abs(float(gs) - c["scale_grad"]) <= 1e-6 * max(1.0, abs(c["scale_grad"]))
+
+
+def test_lsq_step_asym_matches_oracle():
+    """The asymmetric learnable step (LSQQuantizer: learnable zero point through
+    zero_point_rounding, uniform.py:47-56, 98-102) -- bench.py's C3 --asym CPU baseline --
+    against the oracle's closed form: grad_x bitwise, scale / zp gradients to 1e-4."""
+    import numpy as np
+    import torch
+    from oracle import eager_torch as E
+    from oracle import fakequant_np as O
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 3, 16, 16, generator=gen)
+    g = torch.randn(4, 3, 16, 16, generator=gen)
+    gx, gs, gz = E.lsq_step(x, g, scale=0.03, bits=8, zero_point=3.0)
+    _, gxo, gso, gzo = O.lsq_forward_backward(x.numpy(), g.numpy(), 0.03, 3.0, 0, 255,
+                                              (255 * x.numel()) ** -0.5, learn_zp=True)
+    assert np.array_equal(gx.numpy().view(np.uint32), gxo.view(np.uint32))
+    np.testing.assert_allclose(float(gs), gso, rtol=1e-4)
+    np.testing.assert_allclose(float(gz), gzo, rtol=1e-4)
