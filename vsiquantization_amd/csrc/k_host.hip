@@ -9,7 +9,9 @@
 #include <sched.h>
 
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -20,16 +22,28 @@ namespace host {
 
 constexpr int64_t kChunk = 1 << 16;
 
+// VSIQ_HOST_THREADS, else the CPUs this process may run on: the affinity mask capped by
+// the cgroup v2 CPU quota (a shared GPU box can grant 16 CPUs' worth of time on a
+// 256-CPU affinity mask, and threads beyond the quota only queue behind each other).
 inline int usable_cpus() {
   static const int n = [] {
     if (const char *e = std::getenv("VSIQ_HOST_THREADS")) {
       const int v = std::atoi(e);
       if (v > 0) return v;
     }
+    int c = (int)std::thread::hardware_concurrency();
     cpu_set_t s;
-    if (sched_getaffinity(0, sizeof s, &s) == 0) return CPU_COUNT(&s);
-    const int h = (int)std::thread::hardware_concurrency();
-    return h > 0 ? h : 1;
+    if (sched_getaffinity(0, sizeof s, &s) == 0) c = CPU_COUNT(&s);
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long per = 0;
+      if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+        const long long quota = std::atoll(q) / per;
+        c = (int)std::min<long long>(c, std::max<long long>(1, quota));
+      }
+      std::fclose(f);
+    }
+    return c > 0 ? c : 1;
   }();
   return n;
 }
