@@ -59,8 +59,24 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
+def host_sources():
+    """Host-only C++ (csrc/host_*.cpp: the CPU-tensor path's AVX-512 loops), compiled by
+    the system C++ compiler; torch_ops.cpp is the separate torch extension."""
+    return sorted(glob.glob(os.path.join(CSRC, "host_*.cpp")))
+
+
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
+
+
+def cxx() -> str:
+    for cand in (os.environ.get("CXX"), shutil.which("g++"), shutil.which("c++")):
+        if cand and os.path.exists(cand):
+            return cand
+    return hipcc()
+
+
 def _deps():
-    return (sources() + glob.glob(os.path.join(CSRC, "*.cuh"))
+    return (sources() + host_sources() + glob.glob(os.path.join(CSRC, "*.cuh")) + glob.glob(os.path.join(CSRC, "*.h"))
             + [os.path.join(ROOT, "include", "vsiq.h"), os.path.abspath(__file__)])
 
 
@@ -80,11 +96,14 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
     newest_dep = max(os.path.getmtime(d) for d in _deps() if d.endswith((".cuh", ".h", ".py")))
 
     def compile_one(src):
-        obj = os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
+        obj = os.path.join(OBJDIR, os.path.splitext(os.path.basename(src))[0] + ".o")
         if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
                 and os.path.getmtime(obj) > newest_dep):
             return obj
-        cmd = [cc, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *inc, "-c", "-o", obj + ".tmp", src]
+        if src.endswith(".cpp"):
+            cmd = [cxx(), *HOST_FLAGS, *inc, "-c", "-o", obj + ".tmp", src]
+        else:
+            cmd = [cc, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *inc, "-c", "-o", obj + ".tmp", src]
         if verbose:
             print("[vsiq build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -93,7 +112,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> str:
 
     jobs = jobs or min(16, os.cpu_count() or 4)
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(compile_one, sources()))
+        objs = list(ex.map(compile_one, sources() + host_sources()))
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     if verbose:
         print("[vsiq build]", " ".join(cmd), flush=True)

@@ -5,22 +5,31 @@
 // with Python round()'s NaN-for-raise convention, and the SiLU exp split of torch's CPU
 // kernel.  Work is cut into fixed 64K-element chunks folded in chunk order, so every
 // result is independent of the number of host threads (VSIQ_HOST_THREADS, default the
-// CPUs this process may run on).  No device memory, no HIP calls.
+// CPUs this process may run on; a persistent pool).  No activation / ReLU run the
+// AVX-512 loops of host_simd.cpp where the CPU has them (elementwise bit-identical to
+// the scalar loops; VSIQ_HOST_SIMD=0 forces the scalar ones).  No device memory, no HIP
+// calls.
 #include <sched.h>
+#include <unistd.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
+#include "host_simd.h"
 #include "vsiq_common.cuh"
 
 namespace vsiq {
 namespace host {
 
 constexpr int64_t kChunk = 1 << 16;
+constexpr int64_t kPoolMinChunks = 4;   // below this the pool's wake-up costs more than it saves
 
 // VSIQ_HOST_THREADS, else the CPUs this process may run on: the affinity mask capped by
 // the cgroup v2 CPU quota (a shared GPU box can grant 16 CPUs' worth of time on a
@@ -48,24 +57,102 @@ inline int usable_cpus() {
   return n;
 }
 
-// f(chunk, begin, end) over the fixed chunks of [0, n), on up to usable_cpus() threads
+// Persistent workers (created on first use, usable_cpus() - 1 of them; the caller is the
+// last): run(nc, f) calls f(0..nc-1), each chunk exactly once, and returns when all are
+// done.  A call made while the pool is busy (another thread's host op) or in a forked
+// child (the workers do not exist there; DataLoader workers fork) runs serially.
+class Pool {
+ public:
+  static Pool &get() {
+    static Pool p;
+    return p;
+  }
+
+  template <class F>
+  void run(int64_t nc, F &&f) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock() || getpid() != pid_ || workers_.empty() || nc < kPoolMinChunks) {
+      for (int64_t c = 0; c < nc; ++c) f(c);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = [&f](int64_t c) { f(c); };
+      nc_.store(nc);
+      next_.store(0);
+      done_.store(0);
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_.load() == nc_.load(); });
+    job_ = nullptr;
+  }
+
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_)
+      if (t.joinable()) t.join();
+  }
+
+ private:
+  Pool() : pid_(getpid()) {
+    const int n = usable_cpus() - 1;
+    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+
+  void work() {   // take chunks until none is left
+    for (int64_t c; (c = next_.fetch_add(1)) < nc_.load();) {
+      job_(c);
+      if (done_.fetch_add(1) + 1 == nc_.load()) {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        if (!job_) continue;
+      }
+      work();
+    }
+  }
+
+  const pid_t pid_;
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int64_t)> job_;
+  std::atomic<int64_t> next_{0}, done_{0};
+  std::atomic<int64_t> nc_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// f(chunk, begin, end) over the fixed chunks of [0, n)
 template <class F>
 void for_chunks(int64_t n, F &&f) {
   const int64_t nc = cdiv(n, kChunk);
-  const int t = (int)std::min<int64_t>(usable_cpus(), nc);
-  auto run = [&](int64_t c) { f(c, c * kChunk, std::min<int64_t>(n, (c + 1) * kChunk)); };
-  if (t <= 1) {
-    for (int64_t c = 0; c < nc; ++c) run(c);
-    return;
-  }
-  std::atomic<int64_t> next{0};
-  std::vector<std::thread> th;
-  th.reserve(t);
-  for (int i = 0; i < t; ++i)
-    th.emplace_back([&] {
-      for (int64_t c; (c = next.fetch_add(1)) < nc;) run(c);
-    });
-  for (auto &x : th) x.join();
+  Pool::get().run(nc, [&](int64_t c) { f(c, c * kChunk, std::min<int64_t>(n, (c + 1) * kChunk)); });
+}
+
+// the AVX-512 loops (host_simd.cpp) for no activation / ReLU on hosts that have them
+inline bool use_simd(int kind) {
+  static const bool ok = simd::available() && std::getenv("VSIQ_HOST_SIMD") == nullptr;
+  return ok && kind != kActSilu;
 }
 
 inline float act_at(float c, int kind, int64_t e, const SiluLay &L) {
@@ -119,7 +206,12 @@ int vsiq_host_observe_f32(const float *x, int64_t n, int act, double *stats_out,
   const SiluLay L = act_lay(act, n);
   const int64_t nc = cdiv(n, kChunk);
   std::vector<double> part((size_t)nc * 6);
+  const bool vec = use_simd(kind);
   for_chunks(n, [&](int64_t c, int64_t b, int64_t e) {
+    if (vec) {
+      simd::observe(x + b, e - b, kind == kActRelu, &part[(size_t)c * 6]);
+      return;
+    }
     float mn = __builtin_inff(), mx = -__builtin_inff();
     double nan = 0.0, sa = 0.0, s1 = 0.0, s2 = 0.0;
     for (int64_t i = b; i < e; ++i) {
@@ -158,7 +250,13 @@ int vsiq_host_fq_fwd_f32(const float *x, float *y, uint8_t *codes, uint8_t *mask
                    : make_hqp(scale, zp, zp_round, qmin, qmax);
   const int kind = act_kind(act);
   const SiluLay L = act_lay(act, n);
+  const bool vec = use_simd(kind);
   for_chunks(n, [&](int64_t, int64_t b, int64_t e) {
+    if (vec) {
+      simd::fq(x + b, y + b, codes ? codes + b : nullptr, mask ? mask + b : nullptr, e - b, kind == kActRelu, p.s,
+               p.z, p.lo, p.hi, discrete);
+      return;
+    }
     for (int64_t i = b; i < e; ++i) {
       bool m;
       uint8_t c;
@@ -177,7 +275,12 @@ int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre,
   const float s = (float)scale;
   const int kind = act_kind(act);
   const SiluLay L = act_lay(act, n);
+  const bool vec = use_simd(kind);
   for_chunks(n, [&](int64_t, int64_t b, int64_t e) {
+    if (vec) {
+      simd::ste(g + b, mask + b, pre ? pre + b : nullptr, gx + b, e - b, kind == kActRelu, s);
+      return;
+    }
     for (int64_t i = b; i < e; ++i) {
       const float o = (mask[i] ? g[i] * s : 0.0f) / s;   // MulBackward0, ClampBackward1, DivBackward0
       gx[i] = kind == kActNone ? o : act_bwd_at(o, pre[i], kind, i, L);
@@ -194,7 +297,12 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
   const SiluLay L = act_lay(act, n);
   const int64_t nc = cdiv(n, kChunk);
   std::vector<double> part((size_t)nc * 2);
+  const bool vec = use_simd(kind);
   for_chunks(n, [&](int64_t c, int64_t b, int64_t e) {
+    if (vec) {
+      simd::lsq(g + b, x + b, gx + b, e - b, kind == kActRelu, p.s, p.z, p.lo, p.hi, zp_learn, &part[(size_t)c * 2]);
+      return;
+    }
     double st = 0.0, sz = 0.0;
     for (int64_t i = b; i < e; ++i) {   // autograd of uniform.py:47-56, term by term (k_body.cuh lsq_elem)
       const float xa = act_at(x[i], kind, i, L);
