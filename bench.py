@@ -965,6 +965,7 @@ def host_product_baseline(seconds):
         return q.quantize(x, s, z, False)
     t, runs = _best_time(fn, seconds)
     return {"value": x.numel() / t / 1e6, "unit": "Melem/s", "us_per_call": 1e6 * t, "host_threads": host.threads(),
+            "host_simd": host.simd(),
             "sample": f"the whole 256x256 C1 call (fresh observer, observe + fake quant), min of {runs} runs"}
 
 

@@ -526,8 +526,11 @@ int vsiq_bn_fold_f32(const float *w, const float *b, const float *gamma, const f
 /*
  * Host path (CPU tensors; the reference's own environment, BASELINE C1): the same
  * element arithmetic on HOST pointers, native C++ loops over fixed 64K-element chunks
- * on up to VSIQ_HOST_THREADS threads (default: the CPUs this process may use); results
- * do not depend on the thread count.  mask: one byte per element.
+ * on up to VSIQ_HOST_THREADS threads (default: the CPUs this process may use, capped by
+ * the cgroup CPU quota; a persistent pool for tensors of 4+ chunks); results do not
+ * depend on the thread count.  No activation / ReLU run AVX-512 loops where the CPU has
+ * them (elementwise bit-identical to the scalar loops; VSIQ_HOST_SIMD=0 forces the
+ * scalar ones).  mask: one byte per element.
  *   vsiq_host_observe_f32  = vsiq_act_observe_f32        (minmax.py:42-74, qm.py:66-68)
  *   vsiq_host_fq_fwd_f32   = vsiq_act_fq_fwd_f32         (uniform.py:55,95; qp nullable)
  *   vsiq_host_ste_bwd_f32  = vsiq_act_ste_bwd_f32        (autograd of uniform.py:55,95)
@@ -543,6 +546,7 @@ int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre,
 int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, int act, double scale, double zp,
                           int zp_learn, int qmin, int qmax, double gscale, double *grad_out);
 int vsiq_host_threads(void);
+int vsiq_host_simd(void);   /* 1: the AVX-512 loops are in use */
 
 #ifdef __cplusplus
 }

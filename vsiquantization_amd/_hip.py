@@ -148,6 +148,7 @@ _SIGS = {
     "vsiq_host_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_d], c_int),
     "vsiq_host_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_d, c_d, c_int, c_int, c_int, c_d, c_p], c_int),
     "vsiq_host_threads": ([], c_int),
+    "vsiq_host_simd": ([], c_int),
     "vsiq_act_fwd_f32": ([c_p, c_p, c_i64, c_int, c_p], c_int),
     "vsiq_act_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_p], c_int),
     "vsiq_selftest_exp_f32": ([c_p, c_p, c_p, c_i64, c_p], c_int),

@@ -340,4 +340,6 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
 
 int vsiq_host_threads(void) { return usable_cpus(); }
 
+int vsiq_host_simd(void) { return use_simd(kActNone) ? 1 : 0; }
+
 }  // extern "C"

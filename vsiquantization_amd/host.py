@@ -147,4 +147,9 @@ def threads() -> int:
     return int(H.lib().vsiq_host_threads())
 
 
-__all__ = ["is_host", "fake_quant", "fake_quant_fixed", "fake_quant_learn", "observe_tensor", "threads"]
+def simd() -> bool:
+    """True when the host loops run their AVX-512 form (csrc/host_simd.cpp)."""
+    return bool(H.lib().vsiq_host_simd())
+
+
+__all__ = ["is_host", "fake_quant", "fake_quant_fixed", "fake_quant_learn", "observe_tensor", "threads", "simd"]
