@@ -18,7 +18,10 @@ The same JSON line carries, under "configs", the other BASELINE configs measured
 the same run (C1 per-tensor, C3 LSQ, C4 YOLOv8n backbone, C5 calibration) and
 "batched_act_quant" (north_star's batched activation quant: per-call observe with the
 RCCL exchange + fake quant over a 1024-image batch split across the ranks), plus
-"api_us_per_step" (the C2 step through the public Python API).
+"api_us_per_step" (the C2 step through the public Python API), beside
+"api_torch_ref_us_per_step" (torch's own (x * 1.0).backward(g) on the same tensor and
+box) and the learnable per-call step "api_learn_us_per_step" beside torch's x * s
+("api_learn_torch_xs_us_per_step").
 
   python bench.py [--gpus N --steps K --warmup W] [--workload c1..c5] [--extras LIST]
 
@@ -282,9 +285,10 @@ class C1PerTensor(C2PerChannel):
     """C1: the reference's minimal config -- MinMaxObserver + UniformQuantizer, per-tensor
     symmetric int8, on a 256x256 fp32 weight (observers/minmax.py:76-88 then
     quantizers/uniform.py:34-56): per step the per-call observe + fake quant the manager
-    runs at this size, K9 (vsiq_act_observe_fq_parts_f32: K2p records, then one fake-quant
-    launch whose every workgroup folds them into the running min/max + f64 qparams; no
-    arrival chain); `C1_K2K1=1` times round 1's K2 observe + K1 fake quant instead.
+    runs at this size, K10 (vsiq_act_observe_fq_grid_f32: ONE launch -- K2p records, a
+    grid barrier, every workgroup folds them into the running min/max + f64 qparams and
+    quantizes from registers); `C1_K9=1` times round 2's two-launch K9 instead, `C1_K2K1=1`
+    round 1's K2 observe + K1 fake quant.
     65,536 elements: latency-bound (two launches), the GB/s are not the
     point."""
 
@@ -314,12 +318,17 @@ class C1PerTensor(C2PerChannel):
             self.slots.append(s)
             s["k9"] = (P["x"], P["y"], None, None, H.c_i64(n), 0, None, P["rmm"], P["qp"], 1, qd, 1e-8, -128, 127,
                        H.ptr(w.ws), H.c_i64(w.ws_len), st)
+            if os.environ.get("C1_K9", "0") != "1":
+                s["k9"] = s["k9"][:-1] + (H.ptr(w.counter), st)
         self.f_fwd = lib.vsiq_observe_f32
         self.f_bwd = lib.vsiq_fq_fwd_f32
-        self.f_k9 = lib.vsiq_act_observe_fq_parts_f32
+        self.f_k9 = (lib.vsiq_act_observe_fq_parts_f32 if os.environ.get("C1_K9", "0") == "1"
+                     else lib.vsiq_act_observe_fq_grid_f32)
         self.k2k1 = os.environ.get("C1_K2K1", "0") == "1"
-        # algorithmic bytes: observe reads x (4 B/elem), fake quant reads x, writes y (8)
-        self.kernels = {"observe": 4 * n, "fq_fwd": 8 * n} if self.k2k1 else {"observe_fq": 12 * n}
+        # algorithmic bytes: observe reads x (4 B/elem), fake quant reads x, writes y (8);
+        # K10 reads x once (registers across the grid barrier) and writes y: 8 B/elem
+        self.kernels = ({"observe": 4 * n, "fq_fwd": 8 * n} if self.k2k1 else
+                        {"observe_fq": (12 if os.environ.get("C1_K9", "0") == "1" else 8) * n})
 
     def launch(self, i):
         if self.k2k1:
@@ -1230,6 +1239,63 @@ def api_us_per_step(dev, steps=360, warmup=30):
     return reps[4], reps[0]
 
 
+def _interleaved_us(fns, steps=40, reps=9, warmup=30):
+    """Host + GPU time per call (us) of each step function, the reps interleaved so that
+    both see the same host load: (median, min) per function."""
+    for f in fns:
+        for i in range(warmup):
+            f(i)
+    res = [[] for _ in fns]
+    for r in range(reps):
+        for k, f in enumerate(fns):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                f(i)
+            torch.cuda.synchronize()
+            res[k].append((time.perf_counter() - t0) / steps * 1e6)
+    return [(sorted(v)[len(v) // 2], min(v)) for v in res]
+
+
+def api_torch_reference_us(dev):
+    """Torch's own trivial autograd step on the same box, the floor of any public-API
+    step there: (x * 1.0).backward(g) on the C2 weight shape (4 weights in rotation), and
+    the learnable per-call comparison -- UniformQuantizer(4, True).quantize(x, s, 0, True)
+    fwd + bwd (K1 + K4 through the C++ node, f64 scale Parameter) against torch's own
+    x * s fwd + bwd on one 8x16x20x20 activation (tools/exp/api_learn.py's case).
+    Interleaved median (and min) of 9 runs each, us per step."""
+    import vsiquantization_amd as V
+    gen = torch.Generator(device=dev).manual_seed(12)
+    xs = [(torch.randn(C2PerChannel.shape, device=dev, generator=gen) * 0.05).requires_grad_(True)
+          for _ in range(4)]
+    g = torch.randn(C2PerChannel.shape, device=dev, generator=gen)
+
+    def trivial(i):
+        x = xs[i % 4]
+        x.grad = None
+        (x * 1.0).backward(g)
+
+    xa = torch.randn(8, 16, 20, 20, device=dev, generator=gen).requires_grad_(True)
+    ga = torch.randn(8, 16, 20, 20, device=dev, generator=gen)
+    q = V.UniformQuantizer(4, True)
+    sc = torch.nn.Parameter(torch.tensor(0.05, dtype=torch.float64, device=dev))
+
+    def learn(i):
+        xa.grad = None
+        sc.grad = None
+        q.quantize(xa, sc, 0, True).backward(ga)
+
+    def torch_xs(i):
+        xa.grad = None
+        sc.grad = None
+        (xa * sc.float()).backward(ga)
+
+    (tr, tr_min), (le, le_min), (tx, tx_min) = _interleaved_us([trivial, learn, torch_xs])
+    return {"api_torch_ref_us_per_step": tr, "api_torch_ref_us_per_step_min": tr_min,
+            "api_learn_us_per_step": le, "api_learn_us_per_step_min": le_min,
+            "api_learn_torch_xs_us_per_step": tx, "api_learn_torch_xs_us_per_step_min": tx_min}
+
+
 def api_graph_us_per_step(dev, steps=300):
     """The same public-API C2 step captured once with utils.graph.GraphedStep and replayed
     (the way to drop the per-step host cost of the Python API and torch's autograd engine):
@@ -1405,6 +1471,7 @@ def main(argv=None):
         out["api_us_per_step"], out["api_us_per_step_min"] = api_us_per_step(dev)
         out["api_gate_retunes"] = gate_retunes(H) - r0
         out["api_graph_us_per_step"] = api_graph_us_per_step(dev)
+        out.update(api_torch_reference_us(dev))
         torch.cuda.empty_cache()
 
     extras = {}

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 7
+#define VSIQ_ABI_VERSION 8
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -254,6 +254,24 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
                                   double *stats_out, float *run_minmax, double *qp_out, int symmetric,
                                   double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
                                   void *stream);
+
+/*
+ * K9 in ONE launch (K10, ABI 8): the same arguments plus `counter` (the
+ * VSIQ_COUNTER_WORDS words of the stream's workspace; it uses words 33-35 and leaves
+ * them zero).  The grid is K9's K2p grid (<= 32 workgroups); each workgroup keeps its
+ * share of act(c) in registers, stores its K2p records, waits at a grid barrier on the
+ * counter, folds every record in K9's order and quantizes from registers.  Results bit
+ * for bit equal to vsiq_act_observe_fq_parts_f32, stats included.  A workgroup that
+ * waits more than ~42 ms at the barrier (the grid not co-resident) writes NaN and bumps
+ * counter word 35 instead of spinning on.  Replaces the same reference call sequence
+ * as K9 (quantization_manager.py:73-90 -> minmax.py:32-74 -> uniform.py:34-56);
+ * BASELINE C1 (256x256) and the manager's per-call observe + quantize of 16K-256K
+ * elements run on it.
+ */
+int vsiq_act_observe_fq_grid_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                                 double *stats_out, float *run_minmax, double *qp_out, int symmetric,
+                                 double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
+                                 uint32_t *counter, void *stream);
 
 /*
  * Deferred-calibration observer (K2p): the K2 pass over act(c) WITHOUT the

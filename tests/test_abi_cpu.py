@@ -116,6 +116,15 @@ def test_round2_entry_points_validate_on_host():
                                              127, 16, 16 * 4 * H.PART_LEN - 1, null) == -3   # workspace too small
     assert lib.vsiq_act_observe_fq_parts_f32(16, 16, null, 12, 16, 0, null, null, null, 1, 127.0, 1e-8, -128,
                                              127, 16, 1 << 20, null) == -2            # misaligned mask
+    k10 = lib.vsiq_act_observe_fq_grid_f32
+    assert k10(16, 16, null, null, 262145, 0, null, null, null, 1, 127.0, 1e-8, -128, 127, 16, 1 << 20, 16,
+               null) == -1                                                             # too large
+    assert k10(16, 16, null, null, 16, 0, null, null, null, 1, 127.0, 1e-8, -128, 127, 16, 1 << 20, null,
+               null) == -1                                                             # no barrier counter
+    assert k10(16, 16, null, null, 65536, 0, null, null, null, 1, 127.0, 1e-8, -128, 127, 16,
+               16 * 4 * H.PART_LEN - 1, 16, null) == -3                                # workspace too small
+    assert k10(16, 16, null, 12, 16, 0, null, null, null, 1, 127.0, 1e-8, -128, 127, 16, 1 << 20, 16,
+               null) == -2                                                             # misaligned mask
     assert lib.vsiq_lsq_part_records(0) == -1
     assert lib.vsiq_lsq_part_records(1) == 1
     assert lib.vsiq_act_lsq_bwd_part_f32(16, 16, 16, 0, 0, null, 1.0, null, 0.0, 0, -8, 7, 16, 2, null) == -1

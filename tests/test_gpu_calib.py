@@ -178,15 +178,16 @@ def test_queued_observer_detects_in_place_change():
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("sym,qmin,qmax", [(True, -128, 127), (False, 0, 255), (True, -8, 7), (False, 0, 3)])
 @pytest.mark.parametrize("n", [1, 7, 255, 256, 4097, 65535, 65536, 65537, 262143, 262144])
-@pytest.mark.parametrize("parts", [None, False, True])
+@pytest.mark.parametrize("parts", [None, False, True, "k9"])
 def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act, parts):
     """K8 (vsiq_act_observe_fq_f32: observe + qparams + fake quant of a small tensor in one
     launch) == K2 (vsiq_act_observe_f32) then K1 (vsiq_act_fq_fwd_f32 on its qparams
     record): running state, qparams record, y, codes and the 1-bit mask bit for bit, the
     stats sums to float64 reordering; three calls carry the running state (one with a NaN,
     which changes nothing, minmax.py:42-47); misaligned input takes the scalar path.
-    The same for K9 (vsiq_act_observe_fq_parts_f32: K2p records, then every fake-quant
-    workgroup folds them; parts=True, and the default above 16384 elements)."""
+    The same for K10 (vsiq_act_observe_fq_grid_f32: K2p records, a grid barrier, every
+    workgroup folds them; parts=True, and the default above 16384 elements) and K9
+    (vsiq_act_observe_fq_parts_f32, the two-launch form; parts="k9")."""
     from vsiquantization_amd import _hip as H
     from vsiquantization_amd import fakequant as FQ
     if parts is False and n > FQ.observe_fq_max_elems():
@@ -212,6 +213,65 @@ def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act, parts)
         exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
         assert torch.equal(st[exact], st2[exact])
         np.testing.assert_allclose(st.cpu().numpy(), st2.cpu().numpy(), rtol=1e-12, atol=1e-300, equal_nan=True)
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+@pytest.mark.parametrize("n", [16385, 20000, 65536, 65537, 100003, 131072, 200000, 262144])
+def test_k10_grid_barrier_equals_k9(n, act):
+    """K10 (one launch, grid barrier) == K9 (two launches) bit for bit -- y, codes, mask,
+    running state, qparams AND the stats record (the same K2p records folded in the same
+    order) -- over calls of different grid sizes back to back on one stream (the barrier
+    words are reset by the last workgroup out), and the barrier's counter words are zero
+    afterwards with no timed-out waits (counter word 35)."""
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd import fakequant as FQ
+    g = torch.Generator(device=DEV).manual_seed(n)
+    ra = torch.zeros(2, device=DEV)
+    rb = torch.zeros(2, device=DEV)
+    for m in (n, 16385 + n % 977, n):   # alternate grid sizes on the same counter words
+        for i in range(2):
+            x = torch.randn(m, device=DEV, generator=g) * (1 + i)
+            if i:
+                x[m // 3] = float("nan")
+            a = FQ.observe_fake_quant(x, symmetric=False, qmin=0, qmax=255, run_minmax=ra, act=act,
+                                      want_mask=True, want_codes=True, parts="k10")
+            b = FQ.observe_fake_quant(x, symmetric=False, qmin=0, qmax=255, run_minmax=rb, act=act,
+                                      want_mask=True, want_codes=True, parts="k9")
+            torch.cuda.synchronize()
+            assert torch.equal(ra.view(torch.int32), rb.view(torch.int32))
+            for u, v in zip(a, b):
+                assert torch.equal(u.view(torch.uint8), v.view(torch.uint8))
+    w = H.workspace(DEV, n)
+    assert w.counter[33:36].cpu().tolist() == [0, 0, 0]
+
+
+def test_k10_graph_replay_equals_eager():
+    """K10 captured in a HIP graph and replayed (BASELINE C1's launch mode in bench.py):
+    the same bits as eager, the barrier words zero after the replays."""
+    from vsiquantization_amd import _hip as H
+    from vsiquantization_amd import fakequant as FQ
+    x = torch.randn(256, 256, device=DEV)
+    ra = torch.zeros(2, device=DEV)
+    y0, qp0, st0, _, _ = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=ra)
+    s = torch.cuda.Stream(DEV)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        rb = torch.zeros(2, device=DEV)
+        FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb)   # workspace of s
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            out = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        rb.zero_()
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out[0].view(torch.int32), y0.view(torch.int32))
+    assert torch.equal(out[1].view(torch.int64), qp0.view(torch.int64))
+    assert torch.equal(out[2].view(torch.int64), st0.view(torch.int64))
+    assert torch.equal(rb, ra)
+    for w in list(H._WS.values()):   # every stream's and capture's barrier words
+        assert int(w.counter[33:36].abs().sum()) == 0
 
 
 def test_observe_fq_small_rejects_large():

@@ -14,7 +14,12 @@ procs = []
 for src in srcs:
     obj = os.path.join(tmp, os.path.basename(src) + ".o")
     objs.append(obj)
-    procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *_build.FLAGS, *defs, *inc, "-c", "-o", obj, src]))
+    procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *_build.FLAGS, *_build.FILE_FLAGS.get(os.path.basename(src), []),
+                                   *defs, *inc, "-c", "-o", obj, src]))
+for src in _build.host_sources():   # the CPU-tensor path's host loops (g++)
+    obj = os.path.join(tmp, os.path.basename(src) + ".o")
+    objs.append(obj)
+    procs.append(subprocess.Popen([_build.cxx(), *_build.HOST_FLAGS, *inc, "-c", "-o", obj, src]))
 assert all(p.wait() == 0 for p in procs)
 subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs])
 print("built", out)

@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 
 # record layouts (include/vsiq.h)
@@ -139,6 +139,8 @@ _SIGS = {
     "vsiq_observe_fq_parts_max_elems": ([], c_i64),
     "vsiq_act_observe_fq_parts_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_int,
                                        c_int, c_p, c_i64, c_p], c_int),
+    "vsiq_act_observe_fq_grid_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_int,
+                                      c_int, c_p, c_i64, c_p, c_p], c_int),
     "vsiq_observe_fold_parts": ([c_p, c_i64, c_i64, c_p, c_p], c_int),
     "vsiq_lsq_multi_workspace_doubles": ([c_p, c_int], c_i64),
     "vsiq_lsq_fwd_multi_f32": ([c_p, c_int, c_p], c_int),

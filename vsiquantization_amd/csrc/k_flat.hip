@@ -479,6 +479,191 @@ void launch_fold_fq_act(bool vec, bool nt, const float *x, float *y, uint8_t *c,
 }
 
 // ----------------------------------------------------------------------------
+// K10: K9 in ONE launch.  The grid is K2p's (fold_fq_part_grid(n) <= 32 workgroups,
+// kFoldFqU groups per lane per step, <= 2 steps up to kFoldFqMax), so every workgroup
+// holds its share of act(x) in registers (<= 8 groups per lane), accumulates it in
+// k_observe_part's order and stores its per-wave records write-through -- the same bits
+// as K9's K2p launch.  A grid barrier on two counter words replaces the kernel
+// boundary: arrive, spin (s_sleep) until every workgroup has arrived, fold all records
+// in K9's fixed order, derive the running update + f64 qparams (minmax.py:42-74) and
+// quantize from registers (uniform.py:55,95).  The running state is read BEFORE the
+// arrival, so workgroup 0's write after the barrier cannot race a reader; the last
+// workgroup to leave resets both words (stream-ordered reuse).  The grid is tiny
+// (<= 32 workgroups of 256 lanes on 256 CUs): co-resident with room to spare; a
+// workgroup that waits longer than kGridBarTimeout (42 ms) stops waiting, counts the
+// event in counter word kGridBarErrors and writes NaN, so no wave can spin forever.
+// ----------------------------------------------------------------------------
+constexpr int kGridBarArrive = 1 + kArriveGroups;   // counter words (after arrive_last's 0..32)
+constexpr int kGridBarDepart = 2 + kArriveGroups;
+constexpr int kGridBarErrors = 3 + kArriveGroups;
+static_assert(kGridBarErrors < VSIQ_COUNTER_WORDS, "counter words");
+constexpr uint64_t kGridBarTimeout = 1ull << 22;    // wall-clock ticks (100 MHz)
+
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int S>
+__global__ __launch_bounds__(kBlock) void k_observe_fq_grid(
+    const float *__restrict__ x, float *__restrict__ y, uint8_t *__restrict__ codes,
+    uint64_t *__restrict__ mask, int64_t n, double *__restrict__ parts, uint32_t *__restrict__ counter,
+    double *__restrict__ stats_out, float *__restrict__ run_minmax, double *__restrict__ qp_out, int sym,
+    double qden, double eps, float lo, float hi, SiluLay L) {
+  constexpr int U = kFoldFqU;
+  __shared__ double s_f[kWaves][6];
+  __shared__ double s_qp[2];
+  __shared__ int s_ok;
+  const int64_t ng = cdiv(n, 4);
+  const int64_t nfull = n / 4;
+  const int64_t step = (int64_t)gridDim.x * kBlock * U;
+  const int64_t b0 = (int64_t)blockIdx.x * kBlock * U;
+  const int64_t base = b0 + threadIdx.x;
+  const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
+  float state[2] = {0.f, 0.f};
+  if (run_minmax && threadIdx.x == 0) { state[0] = run_minmax[0]; state[1] = run_minmax[1]; }
+  f4 v[S * U];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[s * U + k] = load_group_c<VEC, NT>(x, base + s * step + k * kBlock, ng, n);
+  ObsAcc a;
+  obs_init(a);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (b0 + s * step >= ng) break;   // block-uniform: observe_stride_b's loop condition
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = base + s * step + k * kBlock;
+      v[s * U + k] = act_fwd4_at<ACT>(v[s * U + k], 4 * i, L);
+      if (i < nfull) obs_add4(a, v[s * U + k], 4);
+      else if (i < ng) obs_add4(a, v[s * U + k], valid_in_group(i, n));
+    }
+  }
+  // store_part_record's reductions, the record stored write-through and drained
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  if (lane == 0) {
+    double *r = parts + ((int64_t)blockIdx.x * kWaves + w) * VSIQ_PART_LEN;
+    partial_store(r + 0, a.mn); partial_store(r + 1, a.mx); partial_store(r + 2, (double)a.nan);
+    partial_store(r + 3, a.sa); partial_store(r + 4, a.s1); partial_store(r + 5, a.s2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#ifndef VSIQ_EXP_K10
+#define VSIQ_EXP_K10 0   // experiments: 1 = no grid barrier, 2 = no record fold (wrong results; timing only)
+#endif
+  if (threadIdx.x == 0 && (VSIQ_EXP_K10 & 1)) s_ok = 1;
+  if (threadIdx.x == 0 && !(VSIQ_EXP_K10 & 1)) {   // grid barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(counter + kGridBarArrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = wall_clock64();
+    int ok = 1;
+    while (__hip_atomic_load(counter + kGridBarArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+      if (wall_clock64() - t0 > kGridBarTimeout) {
+        ok = 0;
+        __hip_atomic_fetch_add(counter + kGridBarErrors, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_ok = ok;
+  }
+  __syncthreads();
+  // k_fold_fq_fwd's fold (k_observe_fold_parts' order): the same bits in every workgroup
+  const int nrec = (int)gridDim.x * kWaves;
+  double f[6];
+  ObsFold::init(f);
+  for (int i = threadIdx.x; i < ((VSIQ_EXP_K10 & 2) ? 0 : nrec); i += kBlock) {
+    const double *r = parts + (int64_t)i * VSIQ_PART_LEN;
+    const double rr[6] = {partial_load(r + 0), partial_load(r + 1), partial_load(r + 2),
+                          partial_load(r + 3), partial_load(r + 4), partial_load(r + 5)};
+    ObsFold::add(f, rr);
+  }
+  ObsFold::wave(f);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s_f[w][k] = f[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kWaves; ++i) {
+      const double rr[6] = {s_f[i][0], s_f[i][1], s_f[i][2], s_f[i][3], s_f[i][4], s_f[i][5]};
+      ObsFold::add(f, rr);
+    }
+    const bool lead = blockIdx.x == 0;
+    observer_update((float)f[0], (float)f[1], f[2] > 0.0, run_minmax ? state : nullptr, lead ? qp_out : nullptr,
+                    sym, qden, eps, &s_qp[0], &s_qp[1]);
+    if (lead) {
+      if (run_minmax) { run_minmax[0] = state[0]; run_minmax[1] = state[1]; }
+      if (stats_out) write_stats(stats_out, f, n);
+    }
+    // leave the barrier; the last workgroup out resets it for the next launch
+    if (__hip_atomic_fetch_add(counter + kGridBarDepart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        gridDim.x - 1) {
+      __hip_atomic_store(counter + kGridBarArrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(counter + kGridBarDepart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  QP p;
+  p.s = s_ok ? (float)s_qp[0] : __builtin_nanf("");
+  p.z = (float)s_qp[1];
+  p.lo = lo;
+  p.hi = hi;
+  p.discrete = 0;
+  p.d = make_fastdiv(p.s);
+  p.fast = fq_fast_qp(p.s, p.z);
+  GroupOut go[S * U];
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int sl = 0; sl < S * U; ++sl) {
+    go[sl] = fq_out_flat<VEC, CODES, MASK>(v[sl], p, base + (sl / U) * step + (sl % U) * kBlock, n);
+    if (MASK) mask_put(mlo, mhi, sl, go[sl].b);
+  }
+#pragma unroll
+  for (int sl = 0; sl < S * U; ++sl) {   // group indices increase with sl
+    const int64_t i = base + (sl / U) * step + (sl % U) * kBlock;
+    if (i - lane >= ng) break;   // whole wave past the end (uniform)
+    fq_store_out<VEC, NT, CODES>(y, codes, i, ng, n, go[sl]);
+  }
+  if (MASK && lane < 4 * S * U) {   // lane 4 sl + j: word j of slot sl's chunk
+    const int sl = lane >> 2;
+    const int64_t first = base - lane + (sl / U) * step + (sl % U) * kBlock;
+    if (first < ng) mask[4 * (first / kWave) + (lane & 3)] = ((uint64_t)mhi << 32) | mlo;
+  }
+}
+
+inline int observe_fq_grid_steps(int64_t n) {
+  return cdiv(cdiv(n, 4), fold_fq_part_grid(n) * kBlock * kFoldFqU) <= 1 ? 1 : 2;
+}
+
+template <int ACT>
+void launch_observe_fq_grid_act(bool vec, bool nt, const float *x, float *y, uint8_t *c, uint64_t *m, int64_t n,
+                                double *parts, uint32_t *counter, double *st, float *run, double *qp, int sym,
+                                double qden, double eps, float lo, float hi, const SiluLay &L, hipStream_t s) {
+  const dim3 grid((unsigned)fold_fq_part_grid(n));
+  const int steps = observe_fq_grid_steps(n);
+#define K10(V, T, C, M, S_)                                                                                      \
+  hipLaunchKernelGGL((k_observe_fq_grid<V, T, C, M, ACT, S_>), grid, dim3(kBlock), 0, s, x, y, c, m, n, parts, \
+                     counter, st, run, qp, sym, qden, eps, lo, hi, L)
+#define K10S(V, T, C, M)                \
+  if (steps == 1) { K10(V, T, C, M, 1); } \
+  else { K10(V, T, C, M, 2); }
+#define K10CM(V, T)                             \
+  if (c && m) { K10S(V, T, true, true) }        \
+  else if (c) { K10S(V, T, true, false) }       \
+  else if (m) { K10S(V, T, false, true) }       \
+  else { K10S(V, T, false, false) }
+  if (vec && nt) { K10CM(true, true) }
+  else if (vec) { K10CM(true, false) }
+  else { K10CM(false, false) }
+#undef K10CM
+#undef K10S
+#undef K10
+}
+
+// ----------------------------------------------------------------------------
 // K1r: the per-call multi-GPU observer exchange's fold + fake quant in ONE launch.  The
 // ranks' stats records (one K2 pass over each rank's shard, then one all_gather, rank
 // order) are folded by EVERY workgroup in rank order -- min / max exact, counts and sums
@@ -1118,6 +1303,22 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
   VSIQ_ACT(act, launch_fold_fq_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, ws,
            stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax, act_lay(act, n),
            (hipStream_t)stream);
+  return launch_rc();
+}
+
+int vsiq_act_observe_fq_grid_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
+                                 double *stats_out, float *run_minmax, double *qp_out, int symmetric,
+                                 double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,
+                                 uint32_t *counter, void *stream) {
+  if (n <= 0 || n > kFoldFqMax || !c || !y || !ws || !counter || qmin > qmax || !act_ok(act))
+    return VSIQ_E_ARG;
+  if (ws_len < fold_fq_part_grid(n) * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
+  if (mask && !aligned8(mask)) return VSIQ_E_ALIGN;
+  if (!aligned4(counter)) return VSIQ_E_ALIGN;
+  const bool vec = n % 4 == 0 && aligned16(c) && aligned16(y) && (!codes || aligned4(codes));
+  VSIQ_ACT(act, launch_observe_fq_grid_act, vec, g_tune.nontemporal != 0, c, y, (uint8_t *)codes, mask, n, ws,
+           counter, stats_out, run_minmax, qp_out, symmetric, qden, eps, (float)qmin, (float)qmax,
+           act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
 
