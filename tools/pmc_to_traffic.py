@@ -16,9 +16,9 @@ import sys
 # workload -> [(kernel-name fragment, bench.py kernel label, launches of it per step)];
 # a label's bytes per step = sum over its fragments of (mean per dispatch x launches)
 KERNEL_KEYS = {
-    # C1: K9 (K2p records + the fake-quant launch folding them) = one "observe_fq" step;
-    # C1_K2K1=1 runs K2 + K1 ("observe", "fq_fwd")
-    "c1": [("k_observe_part<", "observe_fq", 1), ("k_fold_fq_fwd<", "observe_fq", 1),
+    # C1: K10 (one launch, grid barrier) = one "observe_fq" step; C1_K9=1 runs K9 (K2p
+    # records + the fake-quant launch folding them); C1_K2K1=1 K2 + K1 ("observe", "fq_fwd")
+    "c1": [("k_observe_fq_grid<", "observe_fq", 1), ("k_observe_part<", "observe_fq", 1), ("k_fold_fq_fwd<", "observe_fq", 1),
            ("k_observe_loop<", "observe", 1), ("k_fq_fwd<", "fq_fwd", 1)],
     # C2: the mask-only K3 instance (MASK true, CODES false); the run also launches the
     # codes variant (9 B/elem, bench's pc_observe_fq_fwd_with_codes), which must not be
