@@ -931,11 +931,14 @@ def thread_plan(seconds=2.0):
 
 def cpu_baseline(workload, seconds, bits=(2, 4)):
     """The reference's eager-torch op sequence on the host cores: the WHOLE
-    workload, min of N wall times after a warm-up run (within `seconds`, at least one
+    workload (C4: 64 of its 256 images), min of N wall times after a warm-up run (within `seconds`, at least one
     timed run), at each thread count thread_plan() keeps (os.cpu_count() and the usable
     CPU count are both probed and recorded); value = the best whole-workload rate."""
     counts, probe, total, usable = thread_plan()
-    fn, n, desc = cpu_workload(workload, bits)
+    # C4's whole workload (547M elements fwd + bwd) takes ~5 s per run on 16 host CPUs, so
+    # a `seconds` budget held one timed run; a quarter of its images (same per-element
+    # work) gives min-of-several like the other configs
+    fn, n, desc = cpu_workload(workload, bits, frac=4 if workload == "c4" else 1)
     prev = torch.get_num_threads()
     tried, runs = {}, {}
     for th in counts:
