@@ -285,10 +285,11 @@ class C1PerTensor(C2PerChannel):
     """C1: the reference's minimal config -- MinMaxObserver + UniformQuantizer, per-tensor
     symmetric int8, on a 256x256 fp32 weight (observers/minmax.py:76-88 then
     quantizers/uniform.py:34-56): per step the per-call observe + fake quant the manager
-    runs at this size, K10 (vsiq_act_observe_fq_grid_f32: ONE launch -- K2p records, a
-    grid barrier, every workgroup folds them into the running min/max + f64 qparams and
-    quantizes from registers); `C1_K9=1` times round 2's two-launch K9 instead, `C1_K2K1=1`
-    round 1's K2 observe + K1 fake quant.
+    runs at this size, K9 (vsiq_act_observe_fq_parts_f32: K2p records, then one fake-quant
+    launch whose every workgroup folds them into the running min/max + f64 qparams; no
+    arrival chain); `C1_K10=1` times the one-launch K10 (vsiq_act_observe_fq_grid_f32: a
+    grid barrier instead of the second launch; no faster), `C1_K2K1=1` round 1's
+    K2 observe + K1 fake quant.
     65,536 elements: latency-bound (two launches), the GB/s are not the
     point."""
 
@@ -305,6 +306,7 @@ class C1PerTensor(C2PerChannel):
         st = H.stream_of(dev)
         w = H.workspace(dev, n)
         qd = qden(True, 8, 1e-8)
+        k10 = os.environ.get("C1_K10", "0") == "1"
         self.slots = []
         for i in range(slots):
             gen = torch.Generator(device=dev).manual_seed(seed_base + i)
@@ -318,17 +320,16 @@ class C1PerTensor(C2PerChannel):
             self.slots.append(s)
             s["k9"] = (P["x"], P["y"], None, None, H.c_i64(n), 0, None, P["rmm"], P["qp"], 1, qd, 1e-8, -128, 127,
                        H.ptr(w.ws), H.c_i64(w.ws_len), st)
-            if os.environ.get("C1_K9", "0") != "1":
+            if k10:
                 s["k9"] = s["k9"][:-1] + (H.ptr(w.counter), st)
         self.f_fwd = lib.vsiq_observe_f32
         self.f_bwd = lib.vsiq_fq_fwd_f32
-        self.f_k9 = (lib.vsiq_act_observe_fq_parts_f32 if os.environ.get("C1_K9", "0") == "1"
-                     else lib.vsiq_act_observe_fq_grid_f32)
+        self.f_k9 = lib.vsiq_act_observe_fq_grid_f32 if k10 else lib.vsiq_act_observe_fq_parts_f32
         self.k2k1 = os.environ.get("C1_K2K1", "0") == "1"
         # algorithmic bytes: observe reads x (4 B/elem), fake quant reads x, writes y (8);
         # K10 reads x once (registers across the grid barrier) and writes y: 8 B/elem
         self.kernels = ({"observe": 4 * n, "fq_fwd": 8 * n} if self.k2k1 else
-                        {"observe_fq": (12 if os.environ.get("C1_K9", "0") == "1" else 8) * n})
+                        {"observe_fq": (8 if k10 else 12) * n})
 
     def launch(self, i):
         if self.k2k1:

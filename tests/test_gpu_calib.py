@@ -178,16 +178,16 @@ def test_queued_observer_detects_in_place_change():
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("sym,qmin,qmax", [(True, -128, 127), (False, 0, 255), (True, -8, 7), (False, 0, 3)])
 @pytest.mark.parametrize("n", [1, 7, 255, 256, 4097, 65535, 65536, 65537, 262143, 262144])
-@pytest.mark.parametrize("parts", [None, False, True, "k9"])
+@pytest.mark.parametrize("parts", [None, False, True, "k10"])
 def test_observe_fq_small_equals_observe_then_fq(n, sym, qmin, qmax, act, parts):
     """K8 (vsiq_act_observe_fq_f32: observe + qparams + fake quant of a small tensor in one
     launch) == K2 (vsiq_act_observe_f32) then K1 (vsiq_act_fq_fwd_f32 on its qparams
     record): running state, qparams record, y, codes and the 1-bit mask bit for bit, the
     stats sums to float64 reordering; three calls carry the running state (one with a NaN,
     which changes nothing, minmax.py:42-47); misaligned input takes the scalar path.
-    The same for K10 (vsiq_act_observe_fq_grid_f32: K2p records, a grid barrier, every
-    workgroup folds them; parts=True, and the default above 16384 elements) and K9
-    (vsiq_act_observe_fq_parts_f32, the two-launch form; parts="k9")."""
+    The same for K9 (vsiq_act_observe_fq_parts_f32: K2p records, then every fake-quant
+    workgroup folds them; parts=True, and the default above 16384 elements) and K10
+    (vsiq_act_observe_fq_grid_f32, the one-launch form with a grid barrier; parts="k10")."""
     from vsiquantization_amd import _hip as H
     from vsiquantization_amd import fakequant as FQ
     if parts is False and n > FQ.observe_fq_max_elems():
@@ -252,15 +252,15 @@ def test_k10_graph_replay_equals_eager():
     from vsiquantization_amd import fakequant as FQ
     x = torch.randn(256, 256, device=DEV)
     ra = torch.zeros(2, device=DEV)
-    y0, qp0, st0, _, _ = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=ra)
+    y0, qp0, st0, _, _ = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=ra, parts="k10")
     s = torch.cuda.Stream(DEV)
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         rb = torch.zeros(2, device=DEV)
-        FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb)   # workspace of s
+        FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb, parts="k10")   # workspace of s
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=s):
-            out = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb)
+            out = FQ.observe_fake_quant(x, symmetric=True, qmin=-128, qmax=127, run_minmax=rb, parts="k10")
     torch.cuda.current_stream().wait_stream(s)
     for _ in range(3):
         rb.zero_()

@@ -542,10 +542,11 @@ __global__ __launch_bounds__(kBlock) void k_observe_fq_grid(
   a.sa = wave_reduce(a.sa, AddD());
   a.s1 = wave_reduce(a.s1, AddD());
   a.s2 = wave_reduce(a.s2, AddD());
-  if (lane == 0) {
+  if (lane < 6) {   // the reduced fields are wave-uniform: lane k stores field k (one 48-B write)
     double *r = parts + ((int64_t)blockIdx.x * kWaves + w) * VSIQ_PART_LEN;
-    partial_store(r + 0, a.mn); partial_store(r + 1, a.mx); partial_store(r + 2, (double)a.nan);
-    partial_store(r + 3, a.sa); partial_store(r + 4, a.s1); partial_store(r + 5, a.s2);
+    const double fv = lane == 0 ? (double)a.mn : lane == 1 ? (double)a.mx : lane == 2 ? (double)a.nan
+                    : lane == 3 ? a.sa : lane == 4 ? a.s1 : a.s2;
+    partial_store(r + lane, fv);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();

@@ -421,10 +421,11 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
                        want_mask: bool = False, want_codes: bool = False, parts: bool | None = None):
     """Per-tensor observe (running update, f64 qparams, stats) + fake quant of one tensor
     -- observe_tensor + fake_quant(qp=...) fused.  K8 (one launch, one workgroup) up to
-    ``_K8_ELEMS`` elements, K10 (one launch: K2p records, a grid barrier, every workgroup
-    folds them and quantizes from registers) above, up to observe_fq_parts_max_elems().
-    ``parts``: False forces K8, True / "k10" K10, "k9" round 2's two-launch K9 (the same
-    bits as K10).
+    ``_K8_ELEMS`` elements, K9 (K2p records + a fake-quant launch whose every workgroup
+    folds them; no arrival chain) above, up to observe_fq_parts_max_elems().  ``parts``:
+    False forces K8, True / "k9" K9, "k10" the one-launch K10 (K2p records, a grid
+    barrier, every workgroup folds them and quantizes from registers; the same bits as K9,
+    and no faster on MI355X: the barrier costs what the second launch does).
     Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None, codes | None)."""
     x = H.require_device_f32(x)
     n = x.numel()
@@ -438,7 +439,7 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
     codes = torch.empty(x.shape, dtype=torch.int8 if qmin < 0 else torch.uint8, device=dev) if want_codes else None
     if parts is None:
         parts = n > _K8_ELEMS
-    if parts is True or parts == "k10":
+    if parts == "k10":
         w = H.workspace(dev, n)
         rc = H.lib().vsiq_act_observe_fq_grid_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n),
                                                   H.act_code(act), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
@@ -446,7 +447,7 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
                                                   int(qmin), int(qmax), H.ptr(w.ws), _i64(w.ws_len),
                                                   H.ptr(w.counter), H.stream_of(dev))
         H.check(rc, "vsiq_act_observe_fq_grid_f32")
-    elif parts == "k9":
+    elif parts:   # True / "k9"
         w = H.workspace(dev, n)
         rc = H.lib().vsiq_act_observe_fq_parts_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n),
                                                    H.act_code(act), H.ptr(st), H.ptr(run_minmax), H.ptr(qp),
