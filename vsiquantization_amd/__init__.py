@@ -22,7 +22,7 @@ from .quantizers.uniform import UniformQuantizer, ScaleGradient, RoundStraightTh
 from .quantizers.lsq import LSQQuantizer  # noqa: F401
 from .quantizers.per_channel import PerChannelUniformQuantizer  # noqa: F401
 from .observers.minmax import MinMaxObserver  # noqa: F401
-from .observers.lsq import LSQObserver  # noqa: F401
+from .observers.minmax import LSQObserver  # noqa: F401
 from .observers.per_channel import PerChannelMinMaxObserver  # noqa: F401
 from .quantizers.quantization_manager import QuantizationManager  # noqa: F401
 from .quantizers.fake_quantize import FakeQuantize  # noqa: F401

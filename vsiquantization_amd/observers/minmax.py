@@ -139,3 +139,12 @@ class MinMaxObserver(BaseObserver):
     def __repr__(self):
         return (f"MinMaxObserver(symmetric={self.symmetric}, num_bits={self.num_bits}, "
                 f"eps={self.eps})")
+
+
+@register_class
+class LSQObserver(MinMaxObserver):
+    """The observer name README.md:131 advertises but the reference never registers
+    (SURVEY §0.1).  In the reference's QAT flow an observer only feeds the calibration
+    statistics; the LSQ step size itself is initialised from mean(|x|)
+    (QuantizationManager.init_scaling_factor_for_learning, qm.py:105-112), so
+    LSQObserver is MinMaxObserver's K2 pass under the README's name."""
