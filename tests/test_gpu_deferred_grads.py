@@ -120,7 +120,7 @@ def test_model_step_deferred_equals_per_call(multi_weights):
             torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-5, atol=1e-12, msg=na)
         else:
             assert torch.equal(pa.grad, pb.grad), na
-    assert not D._PENDING
+    assert D.pending_count() == 0
     for h in handles:
         h.remove()
 
@@ -169,4 +169,46 @@ def test_second_use_in_one_forward_takes_per_call_path():
     torch.cuda.synchronize()
     assert torch.equal(x.grad, x2.grad)
     np.testing.assert_allclose(float(q.scale.grad), float(ref.scale.grad), rtol=1e-12)
-    assert not D._PENDING
+    assert D.pending_count() == 0
+
+
+@pytest.mark.parametrize("act_learn_zp", [False, True])
+def test_deferred_cpp_node_equals_python_function(act_learn_zp, monkeypatch):
+    """The records-only backward as the C++ node (FqLearnDeferredBackward + deferred_fold,
+    the default) and as the Python DeferredLearnFn (VSIQ_TORCH_EXT=0): the same kernels and
+    arguments, so output, input gradient and every qparam gradient bit for bit, and
+    nothing left pending in either table."""
+    from vsiquantization_amd import _hip as H
+    base = _model()
+    if act_learn_zp:   # the last layer's activation quantizer: asymmetric LSQ, learned zero point
+        qm = base[2].activation_quantizer
+        qm.quantizer = V.LSQQuantizer(4, False)
+        qm.zero_point = nn.Parameter(torch.tensor(3.0, dtype=torch.float64, device=DEV))
+    x = torch.rand(4, 3, 32, 32, device=DEV)
+    res = []
+    for ext in (True, False):
+        monkeypatch.setattr(H, "torch_ext_enabled", lambda e=ext: e)
+        m = copy.deepcopy(base)
+        h = V.enable_deferred_qparam_grads(m)
+        for _ in range(2):   # two steps: the second runs on a new forward generation
+            for p in m.parameters():
+                p.grad = None
+            xi = x.clone().requires_grad_(True)
+            y = m(xi)
+            y.square().mean().backward()
+        torch.cuda.synchronize()
+        res.append((y.detach(), xi.grad, {n: p.grad.clone() for n, p in m.named_parameters()
+                                          if p.grad is not None and "quantizer" in n}))
+        assert D.pending_count() == 0
+        h.remove()
+    monkeypatch.undo()
+    (ya, ga, qa), (yb, gb, qb) = res
+    assert torch.equal(ya, yb) and torch.equal(ga, gb)
+    assert qa.keys() == qb.keys() and len(qa) >= 6
+    if act_learn_zp:
+        assert "2.activation_quantizer.zero_point" in qa
+    for n in qa:
+        if "weight_quantizer" in n:   # from MIOpen's weight-gradient conv (not bit-reproducible)
+            torch.testing.assert_close(qa[n], qb[n], rtol=1e-5, atol=1e-12, msg=n)
+        else:
+            assert torch.equal(qa[n], qb[n]), n

@@ -20,6 +20,8 @@
 //   PcObserveFqBackward  PerChannelObserveFQFn  (K3 forward, STE backward from the 1-bit mask)
 //   FqFixedBackward      FakeQuantFixedFn       (K1 / K5 forward, STE backward)
 //   FqLearnBackward      FakeQuantLearnFn       (K1 / K5 forward, K4 backward: grad_x, d scale, d zp)
+//   FqLearnDeferredBackward  quantizers/deferred.py DeferredLearnFn  (K1 / K5 forward, records-only
+//                        K4d backward; the pending calls are folded by deferred_fold)
 // Inputs are validated on the Python side (CUDA, float32, contiguous); the library
 // never allocates: every buffer here comes from torch's caching allocator, every
 // launch goes to torch's current HIP stream of the tensor's device.
@@ -29,8 +31,10 @@
 #include <torch/csrc/autograd/saved_variable.h>
 #include <c10/hip/HIPStream.h>
 
+#include <list>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <optional>
 #include <tuple>
 
@@ -295,6 +299,163 @@ Tensor fq_learn(Tensor x, std::optional<Tensor> scale, double scale_host, std::o
   return y;
 }
 
+// --------------------------------------------------------------------------- K1/K5 + K4d (deferred fold)
+// quantizers/deferred.py's DeferredLearnFn as a C++ node: the records-only backward
+// (vsiq_act_lsq_bwd_part_f32) returns placeholder qparam gradients -- views of a pending
+// f64[2] -- and registers the call here; the model's bundle node (QParamBundleFn) folds
+// every pending call in one vsiq_lsq_fold_multi launch (deferred_fold) before AccumulateGrad
+// sees the values.  Same kernels and arguments as the Python Function: the same bits.
+struct PendingFold {
+  Tensor records, out, zd;
+  int64_t nrec = 0, gen = 0;
+  double zh = 0.0, gscale = 0.0;
+  int qmin = 0, qmax = 0;
+  bool learn_zp = false;
+};
+std::mutex g_pend_mu;
+std::list<std::pair<uintptr_t, PendingFold>> g_pend;   // oldest first
+std::unordered_map<uintptr_t, std::list<std::pair<uintptr_t, PendingFold>>::iterator> g_pend_at;
+int64_t g_pend_gen = 0;
+constexpr size_t kPendMax = size_t(1) << 14;   // a backward that never reaches the bundle leaves entries
+
+struct FqLearnDeferredBackward : public Node {
+  SavedVariable x;
+  Tensor sd, zd;
+  std::vector<int64_t> s_sizes, z_sizes;
+  double scale_host = 0.0, zp_host = 0.0, gscale = 0.0;
+  int qmin = 0, qmax = 0, act = VSIQ_ACT_NONE;
+  bool learn_zp = false, grad_s = false, grad_z = false;
+  std::string name() const override { return "FqLearnDeferredBackward"; }
+  void release_variables() override {
+    x.reset_data();
+    sd.reset();
+    zd.reset();
+  }
+  variable_list apply(variable_list &&grads) override {
+    if (!grads[0].defined()) return {Tensor(), Tensor(), Tensor()};
+    const Tensor xv = x.unpack();
+    const Tensor g = grads[0].contiguous();
+    Tensor gx = at::empty_like(g);
+    PendingFold e;
+    e.nrec = vsiq_lsq_part_records(g.numel());
+    TORCH_CHECK(e.nrec > 0, "vsiq_lsq_part_records failed (", e.nrec, ")");
+    e.records = at::empty({2 * e.nrec}, g.options().dtype(at::kDouble));
+    e.out = at::empty({2}, g.options().dtype(at::kDouble));
+    check(vsiq_act_lsq_bwd_part_f32(ptr<float>(g), ptr<float>(xv), ptr<float>(gx), g.numel(), act, ptr<double>(sd),
+                                    scale_host, ptr<double>(zd), zp_host, learn_zp ? 1 : 0, qmin, qmax,
+                                    ptr<double>(e.records), 2 * e.nrec, stream_of(g)),
+          "vsiq_act_lsq_bwd_part_f32");
+    e.zd = zd;
+    e.zh = zp_host;
+    e.gscale = gscale;
+    e.qmin = qmin;
+    e.qmax = qmax;
+    e.learn_zp = learn_zp;
+    Tensor gs, gz;
+    if (grad_s) gs = e.out.select(0, 0).view(s_sizes);
+    if (learn_zp && grad_z) gz = e.out.select(0, 1).view(z_sizes);
+    const uintptr_t key = reinterpret_cast<uintptr_t>(e.out.data_ptr());
+    {
+      std::lock_guard<std::mutex> lock(g_pend_mu);
+      e.gen = g_pend_gen;
+      g_pend.emplace_back(key, std::move(e));
+      g_pend_at[key] = std::prev(g_pend.end());
+      while (g_pend.size() > kPendMax) {
+        g_pend_at.erase(g_pend.front().first);
+        g_pend.pop_front();
+      }
+    }
+    return {gx, gs, gz};
+  }
+};
+
+Tensor fq_learn_deferred(Tensor x, Tensor scale, std::optional<Tensor> zp, double zp_host, int64_t qmin,
+                         int64_t qmax, double gscale, bool learn_zp, int64_t act) {
+  Tensor y = at::empty_like(x);
+  Tensor sd = f64_on(scale, x), zd = f64_on(zp, x);
+  check(vsiq_act_fq_fwd_f32(ptr<float>(x), ptr<float>(y), nullptr, nullptr, x.numel(), (int)act, nullptr,
+                            ptr<double>(sd), 0.0, ptr<double>(zd), zp_host, learn_zp ? 1 : 0, 0, (int)qmin,
+                            (int)qmax, stream_of(x)),
+        "vsiq_act_fq_fwd_f32");
+  const Tensor zt = zp.has_value() ? *zp : Tensor();
+  if (torch::autograd::compute_requires_grad(x, scale, zt)) {
+    auto node = std::shared_ptr<FqLearnDeferredBackward>(new FqLearnDeferredBackward(), torch::autograd::deleteNode);
+    node->set_next_edges(torch::autograd::collect_next_edges(x, scale, zt));
+    node->x = SavedVariable(x, false);
+    node->sd = sd;
+    node->zd = zd;
+    node->zp_host = zp_host;
+    node->gscale = gscale;
+    node->qmin = (int)qmin;
+    node->qmax = (int)qmax;
+    node->act = (int)act;
+    node->learn_zp = learn_zp;
+    node->grad_s = needs_grad(scale);
+    node->grad_z = needs_grad(zt);
+    if (node->grad_s) node->s_sizes = scale.sizes().vec();
+    if (node->grad_z) node->z_sizes = zt.sizes().vec();
+    torch::autograd::set_history(y, node);
+  }
+  return y;
+}
+
+// Fold the pending calls whose placeholder gradients have these data pointers (a
+// grad_scale view points at out[0], a grad_zp view at out[1]) in ONE vsiq_lsq_fold_multi
+// launch on the current stream; returns how many pointers matched no pending call here.
+int64_t deferred_fold(const std::vector<int64_t> &ptrs) {
+  std::vector<PendingFold> taken;
+  int64_t missing = 0;
+  {
+    std::lock_guard<std::mutex> lock(g_pend_mu);
+    for (int64_t p : ptrs) {
+      auto it = g_pend_at.find((uintptr_t)p);
+      if (it == g_pend_at.end()) it = g_pend_at.find((uintptr_t)p - sizeof(double));
+      if (it == g_pend_at.end()) {
+        bool done = false;   // the other view of a call already taken
+        for (const auto &t : taken) {
+          const uintptr_t k = reinterpret_cast<uintptr_t>(t.out.data_ptr());
+          done = done || k == (uintptr_t)p || k + sizeof(double) == (uintptr_t)p;
+        }
+        missing += done ? 0 : 1;
+        continue;
+      }
+      taken.push_back(std::move(it->second->second));
+      g_pend.erase(it->second);
+      g_pend_at.erase(it);
+    }
+  }
+  if (taken.empty()) return missing;
+  std::vector<vsiq_lsq_fold> folds(taken.size());
+  for (size_t i = 0; i < taken.size(); ++i) {
+    const PendingFold &e = taken[i];
+    folds[i] = vsiq_lsq_fold{ptr<double>(e.records), e.nrec, ptr<double>(e.zd), e.zh, e.gscale,
+                             ptr<double>(e.out), e.qmin, e.qmax, e.learn_zp ? 1 : 0, 0};
+  }
+  check(vsiq_lsq_fold_multi(folds.data(), (int)folds.size(), stream_of(taken[0].out)), "vsiq_lsq_fold_multi");
+  return missing;
+}
+
+// A new forward generation: drop the entries of backwards older than the previous one
+// (orphans of a backward that never reached the bundle; one generation of slack for a
+// checkpointed layer whose forward re-runs inside the backward).
+void deferred_generation() {
+  std::lock_guard<std::mutex> lock(g_pend_mu);
+  ++g_pend_gen;
+  for (auto it = g_pend.begin(); it != g_pend.end();) {
+    if (it->second.gen < g_pend_gen - 1) {
+      g_pend_at.erase(it->first);
+      it = g_pend.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+int64_t deferred_pending() {
+  std::lock_guard<std::mutex> lock(g_pend_mu);
+  return (int64_t)g_pend.size();
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_vsiq_torch, m) {
@@ -306,6 +467,13 @@ PYBIND11_MODULE(_vsiq_torch, m) {
         pybind11::arg("scale_host"), pybind11::arg("zp"), pybind11::arg("zp_host"), pybind11::arg("qmin"),
         pybind11::arg("qmax"), pybind11::arg("gscale"), pybind11::arg("learn_zp"), pybind11::arg("act"),
         pybind11::arg("ws") = pybind11::none(), pybind11::arg("counter") = pybind11::none());
+  m.def("fq_learn_deferred", &fq_learn_deferred, "K1/K5 learnable fake quant; records-only K4d backward",
+        pybind11::arg("x"), pybind11::arg("scale"), pybind11::arg("zp"), pybind11::arg("zp_host"),
+        pybind11::arg("qmin"), pybind11::arg("qmax"), pybind11::arg("gscale"), pybind11::arg("learn_zp"),
+        pybind11::arg("act"));
+  m.def("deferred_fold", &deferred_fold, "fold the pending K4d calls of these placeholder gradients in one launch");
+  m.def("deferred_generation", &deferred_generation, "new forward generation: drop orphaned pending K4d calls");
+  m.def("deferred_pending", &deferred_pending, "pending K4d calls held by the C++ nodes");
   m.def("release_captures", &release_captures, "drop the C++ workspaces of the given HIP graph capture ids");
   m.def("capture_workspaces", &capture_workspaces, "number of capture-owned C++ workspaces held");
 }

@@ -79,7 +79,8 @@ def fold(entries) -> None:
 
 class DeferredLearnFn(torch.autograd.Function):
     """FakeQuantLearnFn with the records-only backward: the qparam gradients it returns
-    are placeholders (views of a pending f64[2]) that the bundle folds."""
+    are placeholders (views of a pending f64[2]) that the bundle folds.  The Python form
+    of the C++ node fq_learn_deferred (VSIQ_TORCH_EXT=0; tests compare the two)."""
 
     @staticmethod
     def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act):
@@ -112,6 +113,28 @@ class DeferredLearnFn(torch.autograd.Function):
         return gx, gs, gz, None, None, None, None, None
 
 
+def deferred_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act):
+    """Learnable fake quant whose backward is records-only (K4d): the C++ node of
+    _vsiq_torch.so (FqLearnDeferredBackward, no Python in the backward), or
+    DeferredLearnFn with VSIQ_TORCH_EXT=0."""
+    if H.torch_ext_enabled():
+        x = H.require_device_f32(x)
+        cuda_z = isinstance(zero_point, torch.Tensor) and zero_point.device.type == "cuda"
+        zt = zero_point if cuda_z else None   # a CPU tensor / number: its host value (scalar_source)
+        zh = 0.0 if cuda_z else float(zero_point)
+        return H.torch_ext().fq_learn_deferred(x, scale, zt, zh, int(qmin), int(qmax), float(gscale),
+                                               bool(learn_zp), H.act_code(act))
+    return DeferredLearnFn.apply(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
+
+
+def pending_count() -> int:
+    """Records-only backwards waiting for their bundle's fold (Python and C++ nodes)."""
+    n = len(_PENDING)
+    if H.torch_ext_enabled():
+        n += int(H.torch_ext().deferred_pending())
+    return n
+
+
 class QParamBundleFn(torch.autograd.Function):
     """Identity on the model's learnable qparams; its backward folds every pending
     records-only backward in one launch and returns the folded gradients."""
@@ -123,21 +146,26 @@ class QParamBundleFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        entries, seen = [], set()
+        entries, seen, native = [], set(), []
         for g in grads:
             if g is None:
                 continue
             p = g.data_ptr()
             e = _PENDING.get(p) or _PENDING.get(p - 8)
             if e is None:
-                raise RuntimeError("deferred qparam gradient: a bundled scale / zero point received a "
-                                   "gradient that is not a pending fold (was it used twice in one forward?)")
-            if id(e) not in seen:
+                native.append(p)   # a C++ node's pending call (or an error, below)
+            elif id(e) not in seen:
                 seen.add(id(e))
                 entries.append(e)
         fold(entries)
         for e in entries:
             _PENDING.pop(e.out.data_ptr(), None)
+        missing = len(native)
+        if native and H.torch_ext_enabled():
+            missing = int(H.torch_ext().deferred_fold(native))
+        if missing:
+            raise RuntimeError("deferred qparam gradient: a bundled scale / zero point received a "
+                               "gradient that is not a pending fold (was it used twice in one forward?)")
         return grads
 
 
@@ -165,6 +193,8 @@ def bundle_qparams(managers) -> int:
     stale = [k for k, e in _PENDING.items() if e.gen < _GEN[0] - 1]
     for k in stale:
         del _PENDING[k]
+    if H.torch_ext_enabled():
+        H.torch_ext().deferred_generation()
     picked = [qm for qm in managers if _eligible(qm)]
     if not picked or not torch.is_grad_enabled():
         return 0

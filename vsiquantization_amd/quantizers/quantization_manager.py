@@ -280,11 +280,11 @@ class QuantizationManager(nn.Module):
         if self.is_learning_scale and self.is_quantize:
             d = self.__dict__.pop("_deferred_qparams", None)   # quantizers/deferred.py bundle
             if d is not None:
-                from .deferred import DeferredLearnFn
+                from .deferred import deferred_learn
                 q = self.quantizer
                 gscale, zp, learn_zp = q.learn_args(x, d[1])
                 if not isinstance(gscale, torch.Tensor):
-                    return DeferredLearnFn.apply(x, d[0], zp, q.qmin, q.qmax, gscale, learn_zp, act)
+                    return deferred_learn(x, d[0], zp, q.qmin, q.qmax, gscale, learn_zp, act)
         self.collect_qparameter(x, act)
         if self.is_quantize:
             if act is None:
