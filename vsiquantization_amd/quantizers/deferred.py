@@ -233,10 +233,15 @@ class _Handles:
 def enable_deferred_qparam_grads(model):
     """Forward hooks on ``model``: before every forward, bundle the learnable qparams of
     its QuantizationManagers (see the module docstring); after it, drop the unused ones.
-    Returns a handle whose ``remove()`` removes both hooks."""
+    Returns a handle whose ``remove()`` removes both hooks.  The manager list is taken now
+    (two module-tree walks per forward cost ~0.2 ms of host time per step); a manager
+    added later takes the per-call path, which gives the same gradients, so enable again
+    after changing the model's structure only to defer it too."""
+    managers = _managers(model)
+
     def pre(mod, args):
-        bundle_qparams(_managers(mod))
+        bundle_qparams(managers)
 
     def post(mod, args, out):
-        clear_bundled(_managers(mod))
+        clear_bundled(managers)
     return _Handles(model.register_forward_pre_hook(pre), model.register_forward_hook(post))
