@@ -257,6 +257,22 @@ class QuantizationManager(nn.Module):
         this package's kernels it is fused into the observer and the fake quant (K5)."""
         if self.is_quantize or self.is_learning_scale:
             self._join()
+        if self.is_learning_scale and self.is_quantize:
+            # training (learnable qparams): the branches below that observe need
+            # `not is_learning_scale` and collect_qparameter returns at once, so this is
+            # the same sequence without their checks (host time per call of a QAT step)
+            if act is not None and not self._act_fusable(x):
+                x, act = _activation(x, act), None
+            d = self.__dict__.pop("_deferred_qparams", None)   # quantizers/deferred.py bundle
+            if d is not None:
+                from .deferred import deferred_learn
+                q = self.quantizer
+                gscale, zp, learn_zp = q.learn_args(x, d[1])
+                if not isinstance(gscale, torch.Tensor):
+                    return deferred_learn(x, d[0], zp, q.qmin, q.qmax, gscale, learn_zp, act)
+            if act is None:
+                return self.quantizer.quantize(x, self.scale, self.zero_point, True)
+            return self.quantizer.quantize(x, self.scale, self.zero_point, True, act=act)
         if (act is not None and not self.is_quantize and self.dist_defer and not self.is_learning_scale
                 and self.is_observer_qparam and self._act_fusable(x)
                 and not (x.requires_grad and torch.is_grad_enabled())):
@@ -277,14 +293,6 @@ class QuantizationManager(nn.Module):
                 y = self._observe_quantize_small(x, act)
             if y is not None:
                 return y
-        if self.is_learning_scale and self.is_quantize:
-            d = self.__dict__.pop("_deferred_qparams", None)   # quantizers/deferred.py bundle
-            if d is not None:
-                from .deferred import deferred_learn
-                q = self.quantizer
-                gscale, zp, learn_zp = q.learn_args(x, d[1])
-                if not isinstance(gscale, torch.Tensor):
-                    return deferred_learn(x, d[0], zp, q.qmin, q.qmax, gscale, learn_zp, act)
         self.collect_qparameter(x, act)
         if self.is_quantize:
             if act is None:
