@@ -212,3 +212,26 @@ def test_deferred_cpp_node_equals_python_function(act_learn_zp, monkeypatch):
             torch.testing.assert_close(qa[n], qb[n], rtol=1e-5, atol=1e-12, msg=n)
         else:
             assert torch.equal(qa[n], qb[n]), n
+
+
+@pytest.mark.parametrize("ext", [True, False])
+def test_orphaned_pending_folds_dropped_next_forward(ext, monkeypatch):
+    """torch.autograd.grad with respect to the input only never reaches the bundle node, so
+    its records-only backwards stay pending; they are dropped at the next forward but one
+    (one generation of slack), in the C++ table and in the Python one alike, and a normal
+    step afterwards leaves nothing pending."""
+    from vsiquantization_amd import _hip as H
+    monkeypatch.setattr(H, "torch_ext_enabled", lambda e=ext: e)
+    m = _model()
+    h = V.enable_deferred_qparam_grads(m)
+    x = torch.rand(2, 3, 32, 32, device=DEV, requires_grad=True)
+    (gx,) = torch.autograd.grad(m(x).square().mean(), x)
+    assert D.pending_count() == 3   # one per activation quantizer
+    with torch.no_grad():
+        m(x)
+        m(x)
+    assert D.pending_count() == 0
+    m(x).square().mean().backward()
+    torch.cuda.synchronize()
+    assert D.pending_count() == 0
+    h.remove()
