@@ -264,9 +264,10 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
  * for bit equal to vsiq_act_observe_fq_parts_f32, stats included.  A workgroup that
  * waits more than ~42 ms at the barrier (the grid not co-resident) writes NaN and bumps
  * counter word 35 instead of spinning on.  Replaces the same reference call sequence
- * as K9 (quantization_manager.py:73-90 -> minmax.py:32-74 -> uniform.py:34-56);
- * BASELINE C1 (256x256) and the manager's per-call observe + quantize of 16K-256K
- * elements run on it.
+ * as K9 (quantization_manager.py:73-90 -> minmax.py:32-74 -> uniform.py:34-56).
+ * Measured on MI355X no faster than K9 (the barrier's two cross-XCD round trips cost
+ * what K9's second launch boundary does), so the manager and BASELINE C1 stay on K9;
+ * this is an opt-in (observe_fake_quant(..., parts="k10")).
  */
 int vsiq_act_observe_fq_grid_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
                                  double *stats_out, float *run_minmax, double *qp_out, int symmetric,
