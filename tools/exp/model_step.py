@@ -142,17 +142,23 @@ def timed(step):
 def main():
     x = (torch.randint(0, 256, (BATCH, 3, 320, 320), generator=torch.Generator().manual_seed(9),
                        dtype=torch.uint8).float() / 255).to(dev)
+    want = os.environ.get("VARIANTS", "float,reference,ours,plus").split(",")
     base = ours(chain())
     rows = {}
-    rows["float"] = timed(step_fn(nn.Sequential(*[RefLayer(l, False) for l in base]).to(dev), x))
-    rows["reference (eager torch)"] = timed(step_fn(nn.Sequential(*[RefLayer(l, True) for l in base]).to(dev), x))
-    rows["ours"] = timed(step_fn(base, x))
-    plus = ours(chain())
-    enable_multi_tensor_weights(plus)
-    enable_deferred_qparam_grads(plus)
-    rows["ours + K7 weights + K4d deferred"] = timed(step_fn(plus, x))
+    if "float" in want:
+        rows["float"] = timed(step_fn(nn.Sequential(*[RefLayer(l, False) for l in base]).to(dev), x))
+    if "reference" in want:
+        rows["reference (eager torch)"] = timed(step_fn(nn.Sequential(*[RefLayer(l, True) for l in base]).to(dev),
+                                                        x))
+    if "ours" in want:
+        rows["ours"] = timed(step_fn(base, x))
+    if "plus" in want:
+        plus = ours(chain())
+        enable_multi_tensor_weights(plus)
+        enable_deferred_qparam_grads(plus)
+        rows["ours + K7 weights + K4d deferred"] = timed(step_fn(plus, x))
     print(f"batch {BATCH}, 27 layers, 320x320, w{BITS_W}/a{BITS_A}; ms per training step (fwd + bwd + SGD)")
-    fl = rows["float"][0]
+    fl = rows["float"][0] if "float" in rows else 0.0
     for k, (ms, loss) in rows.items():
         print(f"{k:34s} {ms:8.2f} ms   QAT overhead over float {ms - fl:7.2f} ms   first loss {loss:.6f}",
               flush=True)
