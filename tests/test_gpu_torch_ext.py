@@ -150,3 +150,38 @@ def test_public_api_host_cost_is_low():
     us = (time.perf_counter() - t) / 100 * 1e6
     print(f"public API C2 fwd+bwd: {us:.1f} us/step")
     assert np.isfinite(us)
+
+
+@pytest.mark.parametrize("with_zp", [False, True])
+def test_lsq_multi_ext_equals_python(with_zp, monkeypatch):
+    """K7 (every learnable weight quantizer in one launch each way) as the C++ node
+    LsqMultiBackward and as the Python FakeQuantLearnMultiFn: outputs, input gradients and
+    every scale / zero-point gradient bit for bit; a host-number scale and an unused
+    output (zero gradient) included."""
+    from vsiquantization_amd.fakequant import LsqSpec, lsq_fake_quant_multi
+    g0 = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(16, 3, 3, 3), (32, 16, 3, 3), (600000,), (5, 7), (300000,)]   # 600000 > 2^19: K4 inside
+    ws = [torch.randn(s, device=DEV, generator=g0) * 0.1 for s in shapes]
+    gs = [torch.randn(s, device=DEV, generator=g0) for s in shapes]
+
+    def run():
+        xs = [w.clone().requires_grad_(True) for w in ws]
+        scales = [torch.nn.Parameter(torch.tensor(0.02 + 0.01 * i, dtype=torch.float64, device=DEV))
+                  for i in range(len(xs) - 1)] + [0.05]   # the last: a host number
+        zp = torch.nn.Parameter(torch.tensor(2.0, dtype=torch.float64, device=DEV)) if with_zp else 0
+        specs = [LsqSpec(s, zp if (with_zp and i == 1) else 0, 0 if (with_zp and i == 1) else -2,
+                         15 if (with_zp and i == 1) else 1, (15 * x.numel()) ** -0.5, with_zp and i == 1)
+                 for i, (x, s) in enumerate(zip(xs, scales))]
+        ys = lsq_fake_quant_multi(xs, specs)
+        loss = sum((y * g).sum() for y, g in zip(ys[:-1], gs[:-1]))   # the last output unused
+        loss.backward()
+        out = list(ys) + [x.grad for x in xs] + [s.grad for s in scales[:-1]]
+        if with_zp:
+            out.append(zp.grad)
+        return out
+
+    a, b = both(run, monkeypatch)
+    assert len(a) == len(b)
+    for u, v in zip(a, b):
+        assert u is not None and v is not None
+        assert torch.equal(_bits(u), _bits(v))

@@ -20,6 +20,7 @@
 //   PcObserveFqBackward  PerChannelObserveFQFn  (K3 forward, STE backward from the 1-bit mask)
 //   FqFixedBackward      FakeQuantFixedFn       (K1 / K5 forward, STE backward)
 //   FqLearnBackward      FakeQuantLearnFn       (K1 / K5 forward, K4 backward: grad_x, d scale, d zp)
+//   LsqMultiBackward     FakeQuantLearnMultiFn  (K7: every weight quantizer in one launch each way)
 //   FqLearnDeferredBackward  quantizers/deferred.py DeferredLearnFn  (K1 / K5 forward, records-only
 //                        K4d backward; the pending calls are folded by deferred_fold)
 // Inputs are validated on the Python side (CUDA, float32, contiguous); the library
@@ -86,20 +87,21 @@ struct Ws {
 std::mutex g_ws_mu;
 std::map<std::tuple<int, void *, unsigned long long>, Ws> g_ws;
 
-Ws &workspace(const Tensor &like, int64_t n) {
+Ws &workspace_doubles(const Tensor &like, int64_t need) {
   const int dev = like.device().index();
   const hipStream_t st = stream_of(like);
   hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
   unsigned long long cid = 0;
   if (hipStreamGetCaptureInfo(st, &status, &cid) != hipSuccess || status != hipStreamCaptureStatusActive) cid = 0;
   const auto key = std::make_tuple(dev, cid ? nullptr : (void *)st, cid);
-  const int64_t need = vsiq_workspace_doubles(n);
   std::lock_guard<std::mutex> lock(g_ws_mu);
   Ws &w = g_ws[key];
   if (!w.counter.defined()) w.counter = at::zeros({VSIQ_COUNTER_WORDS}, like.options().dtype(at::kInt));
   if (!w.ws.defined() || w.ws.numel() < need) w.ws = at::empty({need}, like.options().dtype(at::kDouble));
   return w;
 }
+
+Ws &workspace(const Tensor &like, int64_t n) { return workspace_doubles(like, vsiq_workspace_doubles(n)); }
 
 // drop the workspaces of finished captures (utils.graph.GraphedStep.release)
 void release_captures(const std::vector<int64_t> &ids) {
@@ -435,6 +437,127 @@ int64_t deferred_fold(const std::vector<int64_t> &ptrs) {
   return missing;
 }
 
+// --------------------------------------------------------------------------- K7 (multi-tensor learnable)
+// fakequant.py's FakeQuantLearnMultiFn as a C++ node: every learnable weight quantizer of
+// a model in ONE forward launch (vsiq_lsq_fwd_multi_f32) and ONE backward launch
+// (vsiq_lsq_bwd_multi_f32); per tensor bit-identical to the single-tensor K1 / K4.
+// Inputs: the k tensors, then per tensor its scale / zero point (a device f64 tensor or
+// undefined = the host value); edges to the xs and to the scale / zp tensors that need
+// a gradient, in that order (the Python Function's input order).
+struct LsqMultiBackward : public Node {
+  std::vector<SavedVariable> xs;
+  std::vector<Tensor> sd, zd;
+  std::vector<double> sh, zh, gscale;
+  std::vector<int> qmin, qmax, learn_zp;
+  // per tensor: output slot of its scale / zp gradient (-1: none), the parameter's shape / options
+  std::vector<int64_t> s_slot, z_slot;
+  std::vector<std::vector<int64_t>> s_sizes, z_sizes;
+  std::vector<at::TensorOptions> s_opts, z_opts;
+  std::string name() const override { return "LsqMultiBackward"; }
+  void release_variables() override {
+    for (auto &x : xs) x.reset_data();
+    sd.clear();
+    zd.clear();
+  }
+  variable_list apply(variable_list &&grads) override {
+    const size_t k = xs.size();
+    std::vector<Tensor> x(k), g(k), gx(k);
+    for (size_t i = 0; i < k; ++i) {
+      x[i] = xs[i].unpack();
+      g[i] = grads[i].defined() ? grads[i].contiguous() : at::zeros_like(x[i]);
+      gx[i] = at::empty_like(x[i]);
+    }
+    Tensor go = at::empty({(int64_t)k, 2}, x[0].options().dtype(at::kDouble));
+    std::vector<vsiq_lsq_tensor> d(k);
+    for (size_t i = 0; i < k; ++i)
+      d[i] = vsiq_lsq_tensor{ptr<float>(x[i]), nullptr, ptr<float>(g[i]), ptr<float>(gx[i]), ptr<double>(sd[i]),
+                             ptr<double>(zd[i]), ptr<double>(go) + 2 * i, x[i].numel(), sh[i], zh[i], gscale[i],
+                             qmin[i], qmax[i], learn_zp[i], 0};
+    const int64_t need = vsiq_lsq_multi_workspace_doubles(d.data(), (int)k);
+    check(need < 0 ? (int)need : 0, "vsiq_lsq_multi_workspace_doubles");
+    Ws &w = workspace_doubles(x[0], need);
+    check(vsiq_lsq_bwd_multi_f32(d.data(), (int)k, ptr<double>(w.ws), w.ws.numel(), ptr<uint32_t>(w.counter),
+                                 stream_of(x[0])),
+          "vsiq_lsq_bwd_multi_f32");
+    variable_list out(num_outputs());
+    for (size_t i = 0; i < k; ++i) out[i] = gx[i];
+    for (size_t i = 0; i < k; ++i) {
+      if (s_slot[i] >= 0 && should_compute_output(s_slot[i]))
+        out[s_slot[i]] = as_param(go.select(0, i).select(0, 0), s_sizes[i], s_opts[i]);
+      if (z_slot[i] >= 0 && learn_zp[i] && should_compute_output(z_slot[i]))
+        out[z_slot[i]] = as_param(go.select(0, i).select(0, 1), z_sizes[i], z_opts[i]);
+    }
+    return out;
+  }
+};
+
+std::vector<Tensor> lsq_multi(const std::vector<Tensor> &xs, const std::vector<std::optional<Tensor>> &scales,
+                              const std::vector<double> &scale_hosts, const std::vector<std::optional<Tensor>> &zps,
+                              const std::vector<double> &zp_hosts, const std::vector<int64_t> &qmins,
+                              const std::vector<int64_t> &qmaxs, const std::vector<double> &gscales,
+                              const std::vector<bool> &learn_zps) {
+  const size_t k = xs.size();
+  TORCH_CHECK(scales.size() == k && scale_hosts.size() == k && zps.size() == k && zp_hosts.size() == k &&
+                  qmins.size() == k && qmaxs.size() == k && gscales.size() == k && learn_zps.size() == k,
+              "lsq_multi: argument lists of different lengths");
+  if (k == 0) return {};
+  std::vector<Tensor> ys(k), sd(k), zd(k), st(k), zt(k);
+  std::vector<vsiq_lsq_tensor> d(k);
+  for (size_t i = 0; i < k; ++i) {
+    TORCH_CHECK(xs[i].device() == xs[0].device(), "multi-tensor fake quant: all tensors must be on one device");
+    ys[i] = at::empty_like(xs[i]);
+    sd[i] = f64_on(scales[i], xs[i]);
+    zd[i] = f64_on(zps[i], xs[i]);
+    st[i] = scales[i].has_value() ? *scales[i] : Tensor();
+    zt[i] = zps[i].has_value() ? *zps[i] : Tensor();
+    d[i] = vsiq_lsq_tensor{ptr<float>(xs[i]), ptr<float>(ys[i]), nullptr, nullptr, ptr<double>(sd[i]),
+                           ptr<double>(zd[i]), nullptr, xs[i].numel(), scale_hosts[i], zp_hosts[i], gscales[i],
+                           (int32_t)qmins[i], (int32_t)qmaxs[i], learn_zps[i] ? 1 : 0, 0};
+  }
+  check(vsiq_lsq_fwd_multi_f32(d.data(), (int)k, stream_of(xs[0])), "vsiq_lsq_fwd_multi_f32");
+  bool any = false;
+  for (size_t i = 0; i < k; ++i) any = any || needs_grad(xs[i]) || needs_grad(st[i]) || needs_grad(zt[i]);
+  if (!any || !at::GradMode::is_enabled()) return ys;
+  auto node = std::shared_ptr<LsqMultiBackward>(new LsqMultiBackward(), torch::autograd::deleteNode);
+  torch::autograd::edge_list edges;
+  for (size_t i = 0; i < k; ++i) edges.push_back(torch::autograd::impl::gradient_edge(xs[i]));
+  node->s_slot.assign(k, -1);
+  node->z_slot.assign(k, -1);
+  node->s_sizes.resize(k);
+  node->z_sizes.resize(k);
+  node->s_opts.resize(k);
+  node->z_opts.resize(k);
+  int64_t slot = (int64_t)k;
+  for (size_t i = 0; i < k; ++i) {   // the Python Function's parameter order: scale, then zero point
+    if (needs_grad(st[i])) {
+      node->s_slot[i] = slot++;
+      node->s_sizes[i] = st[i].sizes().vec();
+      node->s_opts[i] = st[i].options();
+      edges.push_back(torch::autograd::impl::gradient_edge(st[i]));
+    }
+    if (needs_grad(zt[i])) {
+      node->z_slot[i] = slot++;
+      node->z_sizes[i] = zt[i].sizes().vec();
+      node->z_opts[i] = zt[i].options();
+      edges.push_back(torch::autograd::impl::gradient_edge(zt[i]));
+    }
+  }
+  node->set_next_edges(std::move(edges));
+  for (size_t i = 0; i < k; ++i) {
+    node->xs.emplace_back(xs[i], false);
+    node->sh.push_back(scale_hosts[i]);
+    node->zh.push_back(zp_hosts[i]);
+    node->gscale.push_back(gscales[i]);
+    node->qmin.push_back((int)qmins[i]);
+    node->qmax.push_back((int)qmaxs[i]);
+    node->learn_zp.push_back(learn_zps[i] ? 1 : 0);
+  }
+  node->sd = sd;
+  node->zd = zd;
+  torch::autograd::set_history(ys, node);
+  return ys;
+}
+
 // A new forward generation: drop the entries of backwards older than the previous one
 // (orphans of a backward that never reached the bundle; one generation of slack for a
 // checkpointed layer whose forward re-runs inside the backward).
@@ -471,6 +594,7 @@ PYBIND11_MODULE(_vsiq_torch, m) {
         pybind11::arg("x"), pybind11::arg("scale"), pybind11::arg("zp"), pybind11::arg("zp_host"),
         pybind11::arg("qmin"), pybind11::arg("qmax"), pybind11::arg("gscale"), pybind11::arg("learn_zp"),
         pybind11::arg("act"));
+  m.def("lsq_multi", &lsq_multi, "K7 multi-tensor learnable fake quant (one launch each way)");
   m.def("deferred_fold", &deferred_fold, "fold the pending K4d calls of these placeholder gradients in one launch");
   m.def("deferred_generation", &deferred_generation, "new forward generation: drop orphaned pending K4d calls");
   m.def("deferred_pending", &deferred_pending, "pending K4d calls held by the C++ nodes");

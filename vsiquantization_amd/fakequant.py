@@ -366,8 +366,30 @@ class FakeQuantLearnMultiFn(torch.autograd.Function):
         return (None, *gxs, *out)
 
 
+def _ext_qarg(v):
+    """(CUDA tensor | None, host float) of a scale / zero point for the C++ K7 node, or
+    None when only the Python Function routes it (a gradient-requiring host tensor)."""
+    if isinstance(v, torch.Tensor):
+        if v.device.type == "cuda":
+            return v, 0.0
+        if v.requires_grad:
+            return None
+        return None, float(v.detach().reshape(()).item())
+    return None, float(v)
+
+
 def lsq_fake_quant_multi(xs, specs):
-    """Learnable fake quant of every x in ``xs`` with its LsqSpec, in one launch each way."""
+    """Learnable fake quant of every x in ``xs`` with its LsqSpec, in one launch each way
+    (the C++ node LsqMultiBackward of _vsiq_torch.so, or FakeQuantLearnMultiFn with
+    VSIQ_TORCH_EXT=0)."""
+    if H.torch_ext_enabled() and xs:
+        qs = [(_ext_qarg(sp.scale), _ext_qarg(sp.zero_point)) for sp in specs]
+        if all(a is not None and b is not None for a, b in qs):
+            xs = [H.require_device_f32(x) for x in xs]
+            return tuple(H.torch_ext().lsq_multi(xs, [a[0] for a, _ in qs], [a[1] for a, _ in qs],
+                                                 [b[0] for _, b in qs], [b[1] for _, b in qs],
+                                                 [sp.qmin for sp in specs], [sp.qmax for sp in specs],
+                                                 [sp.gscale for sp in specs], [sp.learn_zp for sp in specs]))
     params = [v for sp in specs for v in (sp.scale, sp.zero_point)
               if isinstance(v, torch.Tensor) and v.requires_grad]
     return FakeQuantLearnMultiFn.apply(tuple(specs), *xs, *params)
