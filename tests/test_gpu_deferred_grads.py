@@ -235,3 +235,31 @@ def test_orphaned_pending_folds_dropped_next_forward(ext, monkeypatch):
     torch.cuda.synchronize()
     assert D.pending_count() == 0
     h.remove()
+
+
+def test_deepcopy_of_enabled_model_defers_its_own_managers():
+    """A deep copy of a model with K7 + K4d enabled (an EMA or teacher copy) runs the same
+    model-level launches on ITS OWN layers and managers: the same output and activation
+    scale gradients bit for bit as the original, nothing left pending, and the original's
+    managers untouched by the copy's forward."""
+    m = _model()
+    hs = [V.enable_deferred_qparam_grads(m), V.enable_multi_tensor_weights(m)]
+    c = copy.deepcopy(m)
+    x = torch.rand(2, 3, 32, 32, device=DEV)
+    res = []
+    for mod in (m, c):
+        for p in mod.parameters():
+            p.grad = None
+        y = mod(x)
+        assert all("_deferred_qparams" not in qm.__dict__ for qm in D._managers(m))
+        y.square().mean().backward()
+        torch.cuda.synchronize()
+        res.append((y.detach(), {n: p.grad for n, p in mod.named_parameters()
+                                 if p.grad is not None and "activation_quantizer" in n}))
+    assert D.pending_count() == 0
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1].keys() == res[1][1].keys() and len(res[0][1]) == 3
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
+    for h in hs:
+        h.remove()

@@ -26,6 +26,8 @@ with a 0-dim float64 CUDA scale (and zero point, when learned) and a scalar grad
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from .. import _hip as H
@@ -236,12 +238,20 @@ def enable_deferred_qparam_grads(model):
     Returns a handle whose ``remove()`` removes both hooks.  The manager list is taken now
     (two module-tree walks per forward cost ~0.2 ms of host time per step); a manager
     added later takes the per-call path, which gives the same gradients, so enable again
-    after changing the model's structure only to defer it too."""
-    managers = _managers(model)
+    after changing the model's structure only to defer it too.  The list is kept per
+    hooked module (weakly), so a deep copy of the model bundles its own managers."""
+    lists = weakref.WeakKeyDictionary()
+    lists[model] = _managers(model)
+
+    def managers(mod):
+        ms = lists.get(mod)
+        if ms is None:
+            ms = lists[mod] = _managers(mod)
+        return ms
 
     def pre(mod, args):
-        bundle_qparams(managers)
+        bundle_qparams(managers(mod))
 
     def post(mod, args, out):
-        clear_bundled(managers)
+        clear_bundled(managers(mod))
     return _Handles(model.register_forward_pre_hook(pre), model.register_forward_hook(post))

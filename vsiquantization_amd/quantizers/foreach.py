@@ -21,6 +21,8 @@ layer keeps its own path.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from ..fakequant import LsqSpec, lsq_fake_quant_multi
@@ -72,9 +74,14 @@ def enable_multi_tensor_weights(model):
     FakeQuantize layers before every forward.  Returns the hook handle.  The layer list is
     taken now (walking the module tree on every forward cost ~0.1 ms of host time per
     step); a layer added later quantizes its weight per call, which gives the same values,
-    so enable again after changing the model's structure only to batch it too."""
-    layers = [m for m in model.modules() if isinstance(m, FakeQuantize)]
+    so enable again after changing the model's structure only to batch it too.  The list
+    is kept per hooked module (weakly), so a deep copy of the model batches its own layers."""
+    lists = weakref.WeakKeyDictionary()
+    lists[model] = [m for m in model.modules() if isinstance(m, FakeQuantize)]
 
     def hook(mod, args):
+        layers = lists.get(mod)
+        if layers is None:
+            layers = lists[mod] = [m for m in mod.modules() if isinstance(m, FakeQuantize)]
         quantize_weights_multi(layers)
     return model.register_forward_pre_hook(hook)
