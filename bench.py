@@ -1128,13 +1128,17 @@ class _NoEvent:
         pass
 
 
-def _pick_launch(W, groups, graphs, reps=5, margin=0.01):
-    """Untimed trial: up to 4 launch groups each way, `reps` rounds, median wall time per
-    mode; graph replay is chosen only when it is faster by more than `margin` (direct
-    launches are the default).  Returns (use graph?, {mode: median ms})."""
+def _pick_launch(W, groups, graphs, reps=5, margin=0.01, min_ms=20.0, max_reps=50):
+    """Untimed trial: up to 4 launch groups each way, `reps` rounds -- more (up to
+    `max_reps`) while the trial has run less than `min_ms` per mode, so that a short
+    workload's (C1: ~0.25 ms per round) choice is not decided by host noise -- median
+    wall time per mode; graph replay is chosen only when it is faster by more than
+    `margin` (direct launches are the default).  Returns (use graph?, {mode: median ms})."""
     sel = list(range(min(4, len(groups))))
     t = {"direct": [], "graph": []}
-    for _ in range(reps):
+    r = 0
+    while r < reps or (r < max_reps and min(sum(t["direct"]), sum(t["graph"])) < min_ms):
+        r += 1
         for mode in ("direct", "graph"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -1147,7 +1151,7 @@ def _pick_launch(W, groups, graphs, reps=5, margin=0.01):
                     assert W.launch_group(g0, cnt, [_NoEvent()] * (len(graphs[j]) + 1)) == 0
             torch.cuda.synchronize()
             t[mode].append((time.perf_counter() - t0) * 1e3)
-    med = {k: sorted(v)[reps // 2] for k, v in t.items()}
+    med = {k: sorted(v)[len(v) // 2] for k, v in t.items()}
     return med["graph"] < (1.0 - margin) * med["direct"], med
 
 
