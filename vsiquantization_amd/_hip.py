@@ -218,10 +218,14 @@ def lib():
 _EXT = None
 
 
+_TORCH_EXT_ON = os.environ.get("VSIQ_TORCH_EXT", "1") != "0"   # read once: every per-call op asks
+
+
 def torch_ext_enabled() -> bool:
-    """VSIQ_TORCH_EXT=0 routes the per-call autograd paths through the Python
-    autograd.Functions over ctypes instead (same kernels; tests compare the two)."""
-    return os.environ.get("VSIQ_TORCH_EXT", "1") != "0"
+    """VSIQ_TORCH_EXT=0 (in the environment at import) routes the per-call autograd paths
+    through the Python autograd.Functions over ctypes instead (same kernels; tests compare
+    the two by patching this function)."""
+    return _TORCH_EXT_ON
 
 
 def torch_ext():
