@@ -13,6 +13,9 @@ xs = [(torch.randn(1024, 1024, 3, 3, device=dev) * 0.05).requires_grad_(True) fo
 g = torch.randn_like(xs[0])
 obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
 mode = os.environ.get("MODE", "api")
+for kv in filter(None, os.environ.get("TUNE", "").split(",")):   # e.g. TUNE=12=0 (gate autotune off)
+    k, v = kv.split("=")
+    V._hip.set_tuning(int(k), int(v))
 
 
 def step(i):
