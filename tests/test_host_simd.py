@@ -1,7 +1,7 @@
 """The host path's AVX-512 loops (csrc/host_simd.cpp) against its scalar loops
-(VSIQ_HOST_SIMD=0, run in a child process): y, integer codes, masks, STE and LSQ grad_x
-bit for bit; observer min / max / NaN count exact and the f64 sums (16 lane
-accumulators instead of one) to 1e-12; scale / zero-point gradient sums to 1e-12.
+(VSIQ_HOST_SIMD=0, run in a child process): y, integer codes, masks, STE and LSQ grad_x,
+the observer's min / max / NaN count and f64 sums, and the scale / zero-point gradient
+sums, all bit for bit (the scalar loops accumulate in the AVX-512 loops' 16-lane order).
 Lengths around the vector width and the 64K chunk; NaN, +-inf, -0.0, denormals and .5
 ties in the data; no activation and fused ReLU."""
 import os
@@ -12,7 +12,6 @@ import numpy as np
 import pytest
 
 from tests.host_simd_cases import cases, run_case
-from vsiquantization_amd import _hip as H
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -35,11 +34,8 @@ def test_simd_equals_scalar(scalar, name):
     got = run_case(*cases()[name])
     for k, v in got.items():
         want = scalar[f"{name}.{k}"]
-        if k == "stats":
-            exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
-            assert np.array_equal(v[exact], want[exact], equal_nan=True), (k, v, want)
-            np.testing.assert_allclose(v, want, rtol=1e-12, atol=1e-300, equal_nan=True, err_msg=k)
-        elif k.startswith("lsqg"):
-            np.testing.assert_allclose(v, want, rtol=1e-12, atol=1e-300, equal_nan=True, err_msg=k)
-        else:
-            assert np.array_equal(v.view(np.uint8), want.view(np.uint8)), (name, k)
+        if v.dtype.kind == "f":   # NaN payloads may differ (inf - inf vs a propagated NaN)
+            nv, nw = np.isnan(v), np.isnan(want)
+            assert np.array_equal(nv, nw), (name, k)
+            v, want = np.where(nv, 0, v).astype(v.dtype), np.where(nw, 0, want).astype(want.dtype)
+        assert np.array_equal(v.view(np.uint8), want.view(np.uint8)), (name, k, v, want)

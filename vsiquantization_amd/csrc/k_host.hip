@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -29,7 +30,8 @@ namespace vsiq {
 namespace host {
 
 constexpr int64_t kChunk = 1 << 16;
-constexpr int64_t kPoolMinChunks = 4;   // below this the pool's wake-up costs more than it saves
+constexpr int64_t kPoolMinChunks = 4;
+constexpr int kLanes = 16;               // host_simd.cpp's accumulator lanes (one __m512 of fp32)   // below this the pool's wake-up costs more than it saves
 
 // VSIQ_HOST_THREADS, else the CPUs this process may run on: the affinity mask capped by
 // the cgroup v2 CPU quota (a shared GPU box can grant 16 CPUs' worth of time on a
@@ -61,6 +63,9 @@ inline int usable_cpus() {
 // last): run(nc, f) calls f(0..nc-1), each chunk exactly once, and returns when all are
 // done.  A call made while the pool is busy (another thread's host op) or in a forked
 // child (the workers do not exist there; DataLoader workers fork) runs serially.
+// Every job has its own counters (Job, held by shared_ptr): a worker still inside work()
+// for an earlier job only ever touches that job's counters, whose next >= nc, so it can
+// neither take a chunk of the new job nor miscount its completion.
 class Pool {
  public:
   static Pool &get() {
@@ -75,19 +80,22 @@ class Pool {
       for (int64_t c = 0; c < nc; ++c) f(c);
       return;
     }
+    auto job = std::make_shared<Job>();
+    job->fn = [&f](int64_t c) { f(c); };
+    job->nc = nc;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = [&f](int64_t c) { f(c); };
-      nc_.store(nc);
-      next_.store(0);
-      done_.store(0);
+      job_ = job;
       ++gen_;
     }
     cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return done_.load() == nc_.load(); });
-    job_ = nullptr;
+    work(*job);
+    {
+      std::unique_lock<std::mutex> lk(job->mu);
+      job->cv.wait(lk, [&] { return job->done.load() == nc; });
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (job_ == job) job_.reset();
   }
 
   ~Pool() {
@@ -102,17 +110,25 @@ class Pool {
   }
 
  private:
+  struct Job {
+    std::function<void(int64_t)> fn;   // refers to the caller's frame: called only while next < nc
+    int64_t nc = 0;
+    std::atomic<int64_t> next{0}, done{0};
+    std::mutex mu;
+    std::condition_variable cv;
+  };
+
   Pool() : pid_(getpid()) {
     const int n = usable_cpus() - 1;
     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
   }
 
-  void work() {   // take chunks until none is left
-    for (int64_t c; (c = next_.fetch_add(1)) < nc_.load();) {
-      job_(c);
-      if (done_.fetch_add(1) + 1 == nc_.load()) {
-        std::lock_guard<std::mutex> lk(mu_);
-        done_cv_.notify_all();
+  static void work(Job &j) {   // take chunks of j until none is left
+    for (int64_t c; (c = j.next.fetch_add(1)) < j.nc;) {
+      j.fn(c);
+      if (j.done.fetch_add(1) + 1 == j.nc) {
+        std::lock_guard<std::mutex> lk(j.mu);
+        j.cv.notify_all();
       }
     }
   }
@@ -120,24 +136,23 @@ class Pool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
-        if (!job_) continue;
+        j = job_;
       }
-      work();
+      if (j) work(*j);
     }
   }
 
   const pid_t pid_;
   std::vector<std::thread> workers_;
   std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  std::function<void(int64_t)> job_;
-  std::atomic<int64_t> next_{0}, done_{0};
-  std::atomic<int64_t> nc_{0};
+  std::condition_variable cv_;
+  std::shared_ptr<Job> job_;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -151,7 +166,10 @@ void for_chunks(int64_t n, F &&f) {
 
 // the AVX-512 loops (host_simd.cpp) for no activation / ReLU on hosts that have them
 inline bool use_simd(int kind) {
-  static const bool ok = simd::available() && std::getenv("VSIQ_HOST_SIMD") == nullptr;
+  static const bool ok = [] {
+    const char *e = std::getenv("VSIQ_HOST_SIMD");   // "0" forces the scalar loops
+    return simd::available() && !(e && std::strcmp(e, "0") == 0);
+  }();
   return ok && kind != kActSilu;
 }
 
@@ -212,9 +230,35 @@ int vsiq_host_observe_f32(const float *x, int64_t n, int act, double *stats_out,
       simd::observe(x + b, e - b, kind == kActRelu, &part[(size_t)c * 6]);
       return;
     }
+    // host_simd.cpp's order: 16 lanes (element i + k into lane k) over the whole 16-blocks,
+    // folded in lane order, then the tail in sequence -- so the scalar and AVX-512 loops
+    // give the same sums and the same signed-zero min/max
+    float lmn[kLanes], lmx[kLanes];
+    double lsa[kLanes] = {}, ls1[kLanes] = {}, ls2[kLanes] = {}, lnan[kLanes] = {};
+    for (int k = 0; k < kLanes; ++k) lmn[k] = __builtin_inff(), lmx[k] = -__builtin_inff();
+    int64_t i = b;
+    for (; i + kLanes <= e; i += kLanes)
+      for (int k = 0; k < kLanes; ++k) {
+        const float v = act_at(x[i + k], kind, i + k, L);
+        if (v != v) lnan[k] += 1.0;
+        lmn[k] = v < lmn[k] ? v : lmn[k];
+        lmx[k] = v > lmx[k] ? v : lmx[k];
+        const double d = (double)v;
+        lsa[k] += __builtin_fabs(d);
+        ls1[k] += d;
+        ls2[k] += d * d;
+      }
     float mn = __builtin_inff(), mx = -__builtin_inff();
     double nan = 0.0, sa = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int64_t i = b; i < e; ++i) {
+    for (int k = 0; k < kLanes; ++k) {
+      mn = lmn[k] < mn ? lmn[k] : mn;
+      mx = lmx[k] > mx ? lmx[k] : mx;
+      nan += lnan[k];
+      sa += lsa[k];
+      s1 += ls1[k];
+      s2 += ls2[k];
+    }
+    for (; i < e; ++i) {
       const float v = act_at(x[i], kind, i, L);
       if (v != v) {
         nan += 1.0;
@@ -303,8 +347,10 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
       simd::lsq(g + b, x + b, gx + b, e - b, kind == kActRelu, p.s, p.z, p.lo, p.hi, zp_learn, &part[(size_t)c * 2]);
       return;
     }
-    double st = 0.0, sz = 0.0;
-    for (int64_t i = b; i < e; ++i) {   // autograd of uniform.py:47-56, term by term (k_body.cuh lsq_elem)
+    // autograd of uniform.py:47-56, term by term (k_body.cuh lsq_elem); the sums in
+    // host_simd.cpp's 16-lane order (see the observer above)
+    double lt[kLanes] = {}, lz[kLanes] = {};
+    auto elem = [&](int64_t i, double *st, double *sz) {
       const float xa = act_at(x[i], kind, i, L);
       const float u = xa / p.s;
       const float r = __builtin_rintf(u + p.z);
@@ -315,11 +361,17 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
       const float t1 = g[i] * (q - p.z);
       const float xs = u / p.s;
       const float t2 = (-gm) * xs;
-      st += (double)t1 + (double)t2;
-      if (zp_learn) sz += (double)gm + (double)(-gq);
+      *st += (double)t1 + (double)t2;
+      if (zp_learn) *sz += (double)gm + (double)(-gq);
       const float o = gm / p.s;
       gx[i] = kind == kActNone ? o : act_bwd_at(o, x[i], kind, i, L);
-    }
+    };
+    int64_t i = b;
+    for (; i + kLanes <= e; i += kLanes)
+      for (int k = 0; k < kLanes; ++k) elem(i + k, &lt[k], &lz[k]);
+    double st = 0.0, sz = 0.0;
+    for (int k = 0; k < kLanes; ++k) st += lt[k], sz += lz[k];
+    for (; i < e; ++i) elem(i, &st, &sz);
     part[(size_t)c * 2] = st;
     part[(size_t)c * 2 + 1] = sz;
   });

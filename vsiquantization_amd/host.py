@@ -1,9 +1,12 @@
 """The fake-quant path for CPU tensors: native host loops in the same library
 (csrc/k_host.hip, vsiq_host_* in include/vsiq.h) -- the reference's own environment
-(BASELINE C1: UniformQuantizer / MinMaxObserver on CPU tensors).  Same arithmetic as
-the HIP kernels, bit for bit (IEEE fp32 division, rint, NaN-propagating clamp, f64
-qparams, torch CPU's SiLU); multi-threaded over fixed chunks, results independent of
-the thread count.  This is not a fallback for CUDA tensors: a CUDA tensor never comes
+(BASELINE C1: UniformQuantizer / MinMaxObserver on CPU tensors).  The elementwise
+outputs (y, integer codes, masks, grad_x), min / max and the f64 qparams are the HIP
+kernels' bit for bit (IEEE fp32 division, rint, NaN-propagating clamp, f64 qparams,
+torch CPU's SiLU).  The f64 sums (mean|x|, mean, std, scale / zero-point gradients) are
+summed in 16 lanes per 64K chunk, folded in lane then chunk order -- the same bits with
+or without AVX-512 (VSIQ_HOST_SIMD=0) and for any thread count, but a different order
+from the GPU's tree (equal to it within the f64 rounding of the sum).  This is not a fallback for CUDA tensors: a CUDA tensor never comes
 here, and a missing library raises like every other op.
 """
 from __future__ import annotations
