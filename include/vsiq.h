@@ -103,6 +103,9 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 #define VSIQ_TUNE_XCD_ORDER 13         /* 1 (default): XCD-contiguous workgroup order where
                                           neighbouring workgroups share cache lines (K6 on
                                           channel columns); 0: hardware order */
+#define VSIQ_TUNE_K2O_FORM 14          /* K2o: 0 (default) one-shot, one record per workgroup;
+                                          1: grid-stride, vsiq_act_observe_part_f32's records */
+#define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = by size */
 int vsiq_set_tuning(int key, int value);
 
 /*
@@ -297,11 +300,15 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
                               void *stream);
 
 /*
- * K2o: vsiq_act_observe_part_f32 that also writes y = act(c) (n floats): a calibration
+ * K2o: the deferred observer pass that also writes y = act(c) (n floats): a calibration
  * forward of a fused layer in one pass -- the activation the next layer consumes
- * (modules/fused.py:133) and the deferred observer's records of it.  Records bit-identical
- * to vsiq_act_observe_part_f32(c, n, act); y bit-identical to vsiq_act_fwd_f32.
+ * (modules/fused.py:133) and the deferred observer's records of it, in the
+ * vsiq_act_observe_part_f32 record format; vsiq_observe_part_out_records(n) (<=
+ * VSIQ_PART_MAX_RECORDS) records, one per workgroup.  y bit-identical to
+ * vsiq_act_fwd_f32; folded min/max/nan/n equal to K2p's, the sums to float64 summation
+ * order (VSIQ_TUNE_K2O_FORM 1: K2p's grid, records bit-identical to it).
  */
+int64_t vsiq_observe_part_out_records(int64_t n);
 int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, double *parts, int64_t parts_len,
                                   void *stream);
 int vsiq_observe_fold_parts(const double *parts, int64_t ncalls, int64_t call_stride,
@@ -367,7 +374,11 @@ int vsiq_ste_bwd_f32(const float *g, const uint64_t *mask, float *gx, int64_t n,
  * clamp, div, mul; uniform.py:242-271):
  *   gx        = (mask ? g*s : 0) / s
  *   grad_s    = gscale * [ sum g*(q-zp) + sum (-(mask?g*s:0)) * ((x/s)/s) ]
- *   grad_zp   = gscale * [ sum (mask?g*s:0) + sum -(g*s) ] * zp_in_range      (zp_learn)
+ *   grad_zp   = gscale * [ sum (mask?g*s:0) + sum -(g*s) ] * zp_in_range      (zp_learn 1)
+ * zp_learn 1: the forward used clamp(rint(zp)) (learned zero point, uniform.py:50-52);
+ * zp_learn 2: zp as given with its gradient and no ScaleGradient factor (a symmetric
+ *   quantizer handed a gradient-requiring zero point, uniform.py:47-56):
+ *   grad_zp = sum (mask?g*s:0) + sum -(g*s);  0: no zero-point gradient.
  * sums of fp32 terms accumulated in float64, fixed reduction order (deterministic).
  * grad_out[0] = grad_s, grad_out[1] = grad_zp (device f64, overwritten).
  */
@@ -564,6 +575,22 @@ int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre,
                           double scale);
 int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, int act, double scale, double zp,
                           int zp_learn, int qmin, int qmax, double gscale, double *grad_out);
+/* Per-channel (axis 0: rows = out-channels of a [rows, rowlen] view) on the host: each row
+ * is the per-tensor host call above on that row alone (SURVEY §0.2's per-channel
+ * definition), with one running {min, max} per row (run_min / run_max fp32[rows]) and
+ * f64 qparams per row (scale_out / zp_out; zp NaN where Python round() would raise);
+ * row_stats (optional) f64[rows][3] = {sum|x|, sum x, sum x^2}; y NULL: observe only.
+ * The learnable backward takes one gscale for all rows; grad_*_out are f64[rows]. */
+int vsiq_host_pc_observe_fq_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
+                                float *run_min, float *run_max, double *scale_out, double *zp_out,
+                                double *row_stats, int symmetric, double qden, double eps, int qmin, int qmax);
+int vsiq_host_pc_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
+                            const double *scale, const double *zp, int zp_round, int qmin, int qmax);
+int vsiq_host_pc_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale);
+int vsiq_host_pc_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale, const double *zp, int zp_learn, int qmin, int qmax, double gscale,
+                             double *grad_scale_out, double *grad_zp_out);
 int vsiq_host_threads(void);
 int vsiq_host_simd(void);   /* 1: the AVX-512 loops are in use */
 

@@ -121,12 +121,18 @@ def lsq_forward_backward(x, g, scale, zero_point, qmin, qmax, gscale, learn_zp=F
     scale: float64 value of the 0-dim Parameter (cast to fp32 in the forward).
     zero_point: 0 (symmetric / int) or the f64 value of a tensor zp (asym; then
     zp_eff = clamp(round(zp)) per uniform.py:98-102).
+    learn_zp 2: a symmetric quantizer handed a gradient-requiring tensor zero point --
+    uniform.py:50 skips zero_point_rounding and ScaleGradient, so zp enters x/s + zp and
+    (x_int - zp) * s as given and its gradient carries no gscale factor.
     Returns y, grad_x, grad_scale (f64 closed form: f64 sums of the fp32 terms
     the reference sums in fp32), grad_zp (or None).
     """
     x = np.asarray(x, dtype=F32)
     g = np.asarray(g, dtype=F32)
-    if learn_zp:
+    if learn_zp == 2:
+        zp_eff = float(zero_point)
+        zp_mask = True
+    elif learn_zp:
         zr = float(np.rint(np.float64(zero_point)))
         zp_eff = min(max(zr, qmin), qmax)
         zp_mask = qmin <= zr <= qmax
@@ -150,7 +156,7 @@ def lsq_forward_backward(x, g, scale, zero_point, qmin, qmax, gscale, learn_zp=F
     if learn_zp:
         a = float(np.sum(gm, dtype=np.float64))                    # AddBackward0 (other)
         b = float(np.sum(-gq, dtype=np.float64))                   # SubBackward0 (other)
-        grad_zp = ((a + b) * gscale) if zp_mask else 0.0
+        grad_zp = (a + b) if learn_zp == 2 else (((a + b) * gscale) if zp_mask else 0.0)
     return y, gx, grad_s, grad_zp
 
 

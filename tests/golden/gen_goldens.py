@@ -266,6 +266,62 @@ for sym, bits in ((True, 8), (False, 8), (True, 4)):
         rec.update(zp=0)
     cases.append(rec)
 
+# 4c. symmetric quantizer + learnable scale + a gradient-requiring TENSOR zero point: the
+#     symmetric branch skips zero_point_rounding / ScaleGradient (uniform.py:50-52), but
+#     autograd still reaches zp through x/scale + zero_point and (x_int - zero_point) * scale
+#     (uniform.py:54-55, 95): zp used as given, integer or not, inside or outside [qmin, qmax].
+symzp_idx = 0
+for bits, zpv in ((8, 0.0), (8, 3.0), (8, 1.3), (4, -2.0), (4, 0.75), (4, 9.0), (2, 0.0)):
+    g = torch.Generator().manual_seed(60 + symzp_idx)
+    x = torch.randn((4, 3, 9, 9), generator=g)
+    gg = torch.randn((4, 3, 9, 9), generator=g)
+    q = UniformQuantizer(bits, True)
+    scale = torch.nn.Parameter(torch.tensor(np.float64(0.03 if bits == 8 else 0.3)))
+    zp = torch.nn.Parameter(torch.tensor(np.float64(zpv)))
+    xr = x.clone().requires_grad_(True)
+    y = q.quantize(xr, scale, zp, True)
+    y.backward(gg)
+    key = f"lsqz{symzp_idx}"
+    symzp_idx += 1
+    cases.append(dict(kind="learnable_fq_sym_tensor_zp", key=key, sym=True, bits=bits,
+                      scale=float(scale.detach()), scale_grad=float(scale.grad), zp=zpv,
+                      zp_grad=float(zp.grad), x=put(key + "_x", x), g=put(key + "_g", gg),
+                      y=put(key + "_y", y), grad_x=put(key + "_gx", xr.grad)))
+
+# 4d. Learnable per-channel (axis 0), by SURVEY §0.2's definition: the reference's
+#     learnable UniformQuantizer.quantize applied to each out-channel row W[c] with its own
+#     0-dim f64 scale Parameter (and, asymmetric, its own f64 zero-point Parameter, which
+#     zero_point_rounding rounds / clamps); ScaleGradient's factor is then the row's
+#     (qmax * numel(W[c])) ** -0.5 (uniform.py:58-71).
+pcl_idx = 0
+for sym, bits in ((True, 8), (True, 4), (False, 8), (False, 4)):
+    g = torch.Generator().manual_seed(80 + pcl_idx)
+    w = torch.randn(6, 5, 3, 3, generator=g) * 0.2
+    w[1] *= 8.0                                   # a row that clamps
+    gg = torch.randn(w.shape, generator=g)
+    q = UniformQuantizer(bits, sym)
+    s0 = (torch.rand(6, generator=g) * 0.02 + 0.01).double() * (1.0 if bits == 8 else 8.0)
+    z0 = [0.0] * 6 if sym else [3.0, 7.0, 0.0, 12.0, 1.0, 200.0]
+    ys, gxs, gss, gzs = [], [], [], []
+    for c in range(w.shape[0]):
+        sc = torch.nn.Parameter(s0[c].clone())
+        zc = 0 if sym else torch.nn.Parameter(torch.tensor(np.float64(z0[c])))
+        xr = w[c].clone().requires_grad_(True)
+        y = q.quantize(xr, sc, zc, True)
+        y.backward(gg[c])
+        ys.append(y.detach())
+        gxs.append(xr.grad.detach())
+        gss.append(float(sc.grad))
+        gzs.append(0.0 if sym else float(zc.grad))
+    key = f"pcl{pcl_idx}"
+    pcl_idx += 1
+    cases.append(dict(kind="per_channel_learnable", key=key, sym=sym, bits=bits, x=put(key + "_x", w),
+                      g=put(key + "_g", gg), scale=put(key + "_scale", s0),
+                      zp=put(key + "_zp", torch.tensor(z0, dtype=torch.float64)),
+                      y=put(key + "_y", torch.stack(ys)), grad_x=put(key + "_gx", torch.stack(gxs)),
+                      scale_grad=put(key + "_gs", torch.tensor(gss, dtype=torch.float64)),
+                      zp_grad=put(key + "_gz", torch.tensor(gzs, dtype=torch.float64))))
+
 # asym + learnable through the manager crashes in the reference (int zp -> torch.round(int)):
 try:
     q = UniformQuantizer(8, False)

@@ -462,3 +462,49 @@ def test_cpu_tensor_takes_the_host_path():
     _, mask, _ = FQ.fake_quant(g, 0.1, 0, -128, 127, want_mask=True)
     with pytest.raises(H.VsiqError):
         FQ.ste_backward(g, mask, 0.1, pre=torch.randn(64), act="relu")
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq_sym_tensor_zp"), ids=lambda c: c["key"])
+def test_golden_learnable_sym_tensor_zp(case):
+    """Symmetric learnable quantize with a gradient-requiring tensor zero point on the GPU
+    (K1 with zp as given + K4 zp_learn 2): y / grad_x bitwise vs the reference, the scale
+    and zero-point gradients to its fp32 sums (1e-4) and the oracle's f64 form (1e-9)."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    q = V.UniformQuantizer(case["bits"], True)
+    scale = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64, device=DEV))
+    zp = torch.nn.Parameter(torch.tensor(case["zp"], dtype=torch.float64, device=DEV))
+    xg = cu(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    # the reference sums ~3K fp32 terms in fp32 (error ~1e-6 absolute; these gradients
+    # cancel down to 1e-3..1e-2): 1e-4 relative or 3e-6 absolute; the oracle's f64 closed
+    # form below is the tight check
+    assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=3e-6)
+    assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=3e-6)
+    qmin, qmax = O.qrange(case["bits"], True)
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                              O.grad_scale(qmax, x.size), learn_zp=2)
+    assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+    assert float(zp.grad) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
+
+
+@pytest.mark.parametrize("case", G.cases("per_channel_learnable"), ids=lambda c: c["key"])
+def test_golden_per_channel_learnable(case):
+    """Learnable PerChannelUniformQuantizer (K3-fixed forward, K6 backward on axis 0) ==
+    the reference's learnable UniformQuantizer per out-channel row."""
+    w, g = G.arr(case["x"]), G.arr(case["g"])
+    sym, bits = case["sym"], case["bits"]
+    q = V.PerChannelUniformQuantizer(bits, sym)
+    s0, z0 = G.arr(case["scale"]), G.arr(case["zp"])
+    scale = torch.nn.Parameter(cu(s0.copy()))
+    zp = 0 if sym else torch.nn.Parameter(cu(z0.copy()))
+    xg = cu(w, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(cu(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    np.testing.assert_allclose(npy(scale.grad), G.arr(case["scale_grad"]), rtol=1e-4, atol=3e-6)
+    if not sym:
+        np.testing.assert_allclose(npy(zp.grad), G.arr(case["zp_grad"]), rtol=1e-4, atol=3e-6)

@@ -192,16 +192,55 @@ def test_silu_act_code_layout():
         H.set_silu_reference()
 
 
-@pytest.mark.parametrize("act", ["relu", "silu"])
-@pytest.mark.parametrize("n", [7, 4096, 100_003, 3 * 2**20 + 4])
+@pytest.mark.parametrize("act", ["relu", "silu", None])
+@pytest.mark.parametrize("n", [7, 4096, 100_003, 3 * 2**20 + 4, 26 * 2**20 + 3])
 def test_observe_parts_out_equals_act_then_parts(n, act, pin):
     """K2o (vsiq_act_observe_part_out_f32): y = act(c) and the deferred records in one
-    pass == the activation alone + K2p over c, bit for bit (records and y)."""
+    pass.  y == the activation alone == the oracle, bit for bit; the folded records ==
+    K2p's fold in min / max / NaN count / n exactly and in the sums to float64 summation
+    order (one record per one-shot workgroup instead of one per grid-stride wave); the
+    legacy grid-stride form (VSIQ_TUNE_K2O_FORM 1) gives K2p's records bit for bit."""
     pin(32, 7)
     c, _ = _inputs(n, n + 5)
     x = cu(c)
     y, parts = FQ.observe_parts_out(x, act)
+    assert parts.numel() == FQ.part_out_slot_doubles(n)
     want_parts = FQ.observe_parts(x, act=act)
-    assert torch.equal(parts.view(torch.int64), want_parts.view(torch.int64))
-    G.assert_bitwise_f32(npy(y), npy(FQ.activation(x, act)), "y")
-    G.assert_bitwise_f32(npy(y), O.act_forward(c, act, (32, 7)), "y vs oracle")
+    got, want = FQ.fold_parts(parts.reshape(1, -1)), FQ.fold_parts(want_parts.reshape(1, -1))
+    exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
+    assert torch.equal(got[0, exact], want[0, exact])
+    torch.testing.assert_close(got, want, rtol=1e-12, atol=0.0, equal_nan=True)
+    G.assert_bitwise_f32(npy(y), npy(FQ.activation(x, act) if act else x), "y")
+    if n < 2**22:
+        G.assert_bitwise_f32(npy(y), O.act_forward(c, act, (32, 7)) if act else c, "y vs oracle")
+    lib = H.lib()
+    assert lib.vsiq_set_tuning(H.TUNE_K2O_FORM, 1) == 0
+    try:
+        y1, parts1 = FQ.observe_parts_out(x, act)
+        assert torch.equal(parts1.view(torch.int64), want_parts.view(torch.int64))
+        assert torch.equal(y1.view(torch.int32), y.view(torch.int32))
+    finally:
+        assert lib.vsiq_set_tuning(H.TUNE_K2O_FORM, 0) == 0
+
+
+@pytest.mark.parametrize("groups", [1, 2, 4, 8, 16])
+def test_observe_parts_out_every_group_count(groups):
+    """Every one-shot K2o groups-per-lane instance (VSIQ_TUNE_K2O_GROUPS) on a ragged,
+    misaligned-tail tensor: y bitwise, folded min / max / NaN exact and sums to f64
+    order against K2p."""
+    lib = H.lib()
+    c, _ = _inputs(5 * 2**20 + 13, groups)
+    c = np.nan_to_num(c, nan=0.5, posinf=50.0, neginf=-50.0)   # finite: the sums are compared too
+    x = cu(c)
+    want = FQ.fold_parts(FQ.observe_parts(x, act="relu").reshape(1, -1))
+    assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, groups) == 0
+    try:
+        y, parts = FQ.observe_parts_out(x, "relu")
+        assert parts.numel() == lib.vsiq_observe_part_out_records(H.c_i64(x.numel())) * H.PART_LEN
+    finally:
+        assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, 0) == 0
+    got = FQ.fold_parts(parts.reshape(1, -1))
+    exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
+    assert torch.equal(got[0, exact], want[0, exact])
+    torch.testing.assert_close(got, want, rtol=1e-12, atol=0.0, equal_nan=True)
+    G.assert_bitwise_f32(npy(y), npy(torch.relu(x)), "y")

@@ -164,3 +164,101 @@ def test_host_stats_record_vs_oracle(n):
 
 def test_host_threads_reported():
     assert host.threads() >= 1
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq_sym_tensor_zp"), ids=lambda c: c["key"])
+def test_golden_learnable_sym_tensor_zp(case):
+    """UniformQuantizer(bits, True).quantize(x, scale, zp_tensor_requiring_grad, True) on
+    CPU tensors (host path, zp_learn 2) == the reference: y / grad_x bitwise, gradients
+    to the reference's fp32 sums (1e-4) and the oracle's f64 closed form (1e-9)."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    q = V.UniformQuantizer(case["bits"], True)
+    scale = torch.nn.Parameter(torch.tensor(case["scale"], dtype=torch.float64))
+    zp = torch.nn.Parameter(torch.tensor(case["zp"], dtype=torch.float64))
+    xg = t(x, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    # the reference sums ~3K fp32 terms in fp32 (error ~1e-6 absolute; these gradients
+    # cancel down to 1e-3..1e-2): 1e-4 relative or 3e-6 absolute; the oracle's f64 closed
+    # form below is the tight check
+    assert float(scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4, abs=3e-6)
+    assert float(zp.grad) == pytest.approx(case["zp_grad"], rel=1e-4, abs=3e-6)
+    qmin, qmax = O.qrange(case["bits"], True)
+    _, _, gs_o, gz_o = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                              O.grad_scale(qmax, x.size), learn_zp=2)
+    assert float(scale.grad) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+    assert float(zp.grad) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("case", G.cases("per_channel_observe_fq"), ids=lambda c: c["key"])
+def test_golden_per_channel_on_cpu(case, fused):
+    """PerChannelMinMaxObserver / PerChannelUniformQuantizer on CPU tensors (the native host
+    loops row by row) == the reference classes looped over out-channels."""
+    w = G.arr(case["x"])
+    obs = V.PerChannelMinMaxObserver(case["sym"], case["obs_bits"])
+    q = V.PerChannelUniformQuantizer(case["bits"], case["sym"])
+    xg = t(w, grad=True)
+    if fused:
+        y, rs = obs.observe_quantize(xg, q, want_row_stats=True)
+        s, z = obs.get_scale_zero_point()
+        assert rs.shape == (w.shape[0], 3)
+    else:
+        s, z = obs.forward(xg.detach())
+        y = q.quantize(xg, s, z, False)
+    assert s.device.type == "cpu" and z.device.type == "cpu"
+    assert np.array_equal(npy(s), G.arr(case["scale"]), equal_nan=True)
+    assert np.array_equal(npy(z), G.arr(case["zp"]).astype(np.float64))
+    assert np.array_equal(npy(obs.min_val), G.arr(case["min_val"]))
+    assert np.array_equal(npy(obs.max_val), G.arr(case["max_val"]))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(G.arr(case["g"])))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+
+
+@pytest.mark.parametrize("case", G.cases("per_channel_learnable"), ids=lambda c: c["key"])
+def test_golden_per_channel_learnable_on_cpu(case):
+    """Learnable PerChannelUniformQuantizer on CPU tensors == the reference's learnable
+    UniformQuantizer.quantize per out-channel row: y / grad_x bitwise, per-row scale and
+    zero-point gradients to the reference's fp32 sums (1e-4) and the f64 closed form."""
+    w, g = G.arr(case["x"]), G.arr(case["g"])
+    sym, bits = case["sym"], case["bits"]
+    q = V.PerChannelUniformQuantizer(bits, sym)
+    s0, z0 = G.arr(case["scale"]), G.arr(case["zp"])
+    scale = torch.nn.Parameter(torch.from_numpy(s0.copy()))
+    zp = 0 if sym else torch.nn.Parameter(torch.from_numpy(z0.copy()))
+    xg = t(w, grad=True)
+    y = q.quantize(xg, scale, zp, True)
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    y.backward(t(g))
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    np.testing.assert_allclose(npy(scale.grad), G.arr(case["scale_grad"]), rtol=1e-4, atol=3e-6)
+    qmin, qmax = O.qrange(bits, sym)
+    C = w.shape[0]
+    for c in range(C):
+        _, _, gs_o, gz_o = O.lsq_forward_backward(w[c], g[c], s0[c], z0[c], qmin, qmax,
+                                                  O.grad_scale(qmax, w[c].size), learn_zp=not sym)
+        assert float(scale.grad[c]) == pytest.approx(gs_o, rel=1e-9, abs=1e-12)
+        if not sym:
+            assert float(zp.grad[c]) == pytest.approx(gz_o, rel=1e-9, abs=1e-12)
+    if not sym:
+        np.testing.assert_allclose(npy(zp.grad), G.arr(case["zp_grad"]), rtol=1e-4, atol=3e-6)
+
+
+def test_per_channel_host_rows_parallel_equal_single_rows():
+    """Many rows (the pool over rows) and a few long rows (the pool inside each row) give
+    each row exactly what the per-tensor host path gives that row alone."""
+    rng = np.random.default_rng(3)
+    for shape in ((64, 3, 3, 3), (3, 70000)):
+        w = (rng.standard_normal(shape) * 0.1).astype(np.float32)
+        obs = V.PerChannelMinMaxObserver(False)
+        q = V.PerChannelUniformQuantizer(8, False)
+        y, _ = obs.observe_quantize(t(w), q)
+        for c in range(shape[0]):
+            o1 = V.MinMaxObserver(False)
+            s, z = o1.forward(t(w[c]))
+            assert float(obs.scale[c]) == s and float(obs.zero_point[c]) == z
+            G.assert_bitwise_f32(npy(y[c]), npy(V.UniformQuantizer(8, False).quantize(t(w[c]), s, z, False)),
+                                 f"row {c}")

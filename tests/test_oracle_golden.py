@@ -201,3 +201,20 @@ def test_lsq_fake_quantize(case):
     G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
     np.testing.assert_allclose(gs, G.arr(case["scale_grad"]).reshape(-1), rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(gz, G.arr(case["zp_grad"]).reshape(-1), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", G.cases("learnable_fq_sym_tensor_zp"), ids=lambda c: c["key"])
+def test_learnable_sym_tensor_zp(case):
+    """Symmetric learnable quantize with a gradient-requiring tensor zero point
+    (uniform.py:47-56: no zero_point_rounding / ScaleGradient on zp in the symmetric
+    branch): zp as given; its gradient sum g*s*(mask-1) without gscale."""
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    qmin, qmax = O.qrange(case["bits"], True)
+    y, gx, gsc, gzp = O.lsq_forward_backward(x, g, case["scale"], case["zp"], qmin, qmax,
+                                             O.grad_scale(qmax, x.size), learn_zp=2)
+    G.assert_bitwise_f32(y, G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(gx, G.arr(case["grad_x"]), "grad_x")
+    # the reference sums ~3K fp32 terms in fp32 (error ~1e-6 absolute; these gradients
+    # cancel down to 1e-3..1e-2): 1e-4 relative or 3e-6 absolute
+    assert gsc == pytest.approx(case["scale_grad"], rel=1e-4, abs=3e-6)
+    assert gzp == pytest.approx(case["zp_grad"], rel=1e-4, abs=3e-6)

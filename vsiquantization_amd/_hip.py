@@ -40,6 +40,7 @@ TUNE_OBS_KERNEL, TUNE_OBS_GRID, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 8, 9, 10
 TUNE_STORE_GATE = 11
 TUNE_GATE_AUTOTUNE = 12
 TUNE_XCD_ORDER = 13
+TUNE_K2O_FORM, TUNE_K2O_GROUPS = 14, 15
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
@@ -126,6 +127,7 @@ _SIGS = {
     "vsiq_act_observe_f32": ([c_p, c_i64, c_int, c_p, c_p, c_p, c_int, c_d, c_d, c_p, c_i64, c_p, c_p],
                              c_int),
     "vsiq_observe_part_records": ([c_i64], c_i64),
+    "vsiq_observe_part_out_records": ([c_i64], c_i64),
     "vsiq_act_observe_part_f32": ([c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
     "vsiq_act_observe_part_multi_f32": ([c_p, c_int, c_int, c_p], c_int),
     "vsiq_act_observe_part_out_f32": ([c_p, c_p, c_i64, c_int, c_p, c_i64, c_p], c_int),
@@ -149,6 +151,12 @@ _SIGS = {
     "vsiq_host_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_d, c_d, c_int, c_int, c_int, c_int], c_int),
     "vsiq_host_ste_bwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_d], c_int),
     "vsiq_host_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_int, c_d, c_d, c_int, c_int, c_int, c_d, c_p], c_int),
+    "vsiq_host_pc_observe_fq_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_int, c_d, c_d, c_int,
+                                     c_int], c_int),
+    "vsiq_host_pc_fq_fwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int], c_int),
+    "vsiq_host_pc_ste_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p], c_int),
+    "vsiq_host_pc_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p, c_p],
+                                 c_int),
     "vsiq_host_threads": ([], c_int),
     "vsiq_host_simd": ([], c_int),
     "vsiq_act_fwd_f32": ([c_p, c_p, c_i64, c_int, c_p], c_int),

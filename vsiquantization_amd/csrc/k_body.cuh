@@ -194,6 +194,10 @@ __device__ __forceinline__ bool lsq_block_record(LsqAcc c, float *__restrict__ g
 // gradient of the zero point after the fold: ClampBackward of zero_point_rounding
 // (uniform.py:101) -- the in-range test on round(zp); NaN -> not in range
 __device__ __forceinline__ double lsq_grad_zp(double zsum, const QPSrc &src, const QP &p, double gscale) {
+  // zp_learn 2 (a symmetric quantizer given a gradient-requiring zero point,
+  // uniform.py:47-56 with `not self.symmetric` False): zp enters x/s + zp and (x_int - zp)
+  // as given -- no rounding, no clamp, no ScaleGradient
+  if (!src.zround) return zsum;
   const double zr = __builtin_rint(src.zdev ? *src.zdev : src.zhost);
   const bool zin = zr >= (double)p.lo && zr <= (double)p.hi;
   return zin ? zsum * gscale : 0.0;

@@ -278,6 +278,82 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_out(const float *__rest
   store_part_record(a, parts, blockIdx.x, gridDim.x, n);
 }
 
+// K2o one-shot form (the default): workgroup b takes groups [b*256*G, (b+1)*256*G) --
+// G loads per lane issued at once, act + observer terms in registers, the workgroup's
+// record through LDS, then the G stores: no loop, so no store shares a vmcnt wait with a
+// later load (a grid-stride step waits for its own stores before the next step's loads
+// can be consumed: hipcc's s_waitcnt treats mixed load / store counts as out of order).
+// One record per WORKGROUP, so the record count stays <= VSIQ_PART_MAX_RECORDS with a
+// grid of up to 4096 workgroups (k2o_groups: the smallest G that fits).  The block
+// reduction runs before the stores (no fence between the y stores and the barrier).
+template <bool VEC, bool NT, int ACT, int G>
+__global__ __launch_bounds__(kBlock) void k_observe_part_out1(const float *__restrict__ x, float *__restrict__ y,
+                                                               int64_t n, double *__restrict__ parts, SiluLay L) {
+  __shared__ float s_mn[kWaves], s_mx[kWaves];
+  __shared__ uint32_t s_nan[kWaves];
+  __shared__ double s_sa[kWaves], s_s1[kWaves], s_s2[kWaves];
+  const int64_t ng = cdiv(n, 4);
+  const int64_t nfull = n / 4;
+  const int64_t base = (int64_t)blockIdx.x * kBlock * G;
+  ObsAcc a;
+  obs_init(a);
+  f4 v[G];
+  const bool whole = VEC && base + (int64_t)kBlock * G <= nfull;   // block-uniform
+  if (whole) {
+    const float *xb = x + 4 * base;
+#pragma unroll
+    for (int k = 0; k < G; ++k) v[k] = ld4<NT>(xb + 4 * (threadIdx.x + k * kBlock));
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      v[k] = act_fwd4_at<ACT>(v[k], 4 * (base + threadIdx.x + k * kBlock), L);
+      obs_add4(a, v[k], 4);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + threadIdx.x + k * kBlock, ng, n);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int64_t i = base + threadIdx.x + k * kBlock;
+      v[k] = act_fwd4_at<ACT>(v[k], 4 * i, L);
+      if (i < nfull) obs_add4(a, v[k], 4);
+      else if (i < ng) obs_add4(a, v[k], valid_in_group(i, n));
+    }
+  }
+  a.mn = wave_reduce(a.mn, MinOp());
+  a.mx = wave_reduce(a.mx, MaxOp());
+  a.nan = wave_reduce(a.nan, AddU());
+  a.sa = wave_reduce(a.sa, AddD());
+  a.s1 = wave_reduce(a.s1, AddD());
+  a.s2 = wave_reduce(a.s2, AddD());
+  const int w = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) {
+    s_mn[w] = a.mn; s_mx[w] = a.mx; s_nan[w] = a.nan;
+    s_sa[w] = a.sa; s_s1[w] = a.s1; s_s2[w] = a.s2;
+  }
+  __syncthreads();
+  if (whole) {
+    float *yb = y + 4 * base;
+#pragma unroll
+    for (int k = 0; k < G; ++k) st4<NT>(yb + 4 * (threadIdx.x + k * kBlock), v[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int64_t i = base + threadIdx.x + k * kBlock;
+      if (i < ng) store_group<VEC, NT>(y, i, n, v[k]);
+    }
+  }
+  if (threadIdx.x == 0) {   // waves in order: fixed per n
+    double f[6] = {s_mn[0], s_mx[0], (double)s_nan[0], s_sa[0], s_s1[0], s_s2[0]};
+    for (int i = 1; i < kWaves; ++i) {
+      f[0] = fminf((float)f[0], s_mn[i]); f[1] = fmaxf((float)f[1], s_mx[i]); f[2] += s_nan[i];
+      f[3] += s_sa[i]; f[4] += s_s1[i]; f[5] += s_s2[i];
+    }
+    double *r = parts + (int64_t)blockIdx.x * VSIQ_PART_LEN;
+    r[0] = f[0]; r[1] = f[1]; r[2] = f[2]; r[3] = f[3];
+    r[4] = f[4]; r[5] = f[5]; r[6] = (double)n; r[7] = (double)gridDim.x;
+  }
+}
+
 // ----------------------------------------------------------------------------
 // K8: per-tensor observe + qparams + fake quant of a SMALL tensor in one launch.  One
 // 1024-lane workgroup holds the whole tensor in registers (<= 16 groups per lane,
@@ -393,6 +469,7 @@ void launch_observe_fq_small(const float *x, float *y, uint8_t *c, uint64_t *m, 
 // (min / max; a NaN call changes nothing, minmax.py:42-47), so a workgroup that reads
 // the state after workgroup 0 has written it computes the same qparams.
 // ----------------------------------------------------------------------------
+constexpr int kK2oMinGroups = 1;               // K2o one-shot: fewest groups per lane
 constexpr int kFoldFqGrid = 32;                 // K2p workgroups: <= 128 records per fold
 constexpr int kFoldFqU = 4;                     // K2p groups per lane per step
 constexpr int64_t kFoldFqMax = (int64_t)1 << 18;   // largest n (fq grid <= 128 workgroups)
@@ -1094,6 +1171,45 @@ int device_cus() {
 
 using namespace vsiq;
 
+// K2o one-shot groups per lane: the smallest G whose grid fits VSIQ_PART_MAX_RECORDS
+// workgroups (one record each); fixed per n (and the k2o_groups knob): deterministic
+inline int k2o_groups(int64_t n) {
+  const int t = g_tune.k2o_groups;
+  if (t) return t;
+  const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
+  for (int g = kK2oMinGroups; g < 16; g *= 2)
+    if (cdiv(units, g) <= VSIQ_PART_MAX_RECORDS) return g;
+  return 16;
+}
+
+inline int64_t k2o_records(int64_t n) {
+  if (g_tune.k2o_form == 1) return observe_part_grid(n) * kWaves;
+  return cdiv(cdiv(cdiv(n, 4), (int64_t)kBlock), k2o_groups(n));
+}
+
+template <bool VEC, bool NT, int ACT>
+void launch_k2o1(int g, int64_t grid, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
+                 hipStream_t st) {
+#define K2O1(G_) hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, G_>), dim3((unsigned)grid), dim3(kBlock), 0, \
+                                    st, c, y, n, parts, L)
+  switch (g) {
+    case 1: K2O1(1); break;
+    case 2: K2O1(2); break;
+    case 4: K2O1(4); break;
+    case 8: K2O1(8); break;
+    default: K2O1(16); break;
+  }
+#undef K2O1
+}
+
+template <int ACT>
+void launch_k2o1_act(bool vec, bool nt, int g, int64_t grid, const float *c, float *y, int64_t n, double *parts,
+                     const SiluLay &L, hipStream_t st) {
+  if (vec && nt) launch_k2o1<true, true, ACT>(g, grid, c, y, n, parts, L, st);
+  else if (vec) launch_k2o1<true, false, ACT>(g, grid, c, y, n, parts, L, st);
+  else launch_k2o1<false, false, ACT>(g, grid, c, y, n, parts, L, st);
+}
+
 extern "C" {
 
 int vsiq_abi_version(void) { return VSIQ_ABI_VERSION; }
@@ -1156,6 +1272,14 @@ int vsiq_set_tuning(int key, int value) {
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.xcd_order = value;
       return 0;
+    case VSIQ_TUNE_K2O_FORM:
+      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      g_tune.k2o_form = value;
+      return 0;
+    case VSIQ_TUNE_K2O_GROUPS:
+      if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16) return VSIQ_E_ARG;
+      g_tune.k2o_groups = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;
@@ -1215,16 +1339,28 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
   return launch_rc();
 }
 
+int64_t vsiq_observe_part_out_records(int64_t n) {
+  if (n <= 0) return VSIQ_E_ARG;
+  return k2o_records(n);
+}
+
 int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, double *parts, int64_t parts_len,
                                   void *stream) {
   if (n <= 0 || !c || !y || !parts || !act_ok(act)) return VSIQ_E_ARG;
-  const int64_t grid = observe_part_grid(n);
-  if (parts_len < grid * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
   const bool vec = aligned16(c) && aligned16(y) && n % 4 == 0;
   const bool nt = g_tune.nontemporal != 0;
-  const int u = observe_part_u(n);
   const SiluLay L = act_lay(act, n);
   const hipStream_t st = (hipStream_t)stream;
+  if (g_tune.k2o_form != 1) {
+    const int64_t grid = k2o_records(n);
+    if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
+    if (parts_len < grid * VSIQ_PART_LEN) return VSIQ_E_WS;
+    VSIQ_ACT(act, launch_k2o1_act, vec, nt, k2o_groups(n), grid, c, y, n, parts, L, st);
+    return launch_rc();
+  }
+  const int64_t grid = observe_part_grid(n);
+  if (parts_len < grid * kWaves * VSIQ_PART_LEN) return VSIQ_E_WS;
+  const int u = observe_part_u(n);
 #define K2O(A, U_)                                                                                              \
   if (vec && nt) hipLaunchKernelGGL((k_observe_part_out<true, true, A, U_>), dim3((unsigned)grid), dim3(kBlock), 0, \
                                     st, c, y, n, parts, L);                                                     \

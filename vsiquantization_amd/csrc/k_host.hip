@@ -335,8 +335,9 @@ int vsiq_host_ste_bwd_f32(const float *g, const uint8_t *mask, const float *pre,
 
 int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, int act, double scale, double zp,
                           int zp_learn, int qmin, int qmax, double gscale, double *grad_out) {
-  if (n <= 0 || !g || !x || !gx || !grad_out || qmin > qmax || !act_ok(act)) return VSIQ_E_ARG;
-  const HQP p = make_hqp(scale, zp, zp_learn, qmin, qmax);
+  if (n <= 0 || !g || !x || !gx || !grad_out || qmin > qmax || !act_ok(act) || zp_learn < 0 || zp_learn > 2)
+    return VSIQ_E_ARG;
+  const HQP p = make_hqp(scale, zp, zp_learn == 1, qmin, qmax);
   const int kind = act_kind(act);
   const SiluLay L = act_lay(act, n);
   const int64_t nc = cdiv(n, kChunk);
@@ -381,13 +382,95 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
     z += part[(size_t)c * 2 + 1];
   }
   grad_out[0] = t * gscale;
-  if (zp_learn) {   // ClampBackward of zero_point_rounding: the in-range test on round(zp)
+  if (zp_learn == 2) {   // zp as given, no ScaleGradient (symmetric quantizer, k_body.cuh lsq_grad_zp)
+    grad_out[1] = z;
+  } else if (zp_learn) {   // ClampBackward of zero_point_rounding: the in-range test on round(zp)
     const double zr = __builtin_rint(zp);
     grad_out[1] = (zr >= (double)qmin && zr <= (double)qmax) ? z * gscale : 0.0;
   } else {
     grad_out[1] = 0.0;
   }
   return 0;
+}
+
+// Per-channel (axis 0, rows = out-channels) host loops: PerChannelMinMaxObserver /
+// PerChannelUniformQuantizer on CPU tensors.  SURVEY §0.2 defines per channel as the
+// reference classes applied to each row W[c] (observers/minmax.py:42-74 with a running
+// state per row, quantizers/uniform.py:34-56 / 95 with the row's qparams), so every row
+// runs exactly the per-tensor host code above (the same bits as vsiq_host_observe_f32 /
+// _fq_fwd_f32 / _ste_bwd_f32 / _lsq_bwd_f32 on that row alone).  Rows go to the pool
+// (a row's own chunk loop then runs serially inside it), or, for fewer than 4 rows, one
+// after the other with the pool inside each row.
+int vsiq_host_pc_observe_fq_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
+                                float *run_min, float *run_max, double *scale_out, double *zp_out,
+                                double *row_stats, int symmetric, double qden, double eps, int qmin, int qmax) {
+  if (rows <= 0 || rowlen <= 0 || !x || !run_min || !run_max || !scale_out || !zp_out || qmin > qmax)
+    return VSIQ_E_ARG;
+  std::atomic<int> rc{0};
+  Pool::get().run(rows, [&](int64_t r) {
+    const float *xr = x + r * rowlen;
+    float st[2] = {run_min[r], run_max[r]};
+    double qp[VSIQ_QP_LEN], stats[VSIQ_ST_LEN];
+    int e = vsiq_host_observe_f32(xr, rowlen, kActNone, stats, st, qp, symmetric, qden, eps);
+    run_min[r] = st[0];
+    run_max[r] = st[1];
+    scale_out[r] = qp[VSIQ_QP_SCALE];
+    zp_out[r] = qp[VSIQ_QP_ZP];
+    if (row_stats) {
+      row_stats[3 * r] = stats[VSIQ_ST_SUMABS];
+      row_stats[3 * r + 1] = stats[VSIQ_ST_SUM];
+      row_stats[3 * r + 2] = stats[VSIQ_ST_SUMSQ];
+    }
+    if (!e && y)
+      e = vsiq_host_fq_fwd_f32(xr, y + r * rowlen, nullptr, mask ? mask + r * rowlen : nullptr, rowlen, kActNone,
+                               qp, 0.0, 0.0, 0, 0, qmin, qmax);
+    if (e) rc.store(e);
+  });
+  return rc.load();
+}
+
+int vsiq_host_pc_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
+                            const double *scale, const double *zp, int zp_round, int qmin, int qmax) {
+  if (rows < 0 || rowlen < 0 || (rows > 0 && (!x || !y || !scale)) || qmin > qmax) return VSIQ_E_ARG;
+  std::atomic<int> rc{0};
+  Pool::get().run(rows, [&](int64_t r) {
+    const int e = vsiq_host_fq_fwd_f32(x + r * rowlen, y + r * rowlen, nullptr, mask ? mask + r * rowlen : nullptr,
+                                       rowlen, kActNone, nullptr, scale[r], zp ? zp[r] : 0.0, zp_round, 0, qmin,
+                                       qmax);
+    if (e) rc.store(e);
+  });
+  return rc.load();
+}
+
+int vsiq_host_pc_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale) {
+  if (rows < 0 || rowlen < 0 || (rows > 0 && (!g || !mask || !gx || !scale))) return VSIQ_E_ARG;
+  std::atomic<int> rc{0};
+  Pool::get().run(rows, [&](int64_t r) {
+    const int64_t o = r * rowlen;
+    const int e = vsiq_host_ste_bwd_f32(g + o, mask + o, nullptr, gx + o, rowlen, kActNone, scale[r]);
+    if (e) rc.store(e);
+  });
+  return rc.load();
+}
+
+int vsiq_host_pc_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale, const double *zp, int zp_learn, int qmin, int qmax, double gscale,
+                             double *grad_scale_out, double *grad_zp_out) {
+  if (rows <= 0 || rowlen <= 0 || !g || !x || !gx || !scale || !grad_scale_out || qmin > qmax ||
+      (zp_learn && !zp) || zp_learn < 0 || zp_learn > 1)
+    return VSIQ_E_ARG;
+  std::atomic<int> rc{0};
+  Pool::get().run(rows, [&](int64_t r) {
+    const int64_t o = r * rowlen;
+    double go[2];
+    const int e = vsiq_host_lsq_bwd_f32(g + o, x + o, gx + o, rowlen, kActNone, scale[r], zp ? zp[r] : 0.0,
+                                        zp_learn, qmin, qmax, gscale, go);
+    grad_scale_out[r] = go[0];
+    if (grad_zp_out) grad_zp_out[r] = go[1];
+    if (e) rc.store(e);
+  });
+  return rc.load();
 }
 
 int vsiq_host_threads(void) { return usable_cpus(); }

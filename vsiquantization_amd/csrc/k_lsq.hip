@@ -111,10 +111,11 @@ int lsq_bwd(const float *g, const float *x, float *gx, int64_t n, int act, const
   const int64_t grid = lsq_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
-  // learnable zp: the forward used clamp(rint(zp)); a non-learnable zp is used as given
-  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
+  // learnable zp (1): the forward used clamp(rint(zp)); 0 / 2: zp as given (2: with its gradient)
+  if (zp_learn < 0 || zp_learn > 2) return VSIQ_E_ARG;
+  QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn == 1, 0};
   const bool nt = g_tune.nontemporal != 0;
-  VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, gscale, grad_out, ws, counter, grid,
+  VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn != 0, gscale, grad_out, ws, counter, grid,
            act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
@@ -129,6 +130,7 @@ int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, 
   const int64_t grid = lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane());
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (records_len < 2 * grid) return VSIQ_E_WS;
+  if (zp_learn < 0 || zp_learn > 1) return VSIQ_E_ARG;   // the deferred fold knows modes 0 / 1 only
   QPSrc src{nullptr, scale_dev, zp_dev, scale_host, zp_host, (float)qmin, (float)qmax, zp_learn, 0};
   const bool nt = g_tune.nontemporal != 0;
   VSIQ_ACT(act, launch_lsq, vec, nt, g, x, gx, n, src, zp_learn, 0.0, nullptr, records, nullptr, grid,

@@ -219,7 +219,7 @@ def fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=Non
     with VSIQ_TORCH_EXT=0).  CPU tensors: the native host path (host.py)."""
     if _host.is_host(x):
         return _host.fake_quant_learn(x, scale, zero_point, qmin, qmax, gscale, learn_zp, act)
-    if H.torch_ext_enabled():   # the C++ node takes its K4 workspace from its own cache
+    if H.torch_ext_enabled() and learn_zp != 2:   # the C++ node takes its K4 workspace from its own cache
         x = H.require_device_f32(x)
         st, sh = _qarg(scale)
         zt, zh = _qarg(zero_point)
@@ -240,7 +240,7 @@ def lsq_backward(g, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None
     zd, zh = scalar_source(zero_point, dev)
     w = H.workspace(dev, g.numel())
     rc = H.lib().vsiq_act_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(g.numel()), H.act_code(act),
-                                      H.ptr(sd), sh, H.ptr(zd), zh, int(bool(learn_zp)), int(qmin),
+                                      H.ptr(sd), sh, H.ptr(zd), zh, int(learn_zp), int(qmin),
                                       int(qmax), float(gscale), H.ptr(grads), H.ptr(w.ws),
                                       _i64(w.ws_len), H.ptr(w.counter), H.stream_of(dev))
     H.check(rc, "vsiq_act_lsq_bwd_f32")
@@ -256,7 +256,7 @@ class FakeQuantLearnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
         x = H.require_device_f32(x)
-        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, act=act)
+        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp == 1, act=act)
         ctx.save_for_backward(x)
         ctx.scale, ctx.zp = scale, zero_point
         ctx.args = (qmin, qmax, gscale, learn_zp, act)
@@ -518,6 +518,14 @@ def part_slot_doubles(n: int | None = None) -> int:
     return r * H.PART_LEN
 
 
+def part_out_slot_doubles(n: int) -> int:
+    """Doubles of one K2o slot for n elements (vsiq_observe_part_out_records(n) x
+    VSIQ_PART_LEN; one record per workgroup of the one-shot pass)."""
+    r = int(H.lib().vsiq_observe_part_out_records(_i64(n)))
+    H.check(r if r < 0 else 0, "vsiq_observe_part_out_records")
+    return r * H.PART_LEN
+
+
 def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) -> torch.Tensor:
     """Deferred observer pass (K2p): the per-wave partial records of act(x) into
     ``out`` (f64, >= part_slot_doubles(numel) entries; allocated when None), no fold,
@@ -539,11 +547,12 @@ def observe_parts(x: torch.Tensor, out: torch.Tensor | None = None, act=None) ->
 def observe_parts_out(x: torch.Tensor, act, out: torch.Tensor | None = None):
     """K2o: y = act(x) and the deferred observer records of act(x) (observe_parts) in ONE
     pass -- a fused layer's calibration forward (modules/fused.py:133 + minmax.py:42-43).
-    Returns (y, out)."""
+    ``out`` holds >= part_out_slot_doubles(numel) doubles (records in observe_parts'
+    format, one per workgroup; fold with ``fold_parts``).  Returns (y, out)."""
     x = H.require_device_f32(x)
     if x.numel() == 0:
         raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
-    need = part_slot_doubles(x.numel())
+    need = part_out_slot_doubles(x.numel())
     if out is None:
         out = torch.empty(need, dtype=torch.float64, device=x.device)
     elif out.dtype != torch.float64 or out.device != x.device or not out.is_contiguous() or out.numel() < need:

@@ -6,8 +6,9 @@ kernels' bit for bit (IEEE fp32 division, rint, NaN-propagating clamp, f64 qpara
 torch CPU's SiLU).  The f64 sums (mean|x|, mean, std, scale / zero-point gradients) are
 summed in 16 lanes per 64K chunk, folded in lane then chunk order -- the same bits with
 or without AVX-512 (VSIQ_HOST_SIMD=0) and for any thread count, but a different order
-from the GPU's tree (equal to it within the f64 rounding of the sum).  This is not a fallback for CUDA tensors: a CUDA tensor never comes
-here, and a missing library raises like every other op.
+from the GPU's tree (equal to it within the f64 rounding of the sum).  This is not a
+fallback for CUDA tensors: a CUDA tensor never comes here, and a missing library raises
+like every other op.
 """
 from __future__ import annotations
 
@@ -92,10 +93,10 @@ class LearnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, act=None):
         x = _f32(x)
-        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, act=act)
+        y, _, _ = fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp == 1, act=act)
         ctx.save_for_backward(x)
         ctx.scale, ctx.zp = scale, zero_point
-        ctx.args = (int(qmin), int(qmax), float(gscale), bool(learn_zp), H.act_code(act))
+        ctx.args = (int(qmin), int(qmax), float(gscale), int(learn_zp), H.act_code(act))
         return y
 
     @staticmethod
@@ -145,6 +146,146 @@ def observe_tensor(x, *, symmetric, num_bits=8, eps=1e-8, run_minmax=None, want_
     return qp, st
 
 
+# --------------------------------------------------------------------------- per-channel (axis 0)
+def _rows(x):
+    C = x.shape[0] if x.dim() > 0 else 1
+    if C == 0 or x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    return C, x.numel() // C
+
+
+def _row_f64(v, C, what):
+    t = (v.detach() if isinstance(v, torch.Tensor) else torch.tensor(float(v))).to("cpu", torch.float64)
+    t = t.reshape(-1)
+    if t.numel() == 1 and C > 1:
+        t = t.expand(C)
+    if t.numel() != C:
+        raise RuntimeError(f"per-channel {what} has {t.numel()} entries, the tensor has {C} channels")
+    return t.contiguous()
+
+
+def pc_observe_fq(x, *, symmetric, qmin, qmax, obs_bits=8, eps=1e-8, run_min=None, run_max=None,
+                  quantize=True, want_mask=False, want_row_stats=False):
+    """Host counterpart of fakequant.per_channel_observe_fq (K3): each out-channel row W[c]
+    observed (running state per row) and fake-quantized with its own f64 qparams, the
+    per-tensor host code on each row.  Same dict as the device function."""
+    from .fakequant import qden
+    x = _f32(x)
+    C, rowlen = _rows(x)
+    if run_min is None or run_max is None:
+        state = torch.zeros(2, C, dtype=torch.float32)
+        run_min = state[0] if run_min is None else run_min
+        run_max = state[1] if run_max is None else run_max
+    for r in (run_min, run_max):
+        if r.numel() != C or r.device.type != "cpu" or r.dtype != torch.float32 or not r.is_contiguous():
+            raise ValueError(f"host per-channel observe: running state must be contiguous CPU float32 [{C}]")
+    y = torch.empty_like(x) if quantize else None
+    mask = torch.empty(x.shape, dtype=torch.uint8) if (want_mask and quantize) else None
+    scale = torch.empty(C, dtype=torch.float64)
+    zp = torch.empty(C, dtype=torch.float64)
+    rstats = torch.empty(C, 3, dtype=torch.float64) if want_row_stats else None
+    rc = H.lib().vsiq_host_pc_observe_fq_f32(H.ptr(x), H.ptr(y), H.ptr(mask), _i64(C), _i64(rowlen), H.ptr(run_min),
+                                             H.ptr(run_max), H.ptr(scale), H.ptr(zp), H.ptr(rstats),
+                                             int(bool(symmetric)), qden(symmetric, obs_bits, eps), float(eps),
+                                             int(qmin), int(qmax))
+    H.check(rc, "vsiq_host_pc_observe_fq_f32")
+    return dict(y=y, scale=scale, zp=zp, run_min=run_min, run_max=run_max, mask=mask, codes=None,
+                row_stats=rstats)
+
+
+def pc_fake_quant(x, scale, zp, qmin, qmax, *, zp_round=False, want_mask=False):
+    """Per-channel (axis 0) fake quant with given [C] qparams on the host: (y, mask | None)."""
+    x = _f32(x)
+    C, rowlen = _rows(x)
+    s = _row_f64(scale, C, "scale")
+    z = _row_f64(zp, C, "zero point") if zp is not None else None
+    y = torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.uint8) if want_mask else None
+    rc = H.lib().vsiq_host_pc_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(mask), _i64(C), _i64(rowlen), H.ptr(s), H.ptr(z),
+                                         int(bool(zp_round)), int(qmin), int(qmax))
+    H.check(rc, "vsiq_host_pc_fq_fwd_f32")
+    return y, mask
+
+
+def pc_ste_backward(g, mask, scale):
+    g = _f32(g, "grad_output")
+    C, rowlen = _rows(g)
+    s = _row_f64(scale, C, "scale")
+    gx = torch.empty_like(g)
+    rc = H.lib().vsiq_host_pc_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(gx), _i64(C), _i64(rowlen), H.ptr(s))
+    H.check(rc, "vsiq_host_pc_ste_bwd_f32")
+    return gx
+
+
+class PcFixedFn(torch.autograd.Function):
+    """Per-channel fake quant with given [C] qparams and the STE backward, on the host."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zp, qmin, qmax):
+        y, mask = pc_fake_quant(x, scale, zp, qmin, qmax, want_mask=True)
+        ctx.save_for_backward(mask, _row_f64(scale, mask.shape[0], "scale"))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        mask, s = ctx.saved_tensors
+        return pc_ste_backward(gy, mask, s), None, None, None, None
+
+
+class PcObserveFQFn(torch.autograd.Function):
+    """Per-channel observe + fake quant with the STE backward, on the host."""
+
+    @staticmethod
+    def forward(ctx, x, symmetric, qmin, qmax, obs_bits, eps, run_min, run_max, want_row_stats):
+        r = pc_observe_fq(x, symmetric=symmetric, qmin=qmin, qmax=qmax, obs_bits=obs_bits, eps=eps,
+                          run_min=run_min, run_max=run_max, want_mask=True, want_row_stats=want_row_stats)
+        ctx.save_for_backward(r["mask"], r["scale"])
+        rs = r["row_stats"] if want_row_stats else r["scale"].new_zeros(0)
+        ctx.mark_non_differentiable(r["scale"], r["zp"], rs)
+        return r["y"], r["scale"], r["zp"], rs
+
+    @staticmethod
+    def backward(ctx, gy, _gs, _gz, _gr):
+        mask, scale = ctx.saved_tensors
+        return pc_ste_backward(gy, mask, scale), None, None, None, None, None, None, None, None
+
+
+class PcLearnFn(torch.autograd.Function):
+    """Learnable per-channel (axis 0) fake quant on the host: each row the per-tensor
+    learnable host path with its own scale / zero point; [C] gradients times gscale."""
+
+    @staticmethod
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+        x = _f32(x)
+        y, _ = pc_fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp)
+        ctx.save_for_backward(x)
+        ctx.scale, ctx.zp = scale, zero_point
+        ctx.args = (int(qmin), int(qmax), float(gscale), int(bool(learn_zp)))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        qmin, qmax, gscale, learn_zp = ctx.args
+        s, z = ctx.scale, ctx.zp
+        g = _f32(gy, "grad_output")
+        C, rowlen = _rows(x)
+        sr = _row_f64(s, C, "scale")
+        zr = _row_f64(z, C, "zero point") if z is not None else None
+        gx = torch.empty_like(g)
+        gs = torch.empty(C, dtype=torch.float64)
+        gz = torch.empty(C, dtype=torch.float64)
+        rc = H.lib().vsiq_host_pc_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(C), _i64(rowlen), H.ptr(sr),
+                                              H.ptr(zr), learn_zp, qmin, qmax, gscale, H.ptr(gs), H.ptr(gz))
+        H.check(rc, "vsiq_host_pc_lsq_bwd_f32")
+        out_s = out_z = None
+        if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
+            out_s = gs.to(device=s.device, dtype=s.dtype).reshape(s.shape)
+        if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
+            out_z = gz.to(device=z.device, dtype=z.dtype).reshape(z.shape)
+        return gx, out_s, out_z, None, None, None, None
+
+
 def threads() -> int:
     """Host threads the CPU path uses (VSIQ_HOST_THREADS, else the CPUs this process may use)."""
     return int(H.lib().vsiq_host_threads())
@@ -155,4 +296,5 @@ def simd() -> bool:
     return bool(H.lib().vsiq_host_simd())
 
 
-__all__ = ["is_host", "fake_quant", "fake_quant_fixed", "fake_quant_learn", "observe_tensor", "threads", "simd"]
+__all__ = ["is_host", "fake_quant", "fake_quant_fixed", "fake_quant_learn", "observe_tensor", "pc_observe_fq",
+           "pc_fake_quant", "threads", "simd"]

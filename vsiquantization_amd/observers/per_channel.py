@@ -8,13 +8,16 @@ out-channel slice W[c] (axis 0 of OIHW / [out, in] weights):
 
 with one running (min_val, max_val) per channel (fresh observers start at 0/0,
 minmax.py:28-29).  All of it is one launch of the K3 kernel; scale and zero
-point come back as float64 [C] device tensors (no host sync).
+point come back as float64 [C] device tensors (no host sync).  CPU tensors (the
+reference's classes run on them, observers/minmax.py:42-43) take the native host
+loops, row by row (host.pc_observe_fq): the same bits as K3.
 """
 from __future__ import annotations
 
 import torch
 
 from .. import _hip as H
+from .. import host as _host
 from ..fakequant import PerChannelObserveFQFn, per_channel_observe_fq, qden
 from ..utils.registry import register_class
 from .base import BaseObserver
@@ -54,11 +57,11 @@ class PerChannelMinMaxObserver(BaseObserver):
 
     # ------------------------------------------------------------------ protocol
     def observe(self, x, want_row_stats=False):
-        x = H.require_device_f32(x)
+        x = x if _host.is_host(x) else H.require_device_f32(x)
         mn, mx = self._state(x)
-        r = per_channel_observe_fq(x, symmetric=self.symmetric, qmin=0, qmax=0, obs_bits=self.num_bits,
-                                   eps=self.eps, run_min=mn, run_max=mx, quantize=False,
-                                   want_row_stats=want_row_stats)
+        fn = _host.pc_observe_fq if _host.is_host(x) else per_channel_observe_fq
+        r = fn(x, symmetric=self.symmetric, qmin=0, qmax=0, obs_bits=self.num_bits, eps=self.eps,
+               run_min=mn, run_max=mx, quantize=False, want_row_stats=want_row_stats)
         self.scale, self.zero_point = r["scale"], r["zp"]
         return r["row_stats"]
 
@@ -76,6 +79,18 @@ class PerChannelMinMaxObserver(BaseObserver):
         """Fused observe + fake quant of ``x`` with ``quantizer``'s integer range (one pass).
 
         Returns (y, row_stats | None); y carries the STE gradient."""
+        if _host.is_host(x):
+            mn, mx = self._state(x)
+            args = (self.symmetric, quantizer.qmin, quantizer.qmax, self.num_bits, self.eps, mn, mx)
+            if x.requires_grad and torch.is_grad_enabled():
+                y, s, z, rs = _host.PcObserveFQFn.apply(x, *args, want_row_stats)
+                rs = rs if want_row_stats else None
+            else:
+                r = _host.pc_observe_fq(x, symmetric=args[0], qmin=args[1], qmax=args[2], obs_bits=args[3],
+                                        eps=args[4], run_min=mn, run_max=mx, want_row_stats=want_row_stats)
+                y, s, z, rs = r["y"], r["scale"], r["zp"], r["row_stats"]
+            self.scale, self.zero_point = s, z
+            return y, rs
         x = H.require_device_f32(x)
         mn, mx = self._state(x)
         if x.requires_grad and torch.is_grad_enabled():

@@ -268,7 +268,7 @@ class QuantizationManager(nn.Module):
                 from .deferred import deferred_learn
                 q = self.quantizer
                 gscale, zp, learn_zp = q.learn_args(x, d[1])
-                if not isinstance(gscale, torch.Tensor):
+                if not isinstance(gscale, torch.Tensor) and learn_zp != 2:
                     return deferred_learn(x, d[0], zp, q.qmin, q.qmax, gscale, learn_zp, act)
             if act is None:
                 return self.quantizer.quantize(x, self.scale, self.zero_point, True)
@@ -306,13 +306,13 @@ class QuantizationManager(nn.Module):
         y = act(x), which the next layer consumes, and this call's K2p records of act(x) in
         ONE pass (K2o, fakequant.observe_parts_out).  Nothing is queued, so user code may
         modify y in place (ReLU(inplace=True), a residual +=) before calibration ends."""
-        from ..fakequant import observe_parts_out
+        from ..fakequant import observe_parts_out, part_out_slot_doubles
         self._join()
         self._x_device = x.device
         obs = self.observer
         if not self._pending_records:
             self._calib_init = (obs.min_val, obs.max_val)
-        slot = torch.empty(part_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
+        slot = torch.empty(part_out_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
         y, _ = observe_parts_out(x, act, out=slot)
         self._pending_records.append(slot)
         return y

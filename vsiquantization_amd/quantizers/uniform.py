@@ -98,8 +98,10 @@ class UniformQuantizer(BaseQuantizer):
             zero_point = self._int_zero_point_learnable(zero_point)
             learn_zp = isinstance(zero_point, torch.Tensor)
         if not learn_zp and isinstance(zero_point, torch.Tensor) and zero_point.requires_grad:
-            raise NotImplementedError("a gradient-requiring zero point with a symmetric learnable "
-                                      "quantizer is not supported")
+            # symmetric: the reference skips zero_point_rounding / ScaleGradient on zp
+            # (uniform.py:50) but autograd still reaches it through x/s + zp and
+            # (x_int - zp) * s: zp as given, grad = sum g*s*(mask - 1) (zp_learn 2)
+            learn_zp = 2
         return gscale, zero_point, learn_zp
 
     def _int_zero_point_learnable(self, zero_point):
