@@ -24,7 +24,9 @@ def _bn(c, seed):
     return bn
 
 
-def model():
+def model(launches=False):
+    """launches: the model-level launches (K7 + K4d) that activate_learning_qparam /
+    activate_quantizer install by default; False: the per-call path."""
     # MIOpen's default weight-gradient kernels may accumulate with atomics: deterministic
     # algorithms, so the ranks' conv gradients do not differ from run to run
     torch.backends.cudnn.deterministic = True
@@ -38,8 +40,8 @@ def model():
     g = torch.Generator().manual_seed(5)
     loader = [(torch.randint(0, 256, (2, 3, 16, 16), generator=g, dtype=torch.uint8), None) for _ in range(3)]
     calibrate_qat_model(m, loader, data_calib, DEV)
-    activate_learning_qparam(m)
-    activate_quantizer(m)
+    activate_learning_qparam(m, model_launches=launches)
+    activate_quantizer(m, model_launches=launches)
     m.train()
     return m
 

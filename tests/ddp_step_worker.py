@@ -20,8 +20,9 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
-    m = model()
-    if os.environ.get("VSIQ_TEST_DEFERRED") == "1":   # deferred qparam-gradient fold under DDP
+    mode = os.environ.get("VSIQ_TEST_DEFERRED")
+    m = model(launches=mode == "default")   # default: the reference flow's K7 + K4d
+    if mode == "1":   # deferred qparam-gradient fold under DDP
         from vsiquantization_amd import enable_deferred_qparam_grads
         enable_deferred_qparam_grads(m)
     ddp = DDP(m, device_ids=[0])

@@ -29,15 +29,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("deferred", [False, True])
+@pytest.mark.parametrize("deferred", [False, True, "default"])
 def test_ddp_learnable_step_two_ranks(tmp_path, deferred):
     """deferred: the ranks run enable_deferred_qparam_grads (records-only K4 + one fold at the
-    end of the backward, quantizers/deferred.py): DDP's hooks see the folded gradients."""
+    end of the backward, quantizers/deferred.py): DDP's hooks see the folded gradients.
+    "default": the model-level launches activate_learning_qparam / activate_quantizer
+    install by themselves (K7 weights + K4d), the reference's own sequence."""
     out = tmp_path / "grads.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "ddp_step_worker.py"), str(out)]
-    env = dict(os.environ, VSIQ_TEST_DEFERRED="1" if deferred else "0")
+    env = dict(os.environ, VSIQ_TEST_DEFERRED=deferred if isinstance(deferred, str) else ("1" if deferred else "0"))
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = json.loads(out.read_text())

@@ -78,8 +78,8 @@ def _model(act_learn_zp=False):
     gen = torch.Generator().manual_seed(1)
     loader = [(torch.randint(0, 256, (4, 3, 32, 32), generator=gen, dtype=torch.uint8), None) for _ in range(2)]
     calibrate_qat_model(model, loader, data_calib, DEV)
-    activate_learning_qparam(model)
-    activate_quantizer(model)
+    activate_learning_qparam(model, model_launches=False)   # the per-call path; hooks enabled per test
+    activate_quantizer(model, model_launches=False)
     model.eval()
     return model
 

@@ -124,8 +124,8 @@ def _model():
     for layer in m:   # learnable scales without a calibration pass
         for qm in (layer.weight_quantizer, layer.activation_quantizer):
             qm.mean_abs_x = [0.05]
-    activate_learning_qparam(m, use_init=True)
-    activate_quantizer(m)
+    activate_learning_qparam(m, use_init=True, model_launches=False)   # per layer; K7 enabled per test
+    activate_quantizer(m, model_launches=False)
     return m.to(DEV)   # the new f64 scale Parameters (reference flow: yolov8_qat.py moves the model)
 
 

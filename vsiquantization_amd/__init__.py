@@ -10,7 +10,7 @@ Importing the package registers the quantizer/observer classes by name in
 
 plus ``LSQFakeQuantize`` (quantizers/lsq_module.py, the torch.ao-based LSQ module).
 All fake-quant arithmetic runs in the HIP kernels of ``csrc/`` through the C ABI of
-``include/vsiq.h``; CPU float32 tensors of the per-tensor classes run the same
+``include/vsiq.h``; CPU float32 tensors run the same
 library's native host loops (``host.py``, ``vsiq_host_*``), never the test oracle.
 """
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
@@ -29,5 +29,7 @@ from .quantizers.fake_quantize import FakeQuantize  # noqa: F401
 from .quantizers.lsq_module import LSQFakeQuantize  # noqa: F401
 from .quantizers.foreach import enable_multi_tensor_weights, quantize_weights_multi  # noqa: F401
 from .quantizers.deferred import bundle_qparams, enable_deferred_qparam_grads  # noqa: F401
+from .utils.quantize_manager import (disable_model_launches, enable_model_launches,  # noqa: F401
+                                     model_launches_enabled)
 
 __version__ = "0.1.0"

@@ -26,12 +26,11 @@ with a 0-dim float64 CUDA scale (and zero point, when learned) and a scalar grad
 """
 from __future__ import annotations
 
-import weakref
-
 import torch
 
 from .. import _hip as H
 from ..fakequant import fake_quant, scalar_source
+from .foreach import ModelHook, NoHandle
 from .per_channel import PerChannelUniformQuantizer
 from .quantization_manager import QuantizationManager
 from .uniform import UniformQuantizer
@@ -232,26 +231,35 @@ class _Handles:
             h.remove()
 
 
+class BundlePreHook(ModelHook):
+    """Forward pre-hook: bundle the learnable qparams of the model's managers."""
+
+    def collect(self, mod):
+        return _managers(mod)
+
+    def __call__(self, mod, args):
+        bundle_qparams(self.items(mod))
+
+
+class BundlePostHook(ModelHook):
+    """Forward hook: drop the bundled qparams the forward did not use."""
+
+    def collect(self, mod):
+        return _managers(mod)
+
+    def __call__(self, mod, args, out):
+        clear_bundled(self.items(mod))
+
+
 def enable_deferred_qparam_grads(model):
     """Forward hooks on ``model``: before every forward, bundle the learnable qparams of
     its QuantizationManagers (see the module docstring); after it, drop the unused ones.
-    Returns a handle whose ``remove()`` removes both hooks.  The manager list is taken now
-    (two module-tree walks per forward cost ~0.2 ms of host time per step); a manager
-    added later takes the per-call path, which gives the same gradients, so enable again
-    after changing the model's structure only to defer it too.  The list is kept per
-    hooked module (weakly), so a deep copy of the model bundles its own managers."""
-    lists = weakref.WeakKeyDictionary()
-    lists[model] = _managers(model)
-
-    def managers(mod):
-        ms = lists.get(mod)
-        if ms is None:
-            ms = lists[mod] = _managers(mod)
-        return ms
-
-    def pre(mod, args):
-        bundle_qparams(managers(mod))
-
-    def post(mod, args, out):
-        clear_bundled(managers(mod))
-    return _Handles(model.register_forward_pre_hook(pre), model.register_forward_hook(post))
+    Returns a handle whose ``remove()`` removes both hooks.  The manager list is taken now;
+    a manager added later takes the per-call path, which gives the same gradients, so
+    enable again after changing the model's structure only to defer it too.  A deep copy
+    of the model bundles its own managers.  Already enabled: nothing is added (the
+    returned handle removes nothing)."""
+    if any(isinstance(h, BundlePreHook) for h in model._forward_pre_hooks.values()):
+        return NoHandle()
+    return _Handles(model.register_forward_pre_hook(BundlePreHook(model)),
+                    model.register_forward_hook(BundlePostHook(model)))

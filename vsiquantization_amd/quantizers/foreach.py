@@ -34,9 +34,10 @@ from .uniform import UniformQuantizer
 
 def _weight_spec(layer):
     """(weight, LsqSpec) when the layer's weight fake quant can join a multi-tensor
-    launch, else None."""
+    launch, else None (quantizer off -- is_quantize False returns the weight unquantized,
+    qm.py:86-90 -- or not learnable / per-tensor / on the GPU)."""
     qm = getattr(layer, "weight_quantizer", None)
-    if not isinstance(qm, QuantizationManager) or not qm.is_learning_scale:
+    if not isinstance(qm, QuantizationManager) or not qm.is_learning_scale or not qm.is_quantize:
         return None
     q = qm.quantizer
     if not isinstance(q, UniformQuantizer) or isinstance(q, PerChannelUniformQuantizer):
@@ -69,19 +70,64 @@ def quantize_weights_multi(layers) -> int:
     return len(picked)
 
 
+class NoHandle:
+    """Returned by an enable_* call on a model that already has that hook."""
+
+    def remove(self):
+        pass
+
+
+class ModelHook:
+    """Base of the model-level launch hooks (K7 here, K4d in deferred.py): a callable
+    object rather than a closure, so a model carrying it still pickles (whole-model
+    torch.save) and a deep copy (EMA / teacher) gets a fresh hook with its own cache.
+    ``vsiq_model_launch`` marks it for utils.quantize_manager.disable_model_launches.
+    Module lists are cached per hooked module (weakly): walking the module tree on every
+    forward cost ~0.1 ms of host time per step."""
+
+    vsiq_model_launch = True
+
+    def __init__(self, model=None):
+        self._cache = weakref.WeakKeyDictionary()
+        if model is not None:
+            self._cache[model] = self.collect(model)
+
+    def collect(self, mod):
+        raise NotImplementedError
+
+    def items(self, mod):
+        ms = self._cache.get(mod)
+        if ms is None:
+            ms = self._cache[mod] = self.collect(mod)
+        return ms
+
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self._cache = weakref.WeakKeyDictionary()
+
+    def __deepcopy__(self, memo):
+        return type(self)()
+
+
+class MultiWeightsHook(ModelHook):
+    """Forward pre-hook: quantize_weights_multi over the model's FakeQuantize layers."""
+
+    def collect(self, mod):
+        return [m for m in mod.modules() if isinstance(m, FakeQuantize)]
+
+    def __call__(self, mod, args):
+        quantize_weights_multi(self.items(mod))
+
+
 def enable_multi_tensor_weights(model):
     """Register a forward pre-hook on ``model`` that runs quantize_weights_multi over its
     FakeQuantize layers before every forward.  Returns the hook handle.  The layer list is
-    taken now (walking the module tree on every forward cost ~0.1 ms of host time per
-    step); a layer added later quantizes its weight per call, which gives the same values,
-    so enable again after changing the model's structure only to batch it too.  The list
-    is kept per hooked module (weakly), so a deep copy of the model batches its own layers."""
-    lists = weakref.WeakKeyDictionary()
-    lists[model] = [m for m in model.modules() if isinstance(m, FakeQuantize)]
-
-    def hook(mod, args):
-        layers = lists.get(mod)
-        if layers is None:
-            layers = lists[mod] = [m for m in mod.modules() if isinstance(m, FakeQuantize)]
-        quantize_weights_multi(layers)
-    return model.register_forward_pre_hook(hook)
+    taken now; a layer added later quantizes its weight per call, which gives the same
+    values, so enable again after changing the model's structure only to batch it too.  A
+    deep copy of the model batches its own layers.  Already enabled: nothing is added
+    (the returned handle removes nothing)."""
+    if any(isinstance(h, MultiWeightsHook) for h in model._forward_pre_hooks.values()):
+        return NoHandle()
+    return model.register_forward_pre_hook(MultiWeightsHook(model))

@@ -7,7 +7,18 @@ flags select the kernel branch:
   calibrate_qat_model       observe only        (K2 / K3 observe, no fake quant)
   activate_learning_qparam  learn-init + Parameters  (K1 fwd + K4 bwd from then on)
   activate_quantizer        fake quant on
+
+Entering training (activate_learning_qparam / activate_quantizer, the reference's
+sequence before its training loop, yolov8_qat.py:90-92) also turns on the model-level
+launches, with no call in user code: every learnable weight quantizer of the model in
+ONE forward and ONE backward launch (K7, quantizers/foreach.py) and every learnable
+quantizer's scale / zero-point gradient folded in ONE launch per backward (K4d,
+quantizers/deferred.py).  Outputs and input gradients are bit-identical to the per-call
+path, qparam gradients equal to float64 summation order.  Opt out per call
+(``model_launches=False``), per process (VSIQ_MODEL_LAUNCHES=0) or per model
+(``disable_model_launches``).
 """
+import os
 
 
 def _managers(module):
@@ -64,8 +75,43 @@ def calibrate_qat_model(model, dataloader, data_calib, device=None, async_observ
         sync_calibration(model)
 
 
-def activate_learning_qparam(model, layer_names=None, use_init=True, active=True):
-    """Set ``is_learning_scale``; optionally re-init scale from mean|x|; make Parameters."""
+def enable_model_launches(model):
+    """Install the model-level launches on ``model`` (forward hooks; idempotent): K7 for
+    the learnable weight quantizers and K4d for the learnable qparam gradients.  Which
+    managers join is decided per forward (learnable, quantizing, per-tensor, on the GPU);
+    every other manager keeps its per-call path."""
+    from ..quantizers.deferred import enable_deferred_qparam_grads
+    from ..quantizers.foreach import enable_multi_tensor_weights
+    enable_multi_tensor_weights(model)
+    enable_deferred_qparam_grads(model)
+
+
+def disable_model_launches(model):
+    """Remove the model-level launch hooks (K7 / K4d) from ``model``: every manager takes
+    its per-call path again (same outputs; qparam gradients to float64 summation order)."""
+    from ..quantizers.deferred import _managers as _all_managers
+    from ..quantizers.deferred import clear_bundled
+    for hooks in (model._forward_pre_hooks, model._forward_hooks):
+        for k in [k for k, h in hooks.items() if getattr(h, "vsiq_model_launch", False)]:
+            del hooks[k]
+    clear_bundled(_all_managers(model))
+
+
+def model_launches_enabled(model) -> bool:
+    return any(getattr(h, "vsiq_model_launch", False) for h in model._forward_pre_hooks.values())
+
+
+def _auto_model_launches(model, model_launches):
+    if model_launches is None:
+        model_launches = os.environ.get("VSIQ_MODEL_LAUNCHES", "1") != "0"
+    if model_launches:
+        enable_model_launches(model)
+
+
+def activate_learning_qparam(model, layer_names=None, use_init=True, active=True, model_launches=None):
+    """Set ``is_learning_scale``; optionally re-init scale from mean|x|; make Parameters.
+    Activating also installs the model-level launches (module docstring; ``model_launches``
+    False or VSIQ_MODEL_LAUNCHES=0: not)."""
     for name, module in model.named_modules():
         if layer_names is not None and name not in layer_names:
             continue
@@ -75,18 +121,24 @@ def activate_learning_qparam(model, layer_names=None, use_init=True, active=True
                 qm.init_scaling_factor_for_learning()
             if active:
                 qm.make_learn_qparameter()
+    if active:
+        _auto_model_launches(model, model_launches)
 
 
 def deactivate_learning_qparam(model, layer_names=None):
     activate_learning_qparam(model, layer_names=layer_names, active=False)
 
 
-def activate_quantizer(model, layer_names=None, active=True):
+def activate_quantizer(model, layer_names=None, active=True, model_launches=None):
+    """Set ``is_quantize``; activating also installs the model-level launches (see
+    activate_learning_qparam)."""
     for name, module in model.named_modules():
         if layer_names is not None and name not in layer_names:
             continue
         for qm in _managers(module):
             qm.is_quantize = active
+    if active:
+        _auto_model_launches(model, model_launches)
 
 
 def deactivate_quantizer(model, layer_names=None):
