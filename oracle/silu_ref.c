@@ -11,7 +11,9 @@
  *                                         sig = 1 / (1 + exp(-x))
  *
  * Third-party algorithms restated here (absent from /root/reference, pinned by the
- * torch build the reference runs on):
+ * torch build the reference runs on; licenses and attributions in NOTICE -- SLEEF is
+ * Boost-1.0, Copyright Naoki Shibata and contributors; glibc is LGPL-2.1-or-later,
+ * Copyright Free Software Foundation, Inc.):
  *   - SLEEF 3.x xexpf (sleefsimdsp.c), the FMA build torch links for AVX2 / AVX-512;
  *   - glibc >= 2.27 expf (sysdeps/ieee754/flt-32/e_expf.c + e_exp2f_data.c), the FMA
  *     ifunc variant x86-64 selects on FMA-capable CPUs.

@@ -407,7 +407,8 @@ __host__ __device__ inline uint32_t silu_scalar4(int64_t e0, const SiluLay &L) {
 __host__ __device__ __forceinline__ float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 __host__ __device__ __forceinline__ uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 
-// Sleef_expf16_u10 (sleefsimdsp.c xexpf, FMA build), op for op
+// Sleef_expf16_u10 (sleefsimdsp.c xexpf, FMA build), op for op.  A restatement of SLEEF
+// (Boost Software License 1.0, Copyright Naoki Shibata and contributors); see NOTICE.
 __host__ __device__ __forceinline__ float sleef_expf_u10(float d) {
   const float qf = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
   const int q = (int)__builtin_fminf(__builtin_fmaxf(qf, -256.0f), 256.0f);   // |d| > 104: replaced below
@@ -427,7 +428,9 @@ __host__ __device__ __forceinline__ float sleef_expf_u10(float d) {
   return d != d ? d : u;
 }
 
-// 2^(i/32) - (i << 47) as doubles' bits (glibc's __exp2f_data.tab)
+// 2^(i/32) - (i << 47) as doubles' bits (glibc's __exp2f_data.tab).  This table and
+// glibc_expf below restate glibc's sysdeps/ieee754/flt-32/e_expf.c + e_exp2f_data.c
+// (LGPL-2.1-or-later, Copyright Free Software Foundation, Inc.; see NOTICE).
 #define VSIQ_EXP2F_TAB \
   0x3ff0000000000000ULL, 0x3fefd9b0d3158574ULL, 0x3fefb5586cf9890fULL, 0x3fef9301d0125b51ULL, \
   0x3fef72b83c7d517bULL, 0x3fef54873168b9aaULL, 0x3fef387a6e756238ULL, 0x3fef1e9df51fdee1ULL, \
