@@ -244,3 +244,55 @@ def test_observe_parts_out_every_group_count(groups):
     assert torch.equal(got[0, exact], want[0, exact])
     torch.testing.assert_close(got, want, rtol=1e-12, atol=0.0, equal_nan=True)
     G.assert_bitwise_f32(npy(y), npy(torch.relu(x)), "y")
+
+
+def test_silu_layout_recorded_with_qparams_survives_checkpoint(pin):
+    """A manager records the SiLU reference layout (W, torch threads) at its first SiLU
+    call and keeps using it: a state_dict saved from a run at 16 torch threads and loaded
+    into a process at 1 thread reproduces the 16-thread bits (forward and the SiLU
+    backward), with a warning; without the record the 1-thread layout gives other bits."""
+    H.set_silu_reference()   # follow this host's torch
+    n = 16 * 40000 + 12      # 16 chunks at 16 threads, one serial run at 1: different scalar tails
+    c, g = _inputs(n, 77)
+    x, gy = cu(c), cu(g)
+
+    def manager():
+        qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", 8, True, is_learning_scale=False)
+        return qm
+
+    def learn(qm):
+        qm.is_learning_scale, qm.is_quantize = True, True
+        qm.make_learn_qparameter()
+
+    def run(qm):
+        xi = x.clone().requires_grad_(True)
+        y = qm.quantize(xi, act="silu")
+        y.backward(gy)
+        torch.cuda.synchronize()
+        return npy(y), npy(xi.grad)
+
+    torch.set_num_threads(16)
+    a = manager()
+    a.is_observer_qparam, a.is_quantize = True, False
+    a.quantize(x, act="silu")
+    a.init_scaling_factor_for_learning()
+    learn(a)
+    assert a.silu_layout == (HOST_W or 16, 16)
+    y16, gx16 = run(a)
+    sd = a.state_dict()
+    assert tuple(sd["silu_layout"].tolist()) == a.silu_layout
+    torch.set_num_threads(1)
+    b = manager()
+    learn(b)
+    b.load_state_dict(sd)
+    assert b.silu_layout == a.silu_layout
+    with pytest.warns(RuntimeWarning, match="SiLU reference layout"):
+        yb, gxb = run(b)
+    G.assert_bitwise_f32(yb, y16, "y")
+    G.assert_bitwise_f32(gxb, gx16, "grad_x")
+    ctrl = manager()
+    learn(ctrl)
+    ctrl.load_state_dict({k: v for k, v in sd.items() if k != "silu_layout"})
+    _, gxc = run(ctrl)
+    assert ctrl.silu_layout == (HOST_W or 16, 1)
+    assert not np.array_equal(gxc.view(np.uint32), gx16.view(np.uint32))

@@ -184,3 +184,33 @@ def test_calib_grad_scale_factor_cached_per_tensor_version():
     assert _calib_factor(q) == 2.0
     q.calib_grad_scale = 0.5
     assert _calib_factor(q) == 0.5
+
+
+def test_silu_layout_state_dict_round_trip():
+    """QuantizationManager.silu_layout (the SiLU reference layout recorded with the qparams)
+    travels in the state_dict only once recorded; strict loads work both ways (a checkpoint
+    without it into a model that has none, and one with it into a fresh model)."""
+    import torch.nn as nn
+    from vsiquantization_amd import _hip as H
+    mk = lambda: nn.Sequential(V.QuantizationManager("UniformQuantizer", "MinMaxObserver", 8, True))  # noqa: E731
+    a = mk()
+    assert "0.silu_layout" not in a.state_dict()
+    assert a[0]._silu_act("silu").layout == H.silu_reference()
+    assert a[0]._silu_act("relu") == "relu" and a[0]._silu_act(None) is None
+    a[0].silu_layout = (32, 16)
+    sd = a.state_dict()
+    assert sd["0.silu_layout"].tolist() == [32, 16]
+    b = mk()
+    b.load_state_dict(sd)   # strict
+    assert b[0].silu_layout == (32, 16)
+    c = mk()
+    c.load_state_dict(mk().state_dict())
+    assert c[0].silu_layout is None
+    act = b[0]._silu_act("silu") if H.silu_reference() == (32, 16) else None
+    if act is None:
+        import warnings
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            act = b[0]._silu_act("silu")
+        assert any("SiLU reference layout" in str(x.message) for x in w)
+    assert act == "silu" and act.layout == (32, 16) and H.act_code(act) == (H.ACT_SILU | (32 << 8) | (16 << 16))

@@ -69,9 +69,27 @@ def silu_reference():
     return _SILU_W.get(torch.backends.cpu.get_cpu_capability(), 16), torch.get_num_threads()
 
 
+class SiluAct(str):
+    """act="silu" bound to one reference CPU layout (W, threads) instead of the process's
+    (silu_reference()): a QuantizationManager passes its recorded layout this way, so a
+    layer keeps the SiLU bits its qparams were observed / learned with.  Compares and
+    hashes as "silu"."""
+
+    def __new__(cls, width, threads):
+        s = super().__new__(cls, "silu")
+        s.layout = (int(width), int(threads))
+        return s
+
+    def __reduce__(self):
+        return (SiluAct, self.layout)
+
+
 def act_code(act) -> int:
     """None / "relu" / "silu" (or the VSIQ_ACT_* integer) -> the C ABI act argument
     (SiLU carries the reference CPU layout, VSIQ_ACT_SILU_REF)."""
+    if isinstance(act, SiluAct):
+        w, t = act.layout
+        return ACT_SILU | (w << 8) | (min(max(t, 0), 32767) << 16)
     if isinstance(act, int) and act in (ACT_NONE, ACT_RELU, ACT_SILU):
         code = act
     else:

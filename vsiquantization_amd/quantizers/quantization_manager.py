@@ -20,6 +20,7 @@ MI355X differences (behaviour-preserving):
 from __future__ import annotations
 
 import itertools
+import warnings
 
 import numpy as np
 import torch
@@ -109,6 +110,45 @@ class QuantizationManager(nn.Module):
         self.mean_abs_x = []
         self.mean_x = []
         self.std = []
+        # (W, threads) of the reference CPU layout of the fused SiLU (vsiq_common.cuh
+        # silu_lay) this manager's qparams were observed / learned with: recorded at the
+        # first SiLU call, used for every later one, saved in the state_dict
+        # ("<prefix>silu_layout", only once recorded)
+        self.silu_layout = None
+
+    # ------------------------------------------------------------------ SiLU layout
+    def _silu_act(self, act):
+        """act, with "silu" bound to this manager's recorded layout (H.SiluAct)."""
+        if act != "silu" or isinstance(act, H.SiluAct):
+            return act
+        cur = H.silu_reference()
+        lay = self.__dict__.get("silu_layout")
+        if lay is None:
+            self.silu_layout = lay = tuple(cur)
+        elif tuple(cur) != tuple(lay) and not self.__dict__.get("_silu_warned"):
+            self._silu_warned = True
+            warnings.warn(f"QuantizationManager: SiLU reference layout (W, threads) {tuple(lay)} recorded with "
+                          f"these qparams differs from this process's {tuple(cur)}; the recorded one is used "
+                          f"(torch's CPU F.silu bits depend on it; H.set_silu_reference pins another)",
+                          RuntimeWarning, stacklevel=3)
+        return H.SiluAct(*lay)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        lay = self.__dict__.get("silu_layout")
+        if lay is not None:
+            destination[prefix + "silu_layout"] = torch.tensor(lay, dtype=torch.int64)
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        key = prefix + "silu_layout"
+        if key in state_dict:
+            self.silu_layout = tuple(int(v) for v in state_dict[key].reshape(-1).tolist())
+            self._silu_warned = False
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+        if key in unexpected_keys:
+            unexpected_keys.remove(key)
 
     # ------------------------------------------------------------------ side stream
     def _join(self):
@@ -146,6 +186,8 @@ class QuantizationManager(nn.Module):
         (qm.py:55-71)."""
         if self.is_learning_scale or not self.is_observer_qparam:
             return
+        if act is not None:
+            act = self._silu_act(act)
         if isinstance(x, torch.Tensor):
             self._x_device = x.device   # where this layer's tensors live (_home_device)
         if act is not None and not self._act_fusable(x):
@@ -254,7 +296,10 @@ class QuantizationManager(nn.Module):
         """collect_qparameter, then fake-quantize when enabled (qm.py:73-90).
 
         ``act`` ("relu" / "silu"): the layer's activation, applied to ``x`` first; with
-        this package's kernels it is fused into the observer and the fake quant (K5)."""
+        this package's kernels it is fused into the observer and the fake quant (K5); a
+        SiLU uses the reference layout recorded with this manager's qparams (silu_layout)."""
+        if act is not None:
+            act = self._silu_act(act)
         if self.is_quantize or self.is_learning_scale:
             self._join()
         if self.is_learning_scale and self.is_quantize:
