@@ -596,25 +596,31 @@ class C4Backbone:
 
 class C5Calibration:
     """C5: calibration of the YOLOv8n backbone's 27 activation quantizers (MinMaxObserver,
-    sym) on batches of 128 images per GPU (1024 over 8 GPUs): per batch and layer one
-    deferred observer pass over the fused ReLU of the conv output (K2p-relu, 4 B/elem
-    read), each writing its partial records into its own device slot (no fold, no
-    atomics, no sync); after the last batch ONE deferred sync -- one fold launch over all
-    slots of all layers and batches, two RCCL all-reduces over the records, and the exact
-    replay of every layer's running min/max (the path of calibrate_qat_model(...,
-    defer_observers=True) / QuantizationManager.dist_defer + distributed.sync_calibration,
-    here driven through the C ABI so the Python manager's per-call host cost is not what
-    is measured).  The manager queues a batch's deferred calls (observe_batch) and
-    observes them in one multi-tensor launch (K2m, per-call records bit-identical), as
-    here: one launch per batch for the 27 layers.  min/max are bit-identical to a 1-GPU run (tests/test_dist_gloo.py).
-    Synthetic conv outputs stand in for the conv (MIOpen, out of scope)."""
+    sym) on batches of 128 images per GPU (1024 over 8 GPUs), as calibrate_qat_model runs
+    it by default (utils/quantize_manager.py:4-31 -> modules/fused.py:124-134 ->
+    quantizers/fake_quantize.py:49-50; here QuantizationManager._observe_deferred_act): per
+    batch and layer ONE K2o launch (vsiq_act_observe_part_out_f32) that reads the conv
+    output c, writes y = relu(c) -- the tensor the next layer consumes -- and stores the
+    deferred observer's partial records of relu(c) in its own device slot (8 B/elem: read
+    4 + write 4; no fold, no atomics, no sync); after the last batch ONE deferred sync --
+    one fold launch over all slots of all layers and batches, two RCCL all-reduces over the
+    records, and the exact replay of every layer's running min/max (distributed.
+    sync_calibration).  Driven through the C ABI so the Python manager's per-call host
+    cost is not what is measured.  min/max are bit-identical to a 1-GPU run
+    (tests/test_dist_gloo.py).  Synthetic conv outputs stand in for the conv (MIOpen, out
+    of scope).
+
+    `alt_kernels` times, on the same inputs, the opt-in observe-only multi-tensor pass
+    (K2m, VSIQ_OBSERVE_BATCH=1: 27 layers' records in one launch, 4 B/elem, the activation
+    not written) that round 2's C5 line measured."""
 
     key = "c5"
-    name = "C5 YOLOv8n backbone calibration: fused-ReLU MinMax observers, deferred RCCL sync"
+    name = "C5 YOLOv8n backbone calibration: per-layer fused-ReLU K2o (act out + observer records), deferred RCCL sync"
     group = 16
 
     def __init__(self, dev, slots, seed_base, batch=128, steps=16):
         from vsiquantization_amd import _hip as H
+        from vsiquantization_amd.fakequant import part_out_slot_doubles, part_slot_doubles
         self.H = H
         lib = H.lib()
         self.st = H.stream_of(dev)
@@ -622,28 +628,35 @@ class C5Calibration:
         self.shape = (batch, 3, 320, 320)
         gen = torch.Generator(device=dev).manual_seed(seed_base)
         self.acts = [torch.randn(batch, co, h, h, device=dev, generator=gen) for _, co, _, _, h in self.layers]
+        self.ys = [torch.empty_like(a) for a in self.acts]   # relu(c), what the next conv reads
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.steps = steps
         L = len(self.layers)
-        from vsiquantization_amd.fakequant import part_slot_doubles
-        self.stride = max(part_slot_doubles(a.numel()) for a in self.acts)
+        self.stride = max(part_out_slot_doubles(a.numel()) for a in self.acts)
         self.parts = torch.zeros(steps, L, self.stride, dtype=torch.float64, device=dev)
-        self.fm = lib.vsiq_act_observe_part_multi_f32
-        self.descs = []
-        for k in range(steps):
-            arr = (H.PartTensor * L)()
-            for j, a in enumerate(self.acts):
-                arr[j] = H.PartTensor(a.data_ptr(), a.numel(), self.parts[k, j].data_ptr(), self.stride)
-            self.descs.append(arr)
+        self.f_k2o = lib.vsiq_act_observe_part_out_f32
+        self.args = [[(H.ptr(a), H.ptr(y), H.c_i64(a.numel()), H.ACT_RELU, self.parts[k, j].data_ptr(),
+                       H.c_i64(self.stride), self.st) for j, (a, y) in enumerate(zip(self.acts, self.ys))]
+                     for k in range(steps)]
+        # K2m (alt_kernels): one observe-only multi-tensor launch per batch
+        self.m_stride = max(part_slot_doubles(a.numel()) for a in self.acts)
+        self.m_parts = torch.zeros(L, self.m_stride, dtype=torch.float64, device=dev)
+        arr = (H.PartTensor * L)()
+        for j, a in enumerate(self.acts):
+            arr[j] = H.PartTensor(a.data_ptr(), a.numel(), self.m_parts[j].data_ptr(), self.m_stride)
+        self.m_desc, self.f_k2m = arr, lib.vsiq_act_observe_part_multi_f32
         self.n = sum(a.numel() for a in self.acts)
         self.slots = [None]
-        self.kernels = {"observe_all_layers": 4 * self.n, "sync": 0}
+        self.kernels = {"act_observe_out_all_layers": 8 * self.n, "sync": 0}
         self.minmax = None
 
     def _observe(self, step):
-        """One calibration batch: the 27 layers' deferred observer calls, queued as
-        QuantizationManager does (observe_batch) and observed in one K2m launch."""
-        return self.fm(self.descs[step % self.steps], len(self.acts), self.H.ACT_RELU, self.st)
+        """One calibration batch: the 27 layers' K2o launches, in layer order."""
+        rc = 0
+        f = self.f_k2o
+        for args in self.args[step % self.steps]:
+            rc |= f(*args)
+        return rc
 
     def launch(self, i):
         """One (untimed, warmup) calibration batch, followed by the deferred sync over the
@@ -675,22 +688,44 @@ class C5Calibration:
         ev[2].record()
         return rc
 
+    def alt_kernels(self, reps=20):
+        """The opt-in K2m pass (observe only, 4 B/elem) over the same 27 tensors, event-
+        timed: {name: {avg_us, alg_bytes, GBps, frac}} (not part of the step)."""
+        for _ in range(3):
+            assert self.f_k2m(self.m_desc, len(self.acts), self.H.ACT_RELU, self.st) == 0
+        e0, e1 = timing_event(), timing_event()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            assert self.f_k2m(self.m_desc, len(self.acts), self.H.ACT_RELU, self.st) == 0
+        e1.record()
+        torch.cuda.synchronize()
+        dt = e0.elapsed_time(e1) * 1e-3 / reps
+        b = 4 * self.n
+        return {"observe_all_layers_k2m_opt_in": {"avg_us": dt * 1e6, "alg_bytes": b, "GBps": b / dt / 1e9,
+                                                  "frac": b / dt / 1e9 / HBM_PEAK_GBS, "in_step": False,
+                                                  "note": "VSIQ_OBSERVE_BATCH=1 path: observe only, the "
+                                                          "activation not written"}}
+
     def check(self):
         """Running min/max after the sync identical on every rank; on one GPU equal to a
-        direct reduction of relu(conv output), and mean|x| within 1e-6 of torch's."""
+        direct reduction of relu(conv output), mean|x| within 1e-6 of torch's, and the
+        written activations y == relu(c) bit for bit."""
         self._sync(1)
         mm = torch.stack(self.minmax, dim=-1)
+        y_ok = all(torch.equal(y.view(torch.int32), torch.where(a < 0, torch.zeros_like(a), a).view(torch.int32))
+                   for a, y in zip(self.acts[::9], self.ys[::9]))   # the CPU relu's bits (-0.0 kept)
         if self.world > 1:
             hi, lo = mm.clone(), mm.clone()
             dist.all_reduce(hi, op=dist.ReduceOp.MAX)
             dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-            return bool(torch.equal(hi, lo))
+            return bool(torch.equal(hi, lo)) and y_ok
         ref = [(min(0.0, float(torch.relu(a).min())), max(0.0, float(torch.relu(a).max()))) for a in self.acts]
         from vsiquantization_amd import _hip as H
         ma = [float(torch.relu(a).double().abs().mean()) for a in self.acts]
         got = self.recs[:, 0, H.ST_SUMABS] / self.recs[:, 0, H.ST_N]
         close = all(abs(float(v) - w) <= 1e-6 * w for v, w in zip(got, ma))
-        return [tuple(r) for r in mm.tolist()] == ref and close
+        return [tuple(r) for r in mm.tolist()] == ref and close and y_ok
 
 
 class ActQuant:
@@ -1338,8 +1373,8 @@ METRICS = {"c1": "Melements/s per-tensor observe + fake-quant fwd (256x256) + ac
            "c3": "Melements/s LSQ fake-quant fwd+bwd + achieved HBM GB/s vs roofline",
            "c4": "Melements/s backbone fake-quant fwd+bwd (weights + fused ReLU/act) + achieved "
                  "HBM GB/s vs roofline",
-           "c5": "Melements/s calibration observer pass (fused ReLU, 27 layers, deferred RCCL "
-                 "sync) + achieved HBM GB/s vs roofline",
+           "c5": "Melements/s calibration pass (fused ReLU written + observer records, 27 layers, "
+                 "deferred RCCL sync) + achieved HBM GB/s vs roofline",
            "act": "Melements/s batched activation observe + fake quant (per-call RCCL exchange) + "
                   "achieved HBM GB/s vs roofline"}
 
@@ -1471,6 +1506,8 @@ def main(argv=None):
     if a.workload == "c2":
         progress("c2: forward with uint8 codes")
         out["kernels"]["pc_observe_fq_fwd_with_codes"] = W.codes_variant()
+    if hasattr(W, "alt_kernels"):
+        out["kernels"].update(W.alt_kernels())
     del W
     torch.cuda.empty_cache()
     if a.workload == "c2" and not a.no_api:
@@ -1490,6 +1527,8 @@ def main(argv=None):
         progress(f"{key}: build + measure")
         Wx = build_workload(key, a, dev, rank, world)
         rx = measure(Wx, steps, warm, world)
+        if hasattr(Wx, "alt_kernels"):
+            rx["kernels"].update(Wx.alt_kernels())
         extras[key] = {"metric": METRICS[key], "value": rx["value"], "unit": "Melem/s",
                        "ms_per_step": rx["ms_per_step"], "steps": steps, "warmup": warm,
                        "scaling": "strong" if key == "act" else "weak",

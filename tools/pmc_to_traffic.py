@@ -29,8 +29,10 @@ KERNEL_KEYS = {
     # each way for the 27 weights
     "c4": [("k_fq_fwd<", "fwd_all_layers", 27), ("k_lsq_fwd_multi<", "fwd_all_layers", 1),
            ("k_lsq_bwd<", "bwd_all_layers", 27), ("k_lsq_bwd_multi<", "bwd_all_layers", 1)],
-    # C5: ONE multi-tensor (K2m) fused-ReLU deferred observer launch per calibration batch
-    "c5": [("k_observe_part_multi<", "observe_all_layers", 1)],
+    # C5: per calibration batch 27 fused-ReLU K2o launches (calibrate_qat_model's default:
+    # y = relu(c) written + the deferred observer's records); round 2/3: one K2m launch
+    "c5": [("k_observe_part_out1<", "act_observe_out_all_layers", 27),
+           ("k_observe_part_multi<", "observe_all_layers", 1)],
 }
 
 
