@@ -266,12 +266,14 @@ int vsiq_act_observe_fq_parts_f32(const float *c, float *y, void *codes, uint64_
  * counter, folds every record in K9's order and quantizes from registers.  Results bit
  * for bit equal to vsiq_act_observe_fq_parts_f32, stats included.  A workgroup that
  * waits more than ~42 ms at the barrier (the grid not co-resident) writes NaN and bumps
- * counter word 35 instead of spinning on.  Replaces the same reference call sequence
+ * counter word VSIQ_COUNTER_GRID_ERRORS (35) instead of spinning on; the caller reads it
+ * (the word is never reset by the library) and treats a non-zero count as an error.  Replaces the same reference call sequence
  * as K9 (quantization_manager.py:73-90 -> minmax.py:32-74 -> uniform.py:34-56).
  * Measured on MI355X no faster than K9 (the barrier's two cross-XCD round trips cost
  * what K9's second launch boundary does), so the manager and BASELINE C1 stay on K9;
  * this is an opt-in (observe_fake_quant(..., parts="k10")).
  */
+#define VSIQ_COUNTER_GRID_ERRORS 35
 int vsiq_act_observe_fq_grid_f32(const float *c, float *y, void *codes, uint64_t *mask, int64_t n, int act,
                                  double *stats_out, float *run_minmax, double *qp_out, int symmetric,
                                  double qden, double eps, int qmin, int qmax, double *ws, int64_t ws_len,

@@ -27,6 +27,7 @@ c_d = ctypes.c_double
 
 ABI_VERSION = 8
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
+COUNTER_GRID_ERRORS = 35   # VSIQ_COUNTER_GRID_ERRORS (K10's barrier-timeout count)
 
 # record layouts (include/vsiq.h)
 ST_MIN, ST_MAX, ST_NAN, ST_SUMABS, ST_SUM, ST_SUMSQ, ST_N, ST_MEANABS, ST_MEAN, ST_STD = range(10)

@@ -61,6 +61,7 @@ struct Site {
   int drifting = 0;                 // consecutive drifting checks
   uint32_t prev_best = 0;           // the gate before the running re-tune
   int retunes = 0;
+  int gen = 0;                      // tuning round: retune() starts a new one
   uint64_t last_sel = 0;            // g_sel when this site was last launched
 };
 
@@ -69,6 +70,7 @@ struct Sample {
   Site *site = nullptr;
   int cand = 0;   // -1: a drift sample of the tuned gate
   int dev = 0;
+  int gen = 0;    // the site's tuning round when issued: samples of an earlier round are dropped
 };
 
 using Key = std::tuple<const void *, int64_t, int64_t, int>;
@@ -122,6 +124,7 @@ void retune(Site &s) {
   s.since_watch = 0;
   s.drifting = 0;
   ++s.retunes;
+  ++s.gen;   // timings still in flight belong to the old round (taken under the old load)
 }
 
 void watch_sample(Site &s, float ms) {
@@ -146,8 +149,11 @@ void harvest_locked() {
       continue;
     }
     float ms = 0.0f;
+    const bool current = p->gen == p->site->gen;
     if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f) {
-      if (p->cand < 0) {
+      if (!current) {
+        // a sample of the round before a re-tune: not counted in the new round's issued[]
+      } else if (p->cand < 0) {
         watch_sample(*p->site, ms);
       } else if (!p->site->done) {
         p->site->ms[p->cand].push_back(ms);
@@ -155,7 +161,7 @@ void harvest_locked() {
       }
       g_pool[p->dev].emplace_back(p->a, p->b);
     } else {
-      if (p->cand >= 0 && !p->site->done) p->site->issued[p->cand]--;   // lost sample: issue again
+      if (current && p->cand >= 0 && !p->site->done) p->site->issued[p->cand]--;   // lost sample: issue again
       (void)hipGetLastError();
     }
     delete p;
@@ -249,6 +255,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   p->site = &s;
   p->cand = c;
   p->dev = dev;
+  p->gen = s.gen;
   if (c >= 0) {
     s.issued[c]++;
     sel.gate = s.ticks[c];
@@ -264,7 +271,7 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (hipEventRecord(p->b, st) != hipSuccess) {
     (void)hipGetLastError();
-    if (p->cand >= 0) p->site->issued[p->cand]--;
+    if (p->cand >= 0 && p->gen == p->site->gen) p->site->issued[p->cand]--;
     g_pool[p->dev].emplace_back(p->a, p->b);
     delete p;
     return;

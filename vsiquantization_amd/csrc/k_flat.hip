@@ -574,6 +574,7 @@ constexpr int kGridBarArrive = 1 + kArriveGroups;   // counter words (after arri
 constexpr int kGridBarDepart = 2 + kArriveGroups;
 constexpr int kGridBarErrors = 3 + kArriveGroups;
 static_assert(kGridBarErrors < VSIQ_COUNTER_WORDS, "counter words");
+static_assert(kGridBarErrors == VSIQ_COUNTER_GRID_ERRORS, "include/vsiq.h names this word");
 constexpr uint64_t kGridBarTimeout = 1ull << 22;    // wall-clock ticks (100 MHz)
 
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int S>

@@ -7,7 +7,9 @@ all_gather of the records (``all_gather_into_tensor`` on every backend), then a
 fold in rank order on every rank -- min / max exact, the sums in float64 in a fixed
 order, so every rank holds the same bits -- followed by the reference's running
 update (observers/minmax.py:42-47) and the f64 qparams.  min/max and the qparams are
-bit-identical to a 1-GPU run; the sums differ only in float64 summation order.
+bit-identical to a 1-GPU run (no activation or ReLU; a fused SiLU follows each rank's
+own shard layout, so SiLU parity with a 1-GPU run is not pinned); the sums differ only
+in float64 summation order.
 (``allreduce_stats`` -- MAX over [-min, max], SUM over the sums -- is what the
 deferred sync uses over all records of all layers at once.)
 
@@ -78,7 +80,8 @@ def gather_finalize(stats: torch.Tensor, run_minmax: torch.Tensor, *, symmetric:
     float64 -- the same bits on every rank), writes the batch's stats record and applies
     the running update + f64 qparams (vsiq_observe_finalize_ranks).  Returns (stats
     f64[ST_LEN], qp f64[QP_LEN]); min/max/qparams bit-identical to one GPU over the whole
-    batch."""
+    batch when the ranks' records were taken with act None / "relu" (a fused SiLU follows
+    each rank's own shard layout; see observe_gather_fake_quant)."""
     from .fakequant import qden
     gathered = gather_stats(stats, group)
     dev = stats.device
@@ -98,8 +101,12 @@ def observe_gather_fake_quant(x: torch.Tensor, run_minmax: torch.Tensor, *, symm
     quantization_manager.py:73-90 under DDP): the local K2 pass (stats record only), ONE
     all_gather of the ranks' records, and ONE launch that folds them in rank order, applies
     the running update + f64 qparams and fake-quantizes act(x) (vsiq_act_fq_fwd_ranks_f32).
-    Two launches and one collective per call; min / max / qparams / y bit-identical to one
-    GPU over the whole batch.  Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None)."""
+    Two launches and one collective per call; for act None / "relu", min / max / qparams / y
+    are bit-identical to one GPU over the whole batch.  A fused SiLU follows the reference
+    CPU layout of THIS RANK's shard (its own size and local element indices decide which
+    elements take glibc's scalar exp), so SiLU parity with a 1-GPU run over the whole batch
+    is not pinned -- each rank equals the reference's F.silu on its own shard.
+    Returns (y, qp f64[QP_LEN], stats f64[ST_LEN], mask | None)."""
     from .fakequant import _i64, observe_tensor, qden
     x = H.require_device_f32(x)
     _, local = observe_tensor(x, symmetric=symmetric, num_bits=num_bits, eps=eps, run_minmax=None,

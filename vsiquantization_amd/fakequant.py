@@ -469,6 +469,13 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
                                                   int(qmin), int(qmax), H.ptr(w.ws), _i64(w.ws_len),
                                                   H.ptr(w.counter), H.stream_of(dev))
         H.check(rc, "vsiq_act_observe_fq_grid_f32")
+        # a workgroup that timed out at the grid barrier wrote NaN and counted itself: fail
+        # loudly (one host sync; K10 is an opt-in measurement path)
+        err = w.counter[H.COUNTER_GRID_ERRORS:H.COUNTER_GRID_ERRORS + 1]
+        if int(err.item()):
+            err.zero_()
+            raise H.VsiqError("vsiq_act_observe_fq_grid_f32: grid barrier timed out (the grid was not "
+                              "co-resident); the outputs of the timed-out workgroups are NaN")
     elif parts:   # True / "k9"
         w = H.workspace(dev, n)
         rc = H.lib().vsiq_act_observe_fq_parts_f32(H.ptr(x), H.ptr(y), H.ptr(codes), H.ptr(mask), _i64(n),
