@@ -744,7 +744,9 @@ class ActQuant:
     name = "batched activation quant: YOLOv8n backbone, per-call MinMax observe (+RCCL) + fake quant, fused ReLU"
     group = 2
 
-    def __init__(self, dev, world, rank, total_batch=ACT_BATCH, bits=4):
+    def __init__(self, dev, world, rank, total_batch=ACT_BATCH, bits=4, exchange=None):
+        """exchange: the per-call RCCL exchange (all_gather + K1r); default world > 1 (a
+        1-rank group can force it to rehearse the collective path, tests)."""
         from vsiquantization_amd import _hip as H
         from vsiquantization_amd.fakequant import qden
         if total_batch % world:
@@ -753,6 +755,7 @@ class ActQuant:
         lib = H.lib()
         st = H.stream_of(dev)
         self.world = world
+        self.exchange = world > 1 if exchange is None else bool(exchange)
         self.batch = total_batch // world
         self.layers = yolov8n_backbone()
         self.shape = (self.batch, 3, 320, 320)
@@ -769,7 +772,7 @@ class ActQuant:
             t["cnt"] = torch.zeros(H.COUNTER_WORDS, dtype=torch.int32, device=dev)
             P = {k: H.ptr(v) for k, v in t.items()}
             n = H.c_i64(x.numel())
-            loc = world == 1   # one GPU: the observer pass updates the state and writes qparams itself
+            loc = not self.exchange   # no exchange: the observer pass updates the state and writes qparams itself
             t["obs"] = (P["x"], n, H.ACT_RELU, P["st"], P["rmm"] if loc else None, P["qp"] if loc else None,
                         1, qd, 1e-8, P["ws"], H.c_i64(t["ws"].numel()), P["cnt"], st)
             t["gat"] = torch.empty(world * H.ST_LEN, dtype=torch.float64, device=dev)
@@ -787,7 +790,7 @@ class ActQuant:
 
     def launch(self, i):
         rc = 0
-        if self.world == 1:
+        if not self.exchange:
             for t in self.L:
                 rc |= self.f_obs(*t["obs"])
                 rc |= self.f_fq(*t["fq"])
@@ -1135,10 +1138,18 @@ def measure(W, steps, warmup, world, graphs=None):
     groups = [(g0, min(ns, steps - g0)) for g0 in range(0, steps, ns)]
     if graphs is None:
         graphs = os.environ.get("VSIQ_BENCH_GRAPH", "1") == "1"
-    captured = capture_groups(W, groups, len(names)) if graphs and world == 1 else None
+    # graphs under RCCL too: a step holding collectives (the act leg's per-layer all_gather,
+    # C5's sync all-reduces) is captured whole, so the N > 1 timed region replays the
+    # exchange with no host work between the kernels; gloo collectives are not capturable
+    can = graphs and (world == 1 or dist.get_backend() == "nccl")
+    captured = capture_groups(W, groups, len(names)) if can else None
+    if world > 1 and not _agree(captured is not None, world):   # every rank captured, or none uses graphs
+        captured = None
     use_graph, trial = False, None
     if captured is not None:
-        use_graph, trial = _pick_launch(W, groups, captured)
+        use_graph, trial = _pick_launch(W, groups, captured, world=world)
+        if world > 1:
+            use_graph = _agree(use_graph, world)
     dt, evs = _timed(W, groups, names, steps, world, captured if use_graph else None)
     alt = _timed(W, groups, names, steps, world, None if use_graph else captured) if captured is not None else None
     out = _report(W, steps, world, dt, _durations(evs, names, steps), names, settle, gate_sites)
@@ -1154,6 +1165,17 @@ def measure(W, steps, warmup, world, graphs=None):
     return out
 
 
+def _agree(flag, world):
+    """True only if `flag` is true on every rank (all-reduce MIN; RCCL tensors on the GPU,
+    gloo on the CPU): ranks whose steps hold collectives must run the same launch mode."""
+    if world <= 1:
+        return bool(flag)
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([int(bool(flag))], dtype=torch.int64, device=torch.cuda.current_device() if on_gpu else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t))
+
+
 def _durations(evs, names, steps):
     return {k: sum(e[i].elapsed_time(e[i + 1]) for e in evs) / steps * 1e-3 for i, k in enumerate(names)}
 
@@ -1163,16 +1185,18 @@ class _NoEvent:
         pass
 
 
-def _pick_launch(W, groups, graphs, reps=5, margin=0.01, min_ms=20.0, max_reps=50):
+def _pick_launch(W, groups, graphs, reps=5, margin=0.01, min_ms=20.0, max_reps=50, world=1):
     """Untimed trial: up to 4 launch groups each way, `reps` rounds -- more (up to
     `max_reps`) while the trial has run less than `min_ms` per mode, so that a short
     workload's (C1: ~0.25 ms per round) choice is not decided by host noise -- median
     wall time per mode; graph replay is chosen only when it is faster by more than
-    `margin` (direct launches are the default).  Returns (use graph?, {mode: median ms})."""
+    `margin` (direct launches are the default).  Several ranks: exactly `reps` rounds
+    (every rank runs the same collectives; the caller agrees on the choice).  Returns
+    (use graph?, {mode: median ms})."""
     sel = list(range(min(4, len(groups))))
     t = {"direct": [], "graph": []}
     r = 0
-    while r < reps or (r < max_reps and min(sum(t["direct"]), sum(t["graph"])) < min_ms):
+    while r < reps or (world == 1 and r < max_reps and min(sum(t["direct"]), sum(t["graph"])) < min_ms):
         r += 1
         for mode in ("direct", "graph"):
             torch.cuda.synchronize()
@@ -1465,6 +1489,12 @@ def main(argv=None):
         else:
             dist.init_process_group(backend)
         world = dist.get_world_size()
+        # the ranks that joined, counted by a real collective of this run (RCCL on the GPUs)
+        t = torch.ones(1, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        ranks_joined = int(t.item())
+    else:
+        ranks_joined = 1
     import vsiquantization_amd  # noqa: F401  (torch first, then the HIP library)
     from vsiquantization_amd import _hip as H
     for kv in a.tune:
@@ -1498,6 +1528,8 @@ def main(argv=None):
         "store_gate": r["store_gate"],
         "launch": r["launch"],
         "timing_events": timing_events_kind(),
+        "ranks_joined": ranks_joined,
+        "backend": (dist.get_backend() if world > 1 else None),
     }
     if "alt_launch" in r:
         out["alt_launch"] = r["alt_launch"]

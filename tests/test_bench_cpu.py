@@ -92,3 +92,23 @@ def test_settle_gates_agrees_across_ranks():
     ret = mp.Manager().dict()
     mp.spawn(_settle_worker, args=(2, port, ret), nprocs=2, join=True)
     assert ret[0] == ret[1] == 32          # 4 rounds of 8 steps on both ranks
+
+
+def _agree_worker(rank, world, port, ret):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ret[rank] = (bench._agree(True, world), bench._agree(rank == 0, world), bench._agree(False, world))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_launch_mode_agreed_across_ranks():
+    """measure()'s capture / graph choice is agreed (all-reduce MIN): graphs only when
+    every rank captured and every rank's trial chose them."""
+    import torch.multiprocessing as mp
+    port = 29900 + os.getpid() % 90
+    ret = mp.Manager().dict()
+    mp.spawn(_agree_worker, args=(2, port, ret), nprocs=2, join=True)
+    assert ret[0] == ret[1] == (True, False, False)
