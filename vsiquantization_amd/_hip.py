@@ -285,9 +285,10 @@ def require_device_f32(x: torch.Tensor, what: str = "x") -> torch.Tensor:
     if x.device.type != "cuda":
         raise VsiqError(
             f"{what} is on {x.device}: this operation runs on MI355X (HIP) only. CPU float32 "
-            "tensors are served by the native host path of the reference's per-tensor classes "
-            "(UniformQuantizer, LSQQuantizer, MinMaxObserver, QuantizationManager, FakeQuantize); "
-            "the per-channel, multi-tensor and fused-layer kernels need the GPU.")
+            "tensors are served by the native host path of the reference's classes "
+            "(UniformQuantizer, LSQQuantizer, MinMaxObserver, the per-channel observer / quantizer, "
+            "QuantizationManager, FakeQuantize); the multi-tensor, fused-kernel and LSQFakeQuantize "
+            "kernels need the GPU.")
     if x.dtype != torch.float32:
         raise TypeError(f"{what}: only float32 is supported by the HIP fake-quant path, got {x.dtype}")
     return x.contiguous()

@@ -147,11 +147,14 @@ std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool
   const int64_t C = x.dim() > 0 ? x.size(0) : 1;
   const int64_t rowlen = C > 0 ? x.numel() / C : 0;
   Tensor y = at::empty_like(x);
-  Tensor scale = at::empty({C}, x.options().dtype(at::kDouble));
-  Tensor zp = at::empty({C}, x.options().dtype(at::kDouble));
+  // scale and zp (and the row stats) in ONE allocation: host time per call of the public
+  // API step (views of a no-history buffer; nothing differentiates through them)
+  Tensor q64 = at::empty({(want_row_stats ? 5 : 2) * C}, x.options().dtype(at::kDouble));
+  Tensor scale = q64.narrow(0, 0, C);
+  Tensor zp = q64.narrow(0, C, C);
   const bool grad = torch::autograd::compute_requires_grad(x);
   Tensor mask = grad ? mask_buffer(C, rowlen, x) : Tensor();
-  Tensor rs = want_row_stats ? at::empty({C, 3}, x.options().dtype(at::kDouble)) : Tensor();   // None
+  Tensor rs = want_row_stats ? q64.narrow(0, 2 * C, 3 * C).view({C, 3}) : Tensor();   // None
   check(vsiq_pc_observe_fq_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), C, rowlen,
                                ptr<float>(run_min), ptr<float>(run_max), ptr<double>(scale), ptr<double>(zp),
                                want_row_stats ? ptr<double>(rs) : nullptr, sym ? 1 : 0, (int)qmin, (int)qmax, qden,
