@@ -243,7 +243,7 @@ def test_observe_parts_out_every_group_count(groups):
     exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
     assert torch.equal(got[0, exact], want[0, exact])
     torch.testing.assert_close(got, want, rtol=1e-12, atol=0.0, equal_nan=True)
-    G.assert_bitwise_f32(npy(y), npy(torch.relu(x)), "y")
+    G.assert_bitwise_f32(npy(y), npy(FQ.activation(x, "relu")), "y")   # CPU relu: -0.0 kept
 
 
 def test_silu_layout_recorded_with_qparams_survives_checkpoint(pin):
