@@ -262,6 +262,8 @@ def test_silu_layout_recorded_with_qparams_survives_checkpoint(pin):
 
     def learn(qm):
         qm.is_learning_scale, qm.is_quantize = True, True
+        if not isinstance(qm.scale, torch.Tensor):   # a fresh manager (the checkpoint brings the value)
+            qm.scale = torch.tensor(0.1, dtype=torch.float64, device=DEV)
         qm.make_learn_qparameter()
 
     def run(qm):
