@@ -1582,9 +1582,29 @@ def main(argv=None):
         out["configs"] = extras
     if rank == 0:
         print(json.dumps(out), flush=True)
+        print(compact_summary(out), file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def compact_summary(out) -> str:
+    """The line's key figures in a few hundred characters on stderr (after the JSON line):
+    a driver that keeps only the tail of a long line still records every config's value
+    and roofline fraction, the public-API timings and the chosen store gates."""
+    def leg(name, d):
+        ks = ",".join(f"{k}={v['frac']:.3f}" for k, v in d.get("kernels", {}).items()
+                      if isinstance(v, dict) and v.get("frac") and v.get("in_step", True))
+        cb = (d.get("cpu_baseline") or {}).get("value")
+        return (f"{name} {d['value']:.1f}Melem/s {1e3 * d['ms_per_step']:.2f}us {d.get('launch', '')[:6]} [{ks}]"
+                + (f" cpu={cb:.1f}" if cb else ""))
+    parts = [leg(out["config"].get("workload", "")[:2], out)]
+    parts += [leg(k, v) for k, v in (out.get("configs") or {}).items()]
+    if "batched_act_quant" in out:
+        parts.append(leg("act", out["batched_act_quant"]))
+    api = {k: round(v, 1) for k, v in out.items() if k.startswith("api_") and isinstance(v, (int, float))}
+    gates = ",".join(f"{s['site']}:{s['gate_ticks']}" for s in out.get("store_gate", {}).get("sites", []))
+    return "[bench summary] " + " | ".join(parts) + f" | api {api} | gates {gates}"
 
 
 if __name__ == "__main__":
