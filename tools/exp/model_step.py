@@ -8,10 +8,11 @@ utils/quantize_manager.py) -- trained with forward + backward + SGD step, in fou
              learnable weight fake quant and the activation fake quant of uniform.py:47-56
              (x / s + zp, RoundStraightThrough, clamp, (q - zp) * s, ScaleGradient), the
              fused layer's conv -> ReLU -> quantize_out (modules/fused.py:112-134)
-  ours       vsiquantization_amd's fused layers (K5 act fake quant with the ReLU fused, K1/K4
-             weight fake quant, C++ autograd nodes)
-  ours+      the same with enable_multi_tensor_weights (K7: one weight launch each way)
-             and enable_deferred_qparam_grads (K4d records + one fold launch)
+  per-call   vsiquantization_amd's fused layers on the per-call path (K5 act fake quant with
+             the ReLU fused, K1/K4 weight fake quant, C++ autograd nodes; model_launches=False)
+  default    the reference's plain sequence (calibrate_qat_model, activate_learning_qparam,
+             activate_quantizer), which since round 4 installs the model-level launches by
+             itself: K7 (one weight launch each way) and K4d (records + one fold launch)
 
 The 27 layers take the backbone's (cout, k, stride) in forward order with cin chained
 (the CSP concats are not modelled), 320x320 input, w2/a4 symmetric (the YAML default).
@@ -29,8 +30,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from vsiquantization_amd.modules.fused import ConvBnReLU  # noqa: E402
-from vsiquantization_amd.quantizers.deferred import enable_deferred_qparam_grads  # noqa: E402
-from vsiquantization_amd.quantizers.foreach import enable_multi_tensor_weights  # noqa: E402
 from vsiquantization_amd.utils.quantize_manager import (activate_learning_qparam, activate_quantizer,  # noqa: E402
                                                         calibrate_qat_model, data_calib)
 
@@ -53,14 +52,14 @@ def chain(seed=0):
     return mods
 
 
-def ours(mods):
+def ours(mods, launches=None):
     m = nn.Sequential(*[ConvBnReLU(cv, bn, nn.ReLU(), "MinMaxObserver", "UniformQuantizer", "MinMaxObserver",
                                    "UniformQuantizer", True, True, True, BITS_W, BITS_A) for cv, bn in mods]).to(dev)
     g = torch.Generator().manual_seed(5)
     loader = [(torch.randint(0, 256, (8, 3, 320, 320), generator=g, dtype=torch.uint8), None) for _ in range(2)]
     calibrate_qat_model(m, loader, data_calib, dev)
-    activate_learning_qparam(m)
-    activate_quantizer(m)
+    activate_learning_qparam(m, model_launches=launches)
+    activate_quantizer(m, model_launches=launches)
     return m.train()
 
 
@@ -143,7 +142,7 @@ def main():
     x = (torch.randint(0, 256, (BATCH, 3, 320, 320), generator=torch.Generator().manual_seed(9),
                        dtype=torch.uint8).float() / 255).to(dev)
     want = os.environ.get("VARIANTS", "float,reference,ours,plus").split(",")
-    base = ours(chain())
+    base = ours(chain(), launches=False)
     rows = {}
     if "float" in want:
         rows["float"] = timed(step_fn(nn.Sequential(*[RefLayer(l, False) for l in base]).to(dev), x))
@@ -151,12 +150,10 @@ def main():
         rows["reference (eager torch)"] = timed(step_fn(nn.Sequential(*[RefLayer(l, True) for l in base]).to(dev),
                                                         x))
     if "ours" in want:
-        rows["ours"] = timed(step_fn(base, x))
+        rows["ours, per-call path"] = timed(step_fn(base, x))
     if "plus" in want:
-        plus = ours(chain())
-        enable_multi_tensor_weights(plus)
-        enable_deferred_qparam_grads(plus)
-        rows["ours + K7 weights + K4d deferred"] = timed(step_fn(plus, x))
+        plus = ours(chain())   # the reference sequence: K7 + K4d installed by activate_*
+        rows["ours, default (K7 + K4d)"] = timed(step_fn(plus, x))
     print(f"batch {BATCH}, 27 layers, 320x320, w{BITS_W}/a{BITS_A}; ms per training step (fwd + bwd + SGD)")
     fl = rows["float"][0] if "float" in rows else 0.0
     for k, (ms, loss) in rows.items():

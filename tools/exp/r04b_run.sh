@@ -15,4 +15,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C -d gpurun_out/pmc_c5_$C -o run --output-format csv -- python3 -u bench.py --workload c5 --steps 16 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_c5_$C.log 2>&1 || { echo "pmc $C rc=$?"; exit 1; }
 done
+for B in 32 64 128; do
+  BATCH=$B timeout -k 10 300 python3 -u tools/exp/model_step.py > gpurun_out/model_step_$B.log 2>&1 || { echo "model_step $B rc=$?"; tail gpurun_out/model_step_$B.log; exit 1; }
+  cat gpurun_out/model_step_$B.log
+done
 echo done
