@@ -1084,7 +1084,10 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   const int64_t grid = observe_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
-  VSIQ_ACT(act, launch_observe, vec, g_tune.nontemporal != 0, x, n, stats_out, run_minmax, qp_out,
+  // a tensor that fits the 256 MB Infinity Cache can be read with cached loads, so the fake
+  // quant that re-reads it right after (observe + quantize, K2 -> K1) may hit there
+  const bool nt = g_tune.nontemporal != 0 && !((n * 4) >> 20 < (int64_t)g_tune.obs_temporal_mb);
+  VSIQ_ACT(act, launch_observe, vec, nt, x, n, stats_out, run_minmax, qp_out,
            symmetric, qden, eps, ws, counter, act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
 }
@@ -1272,6 +1275,10 @@ int vsiq_set_tuning(int key, int value) {
     case VSIQ_TUNE_XCD_ORDER:
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.xcd_order = value;
+      return 0;
+    case VSIQ_TUNE_OBS_TEMPORAL_MB:
+      if (value < 0 || value > 4096) return VSIQ_E_ARG;
+      g_tune.obs_temporal_mb = value;
       return 0;
     case VSIQ_TUNE_K2O_FORM:
       if (value != 0 && value != 1) return VSIQ_E_ARG;
