@@ -237,3 +237,24 @@ def test_quantizer_off_weight_stays_unquantized():
     yb, gxb = _step(b, x)
     torch.cuda.synchronize()
     assert torch.equal(ya, yb) and torch.equal(gxa, gxb)
+
+
+def test_symmetric_tensor_zero_point_stays_per_call():
+    """A symmetric quantizer handed a gradient-requiring tensor zero point (K4 zp_learn 2:
+    zp used as given) is left out of K7 / K4d and gives the per-call path's results,
+    including the zero point's gradient."""
+    a, b = _pair()
+    for m in (a, b):
+        for layer in m:
+            for qm in (layer.weight_quantizer, layer.activation_quantizer):
+                if qm.quantizer.symmetric:
+                    qm.zero_point = nn.Parameter(torch.tensor(0.25, dtype=torch.float64, device=DEV))
+    x = _x(13)
+    ya, gxa = _step(a, x)
+    yb, gxb = _step(b, x)
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb) and torch.equal(gxa, gxb)
+    ga, gb = _grads(a), _grads(b)
+    assert any(n.endswith("weight_quantizer.zero_point") for n in ga)
+    _assert_same_grads(ga, gb, "sym tensor zp")
+    assert D.pending_count() == 0

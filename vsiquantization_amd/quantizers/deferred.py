@@ -184,6 +184,8 @@ def _eligible(qm) -> bool:
     if isinstance(z, torch.Tensor) and z.requires_grad and not (z.is_cuda and z.dtype == torch.float64
                                                                 and z.dim() == 0):
         return False
+    if q.symmetric and isinstance(z, torch.Tensor) and z.requires_grad and not getattr(q, "learns_zero_point", False):
+        return False   # a zero point used as given with its gradient (K4 zp_learn 2): per-call path
     cal = getattr(q, "calib_grad_scale", 1)
     return not (isinstance(cal, torch.Tensor) and cal.numel() > 1)
 

@@ -50,6 +50,8 @@ def _weight_spec(layer):
         return None
     qm._join()
     gscale, zp, learn_zp = q.learn_args(w, qm.zero_point)
+    if learn_zp == 2:   # a zero point used as given with its gradient: the per-layer path (K4 mode 2)
+        return None
     return w, LsqSpec(s, zp, q.qmin, q.qmax, gscale, learn_zp)
 
 
