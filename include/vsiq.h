@@ -308,8 +308,8 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
  * K2o: the deferred observer pass that also writes y = act(c) (n floats): a calibration
  * forward of a fused layer in one pass -- the activation the next layer consumes
  * (modules/fused.py:133) and the deferred observer's records of it, in the
- * vsiq_act_observe_part_f32 record format; vsiq_observe_part_out_records(n) (<=
- * VSIQ_PART_MAX_RECORDS) records, one per workgroup.  y bit-identical to
+ * vsiq_act_observe_part_f32 record format; vsiq_observe_part_out_records(n) records,
+ * one per workgroup (<= VSIQ_PART_MAX_RECORDS up to 64M elements).  y bit-identical to
  * vsiq_act_fwd_f32; folded min/max/nan/n equal to K2p's, the sums to float64 summation
  * order (VSIQ_TUNE_K2O_FORM 1: K2p's grid, records bit-identical to it).
  */

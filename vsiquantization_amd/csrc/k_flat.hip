@@ -283,8 +283,10 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_out(const float *__rest
 // record through LDS, then the G stores: no loop, so no store shares a vmcnt wait with a
 // later load (a grid-stride step waits for its own stores before the next step's loads
 // can be consumed: hipcc's s_waitcnt treats mixed load / store counts as out of order).
-// One record per WORKGROUP, so the record count stays <= VSIQ_PART_MAX_RECORDS with a
-// grid of up to 4096 workgroups (k2o_groups: the smallest G that fits).  The block
+// One record per WORKGROUP: k2o_groups picks the smallest G whose grid fits
+// VSIQ_PART_MAX_RECORDS (4096) workgroups, up to 16 groups per lane -- 4096 records cover
+// 64M elements; a larger tensor keeps G = 16 and one record per workgroup beyond that
+// (vsiq_observe_part_out_records sizes its slot; the fold takes any count).  The block
 // reduction runs before the stores (no fence between the y stores and the barrier).
 template <bool VEC, bool NT, int ACT, int G>
 __global__ __launch_bounds__(kBlock) void k_observe_part_out1(const float *__restrict__ x, float *__restrict__ y,
