@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 COUNTER_GRID_ERRORS = 35   # VSIQ_COUNTER_GRID_ERRORS (K10's barrier-timeout count)
 
