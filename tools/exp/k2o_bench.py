@@ -31,7 +31,7 @@ def main():
     acts = [torch.randn(128, co, h, h, device=dev, generator=gen) for _, co, _, _, h in bench.yolov8n_backbone()]
     ys = [torch.empty_like(a) for a in acts]
     n = sum(a.numel() for a in acts)
-    slot = torch.empty(H.PART_MAX_RECORDS * H.PART_LEN * 4, dtype=torch.float64, device=dev)
+    slot = torch.empty((1 << 16) * H.PART_LEN, dtype=torch.float64, device=dev)   # G=1 at 52M: 51200 records
     relu = H.ACT_RELU
 
     def k2o():

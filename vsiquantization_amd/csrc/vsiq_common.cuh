@@ -73,7 +73,7 @@ struct Tuning {
   std::atomic<int> xcd_order{1};           // XCD-contiguous block order where neighbours share lines
   std::atomic<int> k2o_form{0};            // K2o: 0 one-shot (one record per workgroup), 1 grid-stride (K2p's records)
   std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = by size)
-  std::atomic<int> obs_temporal_mb{0};     // K2: cached (temporal) loads for tensors of <= this many MB
+  std::atomic<int> obs_temporal_mb{256};   // K2: cached (temporal) loads for tensors under this many MB
 };
 extern Tuning g_tune;
 
