@@ -1271,41 +1271,6 @@ def gate_retunes(H):
                if t.startswith("retunes="))
 
 
-def api_us_per_step(dev, steps=360, warmup=30):
-    """The C2 step through the PUBLIC Python API (what a QAT user runs):
-    PerChannelMinMaxObserver.observe_quantize(W, PerChannelUniformQuantizer(8, False))
-    + backward, fresh gradient per step, host + GPU time per step (µs), 4 weights in
-    rotation.  The forward is one pybind call into a C++ autograd node and the backward a
-    C++ node (csrc/torch_ops.cpp); about 25 us of it is torch's autograd engine handing
-    the backward to its device thread and back, which one backward() per model amortizes
-    over all layers and which this one-weight step pays in full."""
-    import vsiquantization_amd as V
-    shape = C2PerChannel.shape
-    gen = torch.Generator(device=dev).manual_seed(11)
-    xs = [(torch.randn(shape, device=dev, generator=gen) * 0.05).requires_grad_(True) for _ in range(4)]
-    g = torch.randn(shape, device=dev, generator=gen)
-    obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
-
-    def step(i):
-        x = xs[i % len(xs)]
-        x.grad = None
-        y, _ = obs.observe_quantize(x, q)
-        y.backward(g)
-
-    for i in range(warmup):
-        step(i)
-    reps = []
-    for r in range(9):   # host time is noisy on a shared box: median (and min) of 9 runs
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(steps // 9):
-            step(i)
-        torch.cuda.synchronize()
-        reps.append((time.perf_counter() - t0) / (steps // 9) * 1e6)
-    reps.sort()
-    return reps[4], reps[0]
-
-
 def _interleaved_us(fns, steps=40, reps=9, warmup=30):
     """Host + GPU time per call (us) of each step function, the reps interleaved so that
     both see the same host load: (median, min) per function."""
@@ -1324,18 +1289,32 @@ def _interleaved_us(fns, steps=40, reps=9, warmup=30):
     return [(sorted(v)[len(v) // 2], min(v)) for v in res]
 
 
-def api_torch_reference_us(dev):
-    """Torch's own trivial autograd step on the same box, the floor of any public-API
-    step there: (x * 1.0).backward(g) on the C2 weight shape (4 weights in rotation), and
-    the learnable per-call comparison -- UniformQuantizer(4, True).quantize(x, s, 0, True)
-    fwd + bwd (K1 + K4 through the C++ node, f64 scale Parameter) against torch's own
-    x * s fwd + bwd on one 8x16x20x20 activation (tools/exp/api_learn.py's case).
-    Interleaved median (and min) of 9 runs each, us per step."""
+def api_timings(dev):
+    """Public-API step timings, interleaved so every step function sees the same host load
+    (host time on the shared boxes moves 2x between processes and minutes): median (and
+    min) of 9 runs of 40 steps each, us per step.
+
+    * api_us_per_step: the C2 step through the PUBLIC Python API (what a QAT user runs):
+      PerChannelMinMaxObserver.observe_quantize(W, PerChannelUniformQuantizer(8, False)) +
+      backward, fresh gradient per step, 4 weights in rotation (C++ autograd nodes,
+      csrc/torch_ops.cpp);
+    * api_torch_ref_us_per_step: torch's own trivial autograd step on the same tensors,
+      (x * 1.0).backward(g) -- the floor of any public-API step on that box;
+    * api_learn_us_per_step vs api_learn_torch_xs_us_per_step: the learnable per-call step,
+      UniformQuantizer(4, True).quantize(x, s, 0, True) fwd + bwd (K1 + K4, f64 scale
+      Parameter) against torch's own x * s fwd + bwd on one 8x16x20x20 activation."""
     import vsiquantization_amd as V
     gen = torch.Generator(device=dev).manual_seed(12)
     xs = [(torch.randn(C2PerChannel.shape, device=dev, generator=gen) * 0.05).requires_grad_(True)
           for _ in range(4)]
     g = torch.randn(C2PerChannel.shape, device=dev, generator=gen)
+    obs, qpc = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+
+    def ours(i):
+        x = xs[i % 4]
+        x.grad = None
+        y, _ = obs.observe_quantize(x, qpc)
+        y.backward(g)
 
     def trivial(i):
         x = xs[i % 4]
@@ -1357,8 +1336,9 @@ def api_torch_reference_us(dev):
         sc.grad = None
         (xa * sc.float()).backward(ga)
 
-    (tr, tr_min), (le, le_min), (tx, tx_min) = _interleaved_us([trivial, learn, torch_xs])
-    return {"api_torch_ref_us_per_step": tr, "api_torch_ref_us_per_step_min": tr_min,
+    (ou, ou_min), (tr, tr_min), (le, le_min), (tx, tx_min) = _interleaved_us([ours, trivial, learn, torch_xs])
+    return {"api_us_per_step": ou, "api_us_per_step_min": ou_min,
+            "api_torch_ref_us_per_step": tr, "api_torch_ref_us_per_step_min": tr_min,
             "api_learn_us_per_step": le, "api_learn_us_per_step_min": le_min,
             "api_learn_torch_xs_us_per_step": tx, "api_learn_torch_xs_us_per_step_min": tx_min}
 
@@ -1545,10 +1525,9 @@ def main(argv=None):
     if a.workload == "c2" and not a.no_api:
         progress("c2: public API timing")
         r0 = gate_retunes(H)
-        out["api_us_per_step"], out["api_us_per_step_min"] = api_us_per_step(dev)
+        out.update(api_timings(dev))
         out["api_gate_retunes"] = gate_retunes(H) - r0
         out["api_graph_us_per_step"] = api_graph_us_per_step(dev)
-        out.update(api_torch_reference_us(dev))
         torch.cuda.empty_cache()
 
     extras = {}

@@ -105,7 +105,8 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
                                           channel columns); 0: hardware order */
 #define VSIQ_TUNE_K2O_FORM 14          /* K2o: 0 (default) one-shot, one record per workgroup;
                                           1: grid-stride, vsiq_act_observe_part_f32's records */
-#define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = by size */
+#define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = default (2) */
+#define VSIQ_TUNE_K2O_BLOCK 17         /* K2o one-shot lanes per workgroup 256/512/1024, 0 = default */
 #define VSIQ_TUNE_OBS_TEMPORAL_MB 16   /* K2 (per-call observer): cached loads for tensors under N MB
                                           (the fake quant re-reading it may hit the 256 MB
                                           Infinity Cache); default 256, 0 = nontemporal always */
@@ -309,7 +310,8 @@ int vsiq_act_observe_part_f32(const float *c, int64_t n, int act, double *parts,
  * forward of a fused layer in one pass -- the activation the next layer consumes
  * (modules/fused.py:133) and the deferred observer's records of it, in the
  * vsiq_act_observe_part_f32 record format; vsiq_observe_part_out_records(n) records,
- * one per workgroup (<= VSIQ_PART_MAX_RECORDS up to 64M elements).  y bit-identical to
+ * one per workgroup (n / 2048 by default; not bounded by VSIQ_PART_MAX_RECORDS).  y
+ * bit-identical to
  * vsiq_act_fwd_f32; folded min/max/nan/n equal to K2p's, the sums to float64 summation
  * order (VSIQ_TUNE_K2O_FORM 1: K2p's grid, records bit-identical to it).
  */

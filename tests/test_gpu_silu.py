@@ -223,8 +223,9 @@ def test_observe_parts_out_equals_act_then_parts(n, act, pin):
         assert lib.vsiq_set_tuning(H.TUNE_K2O_FORM, 0) == 0
 
 
+@pytest.mark.parametrize("block", [256, 512, 1024])
 @pytest.mark.parametrize("groups", [1, 2, 4, 8, 16])
-def test_observe_parts_out_every_group_count(groups):
+def test_observe_parts_out_every_group_count(groups, block):
     """Every one-shot K2o groups-per-lane instance (VSIQ_TUNE_K2O_GROUPS) on a ragged,
     misaligned-tail tensor: y bitwise, folded min / max / NaN exact and sums to f64
     order against K2p."""
@@ -234,11 +235,14 @@ def test_observe_parts_out_every_group_count(groups):
     x = cu(c)
     want = FQ.fold_parts(FQ.observe_parts(x, act="relu").reshape(1, -1))
     assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, groups) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_K2O_BLOCK, block) == 0
     try:
         y, parts = FQ.observe_parts_out(x, "relu")
         assert parts.numel() == lib.vsiq_observe_part_out_records(H.c_i64(x.numel())) * H.PART_LEN
+        assert parts.numel() == -(-x.numel() // (4 * block * groups)) * H.PART_LEN
     finally:
         assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, 0) == 0
+        assert lib.vsiq_set_tuning(H.TUNE_K2O_BLOCK, 0) == 0
     got = FQ.fold_parts(parts.reshape(1, -1))
     exact = [H.ST_MIN, H.ST_MAX, H.ST_NAN, H.ST_N]
     assert torch.equal(got[0, exact], want[0, exact])

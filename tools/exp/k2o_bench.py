@@ -64,17 +64,38 @@ def main():
     rows = []
     rows.append(("act only (vsiq_act_fwd_f32)", *timed(act_only, 8)))
     rows.append(("K2p only (read)", *timed(k2p, 4)))
-    for form, g in ((1, 0), (0, 0), (0, 1), (0, 2), (0, 4), (0, 8), (0, 16)):
+    variants = [(1, 0, 0), (0, 0, 0)] + [(0, g, bs) for bs in (256, 512, 1024) for g in (1, 2, 4)]
+    for form, g, bs in variants:
         assert lib.vsiq_set_tuning(H.TUNE_K2O_FORM, form) == 0
         assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, g) == 0
-        name = "K2o grid-stride (round 3)" if form else f"K2o one-shot G={g or 'auto'}"
+        assert lib.vsiq_set_tuning(H.TUNE_K2O_BLOCK, bs) == 0
+        name = "K2o grid-stride (round 3)" if form else f"K2o one-shot G={g or 'dflt'} BS={bs or 'dflt'}"
         rows.append((name, *timed(k2o, 8)))
-    assert lib.vsiq_set_tuning(H.TUNE_K2O_FORM, 0) == 0
-    assert lib.vsiq_set_tuning(H.TUNE_K2O_GROUPS, 0) == 0
+    for key in (H.TUNE_K2O_FORM, H.TUNE_K2O_GROUPS, H.TUNE_K2O_BLOCK):
+        assert lib.vsiq_set_tuning(key, 0) == 0
+    # the sync's fold over a calibration run's slots (16 batches x 27 layers, default K2o)
+    from vsiquantization_amd.fakequant import fold_parts, part_out_slot_doubles
+    stride = max(part_out_slot_doubles(a.numel()) for a in acts)
+    slots = torch.zeros(16, len(acts), stride, dtype=torch.float64, device=dev)
+    for b in range(16):
+        for j, (a, y) in enumerate(zip(acts, ys)):
+            assert lib.vsiq_act_observe_part_out_f32(H.ptr(a), H.ptr(y), H.c_i64(a.numel()), relu,
+                                                     slots[b, j].data_ptr(), H.c_i64(stride), st) == 0
+    flat = slots.reshape(16 * len(acts), stride)
+    fold_parts(flat)
+    e0, e1 = bench.HipEvent(), bench.HipEvent()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(5):
+        fold_parts(flat)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"sync fold of 16 x 27 default K2o slots ({stride // 8} records max, "
+          f"{flat.numel() * 8 / 2**20:.0f} MB of slots): {e0.elapsed_time(e1) * 1e3 / 5:.1f} us")
     print(f"C5 phase: 27 fused-ReLU layers, batch 128, {n / 1e6:.1f}M elements, {reps} reps")
     for name, us, gbs in rows:
         print(f"{name:34s} {us:9.1f} us/phase  {gbs:8.1f} GB/s  frac {gbs / 8000:.3f}")
-    print("auto groups per layer:", [int(lib.vsiq_observe_part_out_records(H.c_i64(a.numel()))) for a in acts])
+    print("default records per layer:", [int(lib.vsiq_observe_part_out_records(H.c_i64(a.numel()))) for a in acts])
 
 
 if __name__ == "__main__":

@@ -41,7 +41,7 @@ TUNE_OBS_KERNEL, TUNE_OBS_GRID, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 8, 9, 10
 TUNE_STORE_GATE = 11
 TUNE_GATE_AUTOTUNE = 12
 TUNE_XCD_ORDER = 13
-TUNE_K2O_FORM, TUNE_K2O_GROUPS, TUNE_OBS_TEMPORAL_MB = 14, 15, 16
+TUNE_K2O_FORM, TUNE_K2O_GROUPS, TUNE_OBS_TEMPORAL_MB, TUNE_K2O_BLOCK = 14, 15, 16, 17
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 

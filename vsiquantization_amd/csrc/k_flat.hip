@@ -278,44 +278,45 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_out(const float *__rest
   store_part_record(a, parts, blockIdx.x, gridDim.x, n);
 }
 
-// K2o one-shot form (the default): workgroup b takes groups [b*256*G, (b+1)*256*G) --
-// G loads per lane issued at once, act + observer terms in registers, the workgroup's
-// record through LDS, then the G stores: no loop, so no store shares a vmcnt wait with a
-// later load (a grid-stride step waits for its own stores before the next step's loads
-// can be consumed: hipcc's s_waitcnt treats mixed load / store counts as out of order).
-// One record per WORKGROUP: k2o_groups picks the smallest G whose grid fits
-// VSIQ_PART_MAX_RECORDS (4096) workgroups, up to 16 groups per lane -- 4096 records cover
-// 64M elements; a larger tensor keeps G = 16 and one record per workgroup beyond that
-// (vsiq_observe_part_out_records sizes its slot; the fold takes any count).  The block
+// K2o one-shot form (the default): workgroup b (BS lanes) takes groups
+// [b*BS*G, (b+1)*BS*G) -- G loads per lane issued at once, act + observer terms in
+// registers, the workgroup's record through LDS, then the G stores: no loop, so no store
+// shares a vmcnt wait with a later load (a grid-stride step waits for its own stores
+// before the next step's loads can be consumed: hipcc's s_waitcnt treats mixed load /
+// store counts as out of order).  One record per WORKGROUP (k2o_records(n)); the block
 // reduction runs before the stores (no fence between the y stores and the barrier).
-template <bool VEC, bool NT, int ACT, int G>
-__global__ __launch_bounds__(kBlock) void k_observe_part_out1(const float *__restrict__ x, float *__restrict__ y,
-                                                               int64_t n, double *__restrict__ parts, SiluLay L) {
-  __shared__ float s_mn[kWaves], s_mx[kWaves];
-  __shared__ uint32_t s_nan[kWaves];
-  __shared__ double s_sa[kWaves], s_s1[kWaves], s_s2[kWaves];
+// Measured on MI355X (profiles/r04b_k2o_*): G = 2 streams best at every C5 size (52M
+// elements: 68.1 us = 0.77 of 8 TB/s, vs 76.8 us at G = 16 and 96 % of the activation
+// alone); BS trades the record count (the sync's fold) against the tail.
+template <bool VEC, bool NT, int ACT, int G, int BS>
+__global__ __launch_bounds__(BS) void k_observe_part_out1(const float *__restrict__ x, float *__restrict__ y,
+                                                           int64_t n, double *__restrict__ parts, SiluLay L) {
+  constexpr int NW = BS / kWave;
+  __shared__ float s_mn[NW], s_mx[NW];
+  __shared__ uint32_t s_nan[NW];
+  __shared__ double s_sa[NW], s_s1[NW], s_s2[NW];
   const int64_t ng = cdiv(n, 4);
   const int64_t nfull = n / 4;
-  const int64_t base = (int64_t)blockIdx.x * kBlock * G;
+  const int64_t base = (int64_t)blockIdx.x * BS * G;
   ObsAcc a;
   obs_init(a);
   f4 v[G];
-  const bool whole = VEC && base + (int64_t)kBlock * G <= nfull;   // block-uniform
+  const bool whole = VEC && base + (int64_t)BS * G <= nfull;   // block-uniform
   if (whole) {
     const float *xb = x + 4 * base;
 #pragma unroll
-    for (int k = 0; k < G; ++k) v[k] = ld4<NT>(xb + 4 * (threadIdx.x + k * kBlock));
+    for (int k = 0; k < G; ++k) v[k] = ld4<NT>(xb + 4 * (threadIdx.x + k * BS));
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      v[k] = act_fwd4_at<ACT>(v[k], 4 * (base + threadIdx.x + k * kBlock), L);
+      v[k] = act_fwd4_at<ACT>(v[k], 4 * (base + threadIdx.x + k * BS), L);
       obs_add4(a, v[k], 4);
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + threadIdx.x + k * kBlock, ng, n);
+    for (int k = 0; k < G; ++k) v[k] = load_group_c<VEC, NT>(x, base + threadIdx.x + k * BS, ng, n);
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      const int64_t i = base + threadIdx.x + k * kBlock;
+      const int64_t i = base + threadIdx.x + k * BS;
       v[k] = act_fwd4_at<ACT>(v[k], 4 * i, L);
       if (i < nfull) obs_add4(a, v[k], 4);
       else if (i < ng) obs_add4(a, v[k], valid_in_group(i, n));
@@ -336,17 +337,17 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_out1(const float *__res
   if (whole) {
     float *yb = y + 4 * base;
 #pragma unroll
-    for (int k = 0; k < G; ++k) st4<NT>(yb + 4 * (threadIdx.x + k * kBlock), v[k]);
+    for (int k = 0; k < G; ++k) st4<NT>(yb + 4 * (threadIdx.x + k * BS), v[k]);
   } else {
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-      const int64_t i = base + threadIdx.x + k * kBlock;
+      const int64_t i = base + threadIdx.x + k * BS;
       if (i < ng) store_group<VEC, NT>(y, i, n, v[k]);
     }
   }
   if (threadIdx.x == 0) {   // waves in order: fixed per n
     double f[6] = {s_mn[0], s_mx[0], (double)s_nan[0], s_sa[0], s_s1[0], s_s2[0]};
-    for (int i = 1; i < kWaves; ++i) {
+    for (int i = 1; i < NW; ++i) {
       f[0] = fminf((float)f[0], s_mn[i]); f[1] = fmaxf((float)f[1], s_mx[i]); f[2] += s_nan[i];
       f[3] += s_sa[i]; f[4] += s_s1[i]; f[5] += s_s2[i];
     }
@@ -471,7 +472,8 @@ void launch_observe_fq_small(const float *x, float *y, uint8_t *c, uint64_t *m, 
 // (min / max; a NaN call changes nothing, minmax.py:42-47), so a workgroup that reads
 // the state after workgroup 0 has written it computes the same qparams.
 // ----------------------------------------------------------------------------
-constexpr int kK2oMinGroups = 1;               // K2o one-shot: fewest groups per lane
+constexpr int kK2oGroups = 2;                  // K2o one-shot: groups per lane (default)
+constexpr int kK2oBlock = 256;                 // K2o one-shot: lanes per workgroup (default)
 constexpr int kFoldFqGrid = 32;                 // K2p workgroups: <= 128 records per fold
 constexpr int kFoldFqU = 4;                     // K2p groups per lane per step
 constexpr int64_t kFoldFqMax = (int64_t)1 << 18;   // largest n (fq grid <= 128 workgroups)
@@ -889,10 +891,22 @@ __global__ __launch_bounds__(kBlock) void k_observe_fold_parts(const double *__r
   const int64_t nrec = (dg >= 1.0 && dg <= (double)maxrec) ? (int64_t)dg : 0;
   double f[6];
   ObsFold::init(f);
-  for (int64_t i = threadIdx.x; i < nrec; i += kBlock) {
-    const double *r = P + i * VSIQ_PART_LEN;
-    const double rr[6] = {r[0], r[1], r[2], r[3], r[4], r[5]};
-    ObsFold::add(f, rr);
+  // thread t folds records t, t + 256, t + 512, ... in that order; kFoldU of them are loaded
+  // at once (a one-shot K2o call has up to n / 2048 records: one load round trip per
+  // record would make the sync latency-bound)
+  constexpr int kFoldU = 8;
+  for (int64_t i0 = threadIdx.x; i0 < nrec; i0 += (int64_t)kBlock * kFoldU) {
+    double rr[kFoldU][6];
+#pragma unroll
+    for (int u = 0; u < kFoldU; ++u) {
+      const int64_t i = i0 + (int64_t)u * kBlock;
+      const double *r = P + (i < nrec ? i : nrec - 1) * VSIQ_PART_LEN;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) rr[u][k] = r[k];
+    }
+#pragma unroll
+    for (int u = 0; u < kFoldU; ++u)
+      if (i0 + (int64_t)u * kBlock < nrec) ObsFold::add(f, rr[u]);
   }
   ObsFold::wave(f);
   __shared__ double s[kWaves][6];
@@ -1177,26 +1191,27 @@ int device_cus() {
 
 using namespace vsiq;
 
-// K2o one-shot groups per lane: the smallest G whose grid fits VSIQ_PART_MAX_RECORDS
-// workgroups (one record each); fixed per n (and the k2o_groups knob): deterministic
-inline int k2o_groups(int64_t n) {
+// K2o one-shot shape: G groups per lane (k2o_groups knob, default 2) and BS lanes per
+// workgroup (k2o_block knob, default kK2oBlock); fixed per n and knobs: deterministic
+inline int k2o_groups() {
   const int t = g_tune.k2o_groups;
-  if (t) return t;
-  const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
-  for (int g = kK2oMinGroups; g < 16; g *= 2)
-    if (cdiv(units, g) <= VSIQ_PART_MAX_RECORDS) return g;
-  return 16;
+  return t ? t : kK2oGroups;
+}
+
+inline int k2o_block() {
+  const int t = g_tune.k2o_block;
+  return t ? t : kK2oBlock;
 }
 
 inline int64_t k2o_records(int64_t n) {
   if (g_tune.k2o_form == 1) return observe_part_grid(n) * kWaves;
-  return cdiv(cdiv(cdiv(n, 4), (int64_t)kBlock), k2o_groups(n));
+  return cdiv(cdiv(n, 4), (int64_t)k2o_block() * k2o_groups());
 }
 
-template <bool VEC, bool NT, int ACT>
-void launch_k2o1(int g, int64_t grid, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
-                 hipStream_t st) {
-#define K2O1(G_) hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, G_>), dim3((unsigned)grid), dim3(kBlock), 0, \
+template <bool VEC, bool NT, int ACT, int BS>
+void launch_k2o1_bs(int g, int64_t grid, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
+                    hipStream_t st) {
+#define K2O1(G_) hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, G_, BS>), dim3((unsigned)grid), dim3(BS), 0, \
                                     st, c, y, n, parts, L)
   switch (g) {
     case 1: K2O1(1); break;
@@ -1208,12 +1223,20 @@ void launch_k2o1(int g, int64_t grid, const float *c, float *y, int64_t n, doubl
 #undef K2O1
 }
 
+template <bool VEC, bool NT, int ACT>
+void launch_k2o1(int g, int bs, int64_t grid, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
+                 hipStream_t st) {
+  if (bs == 1024) launch_k2o1_bs<VEC, NT, ACT, 1024>(g, grid, c, y, n, parts, L, st);
+  else if (bs == 512) launch_k2o1_bs<VEC, NT, ACT, 512>(g, grid, c, y, n, parts, L, st);
+  else launch_k2o1_bs<VEC, NT, ACT, 256>(g, grid, c, y, n, parts, L, st);
+}
+
 template <int ACT>
-void launch_k2o1_act(bool vec, bool nt, int g, int64_t grid, const float *c, float *y, int64_t n, double *parts,
-                     const SiluLay &L, hipStream_t st) {
-  if (vec && nt) launch_k2o1<true, true, ACT>(g, grid, c, y, n, parts, L, st);
-  else if (vec) launch_k2o1<true, false, ACT>(g, grid, c, y, n, parts, L, st);
-  else launch_k2o1<false, false, ACT>(g, grid, c, y, n, parts, L, st);
+void launch_k2o1_act(bool vec, bool nt, int g, int bs, int64_t grid, const float *c, float *y, int64_t n,
+                     double *parts, const SiluLay &L, hipStream_t st) {
+  if (vec && nt) launch_k2o1<true, true, ACT>(g, bs, grid, c, y, n, parts, L, st);
+  else if (vec) launch_k2o1<true, false, ACT>(g, bs, grid, c, y, n, parts, L, st);
+  else launch_k2o1<false, false, ACT>(g, bs, grid, c, y, n, parts, L, st);
 }
 
 extern "C" {
@@ -1290,6 +1313,10 @@ int vsiq_set_tuning(int key, int value) {
       if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16) return VSIQ_E_ARG;
       g_tune.k2o_groups = value;
       return 0;
+    case VSIQ_TUNE_K2O_BLOCK:
+      if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
+      g_tune.k2o_block = value;
+      return 0;
     case VSIQ_TUNE_PC_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.pc_block = value;
@@ -1365,7 +1392,7 @@ int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, 
     const int64_t grid = k2o_records(n);
     if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
     if (parts_len < grid * VSIQ_PART_LEN) return VSIQ_E_WS;
-    VSIQ_ACT(act, launch_k2o1_act, vec, nt, k2o_groups(n), grid, c, y, n, parts, L, st);
+    VSIQ_ACT(act, launch_k2o1_act, vec, nt, k2o_groups(), k2o_block(), grid, c, y, n, parts, L, st);
     return launch_rc();
   }
   const int64_t grid = observe_part_grid(n);

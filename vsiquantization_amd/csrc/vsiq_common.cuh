@@ -72,7 +72,8 @@ struct Tuning {
   std::atomic<int> gate_autotune{1};       // store gate tuned online per launch site (0 = fixed estimate)
   std::atomic<int> xcd_order{1};           // XCD-contiguous block order where neighbours share lines
   std::atomic<int> k2o_form{0};            // K2o: 0 one-shot (one record per workgroup), 1 grid-stride (K2p's records)
-  std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = by size)
+  std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = default 2)
+  std::atomic<int> k2o_block{0};           // K2o one-shot lanes per workgroup 256 / 512 / 1024 (0 = default 256)
   std::atomic<int> obs_temporal_mb{256};   // K2: cached (temporal) loads for tensors under this many MB
 };
 extern Tuning g_tune;
