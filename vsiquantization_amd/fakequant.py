@@ -470,9 +470,10 @@ def observe_fake_quant(x: torch.Tensor, *, symmetric: bool, num_bits: int = 8, e
                                                   H.ptr(w.counter), H.stream_of(dev))
         H.check(rc, "vsiq_act_observe_fq_grid_f32")
         # a workgroup that timed out at the grid barrier wrote NaN and counted itself: fail
-        # loudly (one host sync; K10 is an opt-in measurement path)
+        # loudly (one host sync; K10 is an opt-in measurement path; not checkable while the
+        # stream is being captured into a HIP graph -- the next eager call reports it)
         err = w.counter[H.COUNTER_GRID_ERRORS:H.COUNTER_GRID_ERRORS + 1]
-        if int(err.item()):
+        if not torch.cuda.is_current_stream_capturing() and int(err.item()):
             err.zero_()
             raise H.VsiqError("vsiq_act_observe_fq_grid_f32: grid barrier timed out (the grid was not "
                               "co-resident); the outputs of the timed-out workgroups are NaN")
