@@ -1086,7 +1086,9 @@ class _PhaseMark:
             cap.graphs.append(cap.cur)
         if not self.last:
             cap.cur = torch.cuda.CUDAGraph()
-            cap.ctx = torch.cuda.graph(cap.cur, stream=cap.stream)
+            # thread_local: torch's NCCL watchdog thread keeps polling earlier collectives'
+            # events during the capture (global mode makes that a capture error -> abort)
+            cap.ctx = torch.cuda.graph(cap.cur, stream=cap.stream, capture_error_mode="thread_local")
             cap.ctx.__enter__()
 
 

@@ -70,7 +70,10 @@ class GraphedStep:
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
         before = set(H._WS)
-        with torch.cuda.graph(self.graph):
+        # thread_local: other threads of the process (torch's NCCL watchdog polling the events
+        # of earlier collectives, autograd's device threads) may keep calling the runtime
+        # while this thread captures; "global" mode turns those calls into capture errors
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self._cids = [H._capture_id(H.stream_of(torch.cuda.current_device()))]
             out = fn()
         # keep the outputs' storage (every replay rewrites it), not their autograd graph:
