@@ -170,6 +170,20 @@ std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool
   return {y, scale, zp, rs};
 }
 
+// The per-channel observe + fake quant bound to one observer state and quantizer range:
+// the public-API C2 step calls it with the tensor alone (one pybind argument instead of
+// nine, a 3-tuple back instead of a 4-element list: host time per call).
+struct PcObserveFqOp {
+  Tensor run_min, run_max;
+  bool sym;
+  int64_t qmin, qmax;
+  double qden, eps;
+  std::tuple<Tensor, Tensor, Tensor> call(const Tensor &x) const {
+    auto r = pc_observe_fq(x, run_min, run_max, sym, qmin, qmax, qden, eps, false);
+    return {r[0], r[1], r[2]};
+  }
+};
+
 // --------------------------------------------------------------------------- K1/K5 + STE
 struct FqFixedBackward : public Node {
   Tensor mask, sb;      // internal mask; scale for the backward (record entry / device copy)
@@ -588,6 +602,10 @@ PYBIND11_MODULE(_vsiq_torch, m) {
   m.doc() = "C++ autograd nodes over the vsiq C ABI (K3/K1/K5 forwards, STE/K4 backwards)";
   m.def("abi_version", []() { return vsiq_abi_version(); });
   m.def("pc_observe_fq", &pc_observe_fq, "K3 per-channel observe + fake quant; STE backward");
+  pybind11::class_<PcObserveFqOp>(m, "PcObserveFqOp")
+      .def(pybind11::init([](Tensor run_min, Tensor run_max, bool sym, int64_t qmin, int64_t qmax, double qden,
+                             double eps) { return PcObserveFqOp{run_min, run_max, sym, qmin, qmax, qden, eps}; }))
+      .def("__call__", &PcObserveFqOp::call, "(y, scale, zp) of pc_observe_fq(x) with the bound state / range");
   m.def("fq_fixed", &fq_fixed, "K1/K5 fake quant with fixed qparams; STE backward");
   m.def("fq_learn", &fq_learn, "K1/K5 learnable fake quant; K4 backward", pybind11::arg("x"), pybind11::arg("scale"),
         pybind11::arg("scale_host"), pybind11::arg("zp"), pybind11::arg("zp_host"), pybind11::arg("qmin"),

@@ -79,19 +79,19 @@ class PerChannelMinMaxObserver(BaseObserver):
         """Fused observe + fake quant of ``x`` with ``quantizer``'s integer range (one pass).
 
         Returns (y, row_stats | None); y carries the STE gradient."""
-        if (H.torch_ext_enabled() and isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32
-                and x.requires_grad and x.is_contiguous() and torch.is_grad_enabled()):
-            # the training step's call (public-API C2 step): straight to the C++ node
+        if (not want_row_stats and H.torch_ext_enabled() and isinstance(x, torch.Tensor) and x.is_cuda
+                and x.dtype == torch.float32 and x.requires_grad and x.is_contiguous() and torch.is_grad_enabled()):
+            # the training step's call (public-API C2 step): straight to a C++ op bound to
+            # this observer's state and the quantizer's range (rebuilt when either changes)
             mn, mx = self._state(x)
-            qd = self.__dict__.get("_qden")
-            if qd is None or qd[0] != (self.symmetric, self.num_bits, self.eps):
-                qd = self._qden = ((self.symmetric, self.num_bits, self.eps),
-                                   qden(self.symmetric, self.num_bits, self.eps))
-            y, s, z, rs = H.torch_ext().pc_observe_fq(x, mn, mx, bool(self.symmetric), int(quantizer.qmin),
-                                                      int(quantizer.qmax), qd[1], float(self.eps),
-                                                      bool(want_row_stats))
-            self.scale, self.zero_point = s, z
-            return y, (rs if want_row_stats else None)
+            key = (mn, self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax)
+            op = self.__dict__.get("_op")
+            if op is None or op[0][0] is not mn or op[0][1:] != key[1:]:
+                op = self._op = (key, H.torch_ext().PcObserveFqOp(
+                    mn, mx, bool(self.symmetric), int(quantizer.qmin), int(quantizer.qmax),
+                    qden(self.symmetric, self.num_bits, self.eps), float(self.eps)))
+            y, self.scale, self.zero_point = op[1](x)
+            return y, None
         if _host.is_host(x):
             mn, mx = self._state(x)
             args = (self.symmetric, quantizer.qmin, quantizer.qmax, self.num_bits, self.eps, mn, mx)
