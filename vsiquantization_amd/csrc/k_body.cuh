@@ -51,8 +51,24 @@ struct LsqAcc {
   double t, z;   // sum [g(q-z) + -(gm)(x/s/s)] ; sum [gm + -(g s)]
 };
 
+// grad_x's division RN(RN(g*s)/s) in one Markstein step from g (the STE backward's
+// quotient, vsiq_common.cuh ste_quot: g is a faithful quotient of RN(g*s)/s) -- for s in
+// (2^-60, 2^60), positive (ste_fast_s, uniform), and g inside ste_ok; 4 instead of ~8
+// instructions per element.  Bitwise RN(gm/s) there (vsiq_selftest_fq mode 1 proves the
+// quotient over all 2^32 gradients).
+__device__ __forceinline__ uint32_t ste_fast_s(const FastDiv &d) {
+  return (__float_as_uint(d.b) - 0x21800000u) <= (0x5d800000u - 0x21800000u) ? 1u : 0u;
+}
+
+__device__ __forceinline__ float ste_quot_d(float g, const FastDiv &d) {
+  const float p = g * d.b;
+  const float e = __builtin_fmaf(-g, d.b, p);
+  return __builtin_copysignf(__builtin_fmaf(e, d.r, g), p);
+}
+
 // one element of the learnable backward; returns grad_x, adds the f64 gradient terms
-template <bool ZPL, bool IEEE>
+// (STEQ: grad_x by ste_quot_d -- the caller checked ste_fast_s and ste_ok(g))
+template <bool ZPL, bool IEEE, bool STEQ = false>
 __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
   const float u = fdiv_t<IEEE>(x, p.d);
   const float r = __builtin_rintf(u + p.z);
@@ -70,14 +86,18 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
     acc.t += (double)t1 + (double)t2;
     if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
   }
+  if (STEQ) return m ? ste_quot_d(g, p.d) : 0.0f * p.d.r;   // DivBackward0 (self); 0/s signed like IEEE
   return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
 }
 
-// all three divisions of an element inside the fast-division range?
+// all three divisions of an element inside the fast-division range?  (STEQ: grad_x's by
+// the one-step STE quotient, valid for g inside ste_ok; the scale's range is the caller's)
+template <bool STEQ = false>
 __device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
   const float u = fdiv_fast(x, p.d);
   const float r = __builtin_rintf(u + p.z);
   const bool m = (r >= p.lo && r <= p.hi);
+  if (STEQ) return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & (m ? ste_ok(g) : 1u);
   const float gm = m ? g * p.s : 0.0f;
   return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
 }
@@ -112,9 +132,21 @@ __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4
                                             LsqAcc &c, const SiluLay &L = SiluLay{}) {
   const f4 xv = act_fwd4_at<ACT>(xc, 4 * i, L);
   const int nv = i < ng ? valid_in_group(i, n) : 0;
+  f4 o;
+#ifndef VSIQ_EXP_K4_STEQ
+#define VSIQ_EXP_K4_STEQ 1   // experiments: 0 = grad_x by the general fast division (round 3)
+#endif
+  if (VSIQ_EXP_K4_STEQ && ste_fast_s(p.d) &&
+      (lsq_fast_ok<true>(xv.x, gv.x, p) & lsq_fast_ok<true>(xv.y, gv.y, p) & lsq_fast_ok<true>(xv.z, gv.z, p) &
+       lsq_fast_ok<true>(xv.w, gv.w, p))) {
+    o.x = lsq_elem<ZPL, false, true>(xv.x, gv.x, p, c, nv > 0);
+    o.y = lsq_elem<ZPL, false, true>(xv.y, gv.y, p, c, nv > 1);
+    o.z = lsq_elem<ZPL, false, true>(xv.z, gv.z, p, c, nv > 2);
+    o.w = lsq_elem<ZPL, false, true>(xv.w, gv.w, p, c, nv > 3);
+    return act_bwd4_at<ACT>(o, xc, 4 * i, L);
+  }
   const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
                   lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p));
-  f4 o;
   if (ok) {
     o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
     o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);
