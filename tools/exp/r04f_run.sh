@@ -2,7 +2,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_torch_ext.py tests/test_gpu_parity.py tests/test_gpu_graph.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_r04f.log 2>&1 || { echo "tests rc=$?"; tail -40 gpurun_out/t_r04f.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_r04f.log 2>&1 || { echo "tests rc=$?"; tail -40 gpurun_out/t_r04f.log; exit 1; }
 tail -2 gpurun_out/t_r04f.log
 timeout -k 10 300 python3 -u tools/exp/api_timings.py > gpurun_out/api_timings.log 2>&1 || { echo "api rc=$?"; tail gpurun_out/api_timings.log; exit 1; }
 cat gpurun_out/api_timings.log
