@@ -29,7 +29,9 @@ def main():
     ex = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "c4_floor.so"))
     ex.exp_add2.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int, P]
     st = H.stream_of(dev)
-    scale = torch.tensor(0.03, dtype=torch.float64, device=dev)
+    # C4's activation scale (bench.C4Backbone: 2 * 0.8 / sqrt(qmax), a4): most elements in range
+    # (SCALE=0.03: most clamped -- the element math then costs more, profiles/r04f_k4_variants.txt)
+    scale = torch.tensor(float(os.environ.get("SCALE", 2 * 0.8 / 7 ** 0.5)), dtype=torch.float64, device=dev)
     sizes = sorted({256 * co * h * h for _, co, _, _, h in bench.yolov8n_backbone()})
     print("C4 act sizes (batch 256), R launches back to back, buffers rotated past the MALL")
     for n in sizes:
@@ -67,11 +69,22 @@ def main():
             return sorted(out)[1]
 
         row = {"K4d": t(k4d)}
+        k4d(0)
+        gx2, s2 = ys[0].clone(), rec.view(-1, 2).sum(0)
+        H.set_tuning(H.TUNE_LSQ_PART_G1_BELOW, 1 << 10)   # K4d at 1 group per lane
+        nrec1 = int(lib.vsiq_lsq_part_records(H.c_i64(n)))
+        rec = torch.empty(2 * nrec1, dtype=torch.float64, device=dev)
+        row["K4d G=1"] = t(k4d)
+        k4d(0)
+        s1 = rec.view(-1, 2).sum(0)
+        assert torch.equal(ys[0], gx2) and torch.allclose(s1, s2, rtol=1e-12, atol=0), (s1, s2)
+        H.set_tuning(H.TUNE_LSQ_PART_G1_BELOW, 0)
+        rec = torch.empty(2 * nrec, dtype=torch.float64, device=dev)
         for G in (1, 2, 4, 8):
             row[f"2:1 G={G}"] = t(plain(G))
-        best = min(v for k, v in row.items() if k != "K4d")
+        best = min(v for k, v in row.items() if not k.startswith("K4d"))
         cells = "  ".join(f"{k} {v:8.2f} us {12 * n / v / 1e3:6.0f} GB/s" for k, v in row.items())
-        print(f"n={n:10d} {cells}  K4d/best-plain {best / row['K4d']:.3f} (frac K4d {12 * n / row['K4d'] / 8e6:.3f})",
+        print(f"n={n:10d} {cells}  K4d/best-plain {best / row['K4d']:.3f} G=1 {best / row['K4d G=1']:.3f} (frac K4d {12 * n / row['K4d'] / 8e6:.3f})",
               flush=True)
         del gs, xs, ys
         torch.cuda.empty_cache()

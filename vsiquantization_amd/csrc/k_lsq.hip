@@ -71,22 +71,27 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
 // -> 105M elements: 9.9 / 16.2 / 28.0 / 51.7 / 101.0 / 205.3 us at 2 per lane against
 // 11.1 / 16.6 / 28.4 / 54.2 / 103.2 / 207.9 us at K4's 4 / 8, profiles/r03g_c4_groups.txt);
 // the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
-inline int lsq_part_groups_per_lane() {
+// Tensors under lsq_part_g1_below MiB-elements (knob, default 0 = never) run 1 group per
+// lane: twice the workgroups for the small C4 layers, whose grids are one round.
+inline int lsq_part_groups_per_lane(int64_t n) {
   const int g = g_tune.lsq_groups;
-  return g > 0 ? g : 2;
+  if (g > 0) return g;
+  return n < ((int64_t)g_tune.lsq_part_g1_below << 20) ? 1 : 2;
 }
 
 template <int ACT, bool VEC, bool NT>
 void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const QPSrc &src, int zpl,
                     double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                     const SiluLay &L, hipStream_t st) {
-  const int per_lane = counter ? lsq_groups_per_lane(cdiv(n, 4)) : lsq_part_groups_per_lane();
+  const int per_lane = counter ? lsq_groups_per_lane(cdiv(n, 4)) : lsq_part_groups_per_lane(n);
   if (per_lane == kLsqGroups)
     launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 8)
     launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 4)
     launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
+  else if (per_lane == 1 && !counter)   // records-only small tensors (lsq_part_g1_below)
+    launch_lsq_g<ACT, VEC, NT, 1>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else
     launch_lsq_g<ACT, VEC, NT, 2>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
 }
@@ -127,7 +132,7 @@ int lsq_bwd_part(const float *g, const float *x, float *gx, int64_t n, int act, 
   if (n <= 0 || !g || !x || !gx || !records || qmin > qmax || !act_ok(act))
     return VSIQ_E_ARG;
   const bool vec = (n % 4 == 0) && aligned16(g) && aligned16(x) && aligned16(gx);
-  const int64_t grid = lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane());
+  const int64_t grid = lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane(n));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (records_len < 2 * grid) return VSIQ_E_WS;
   if (zp_learn < 0 || zp_learn > 1) return VSIQ_E_ARG;   // the deferred fold knows modes 0 / 1 only
@@ -634,7 +639,7 @@ int vsiq_act_lsq_bwd_f32(const float *g, const float *c, float *gc, int64_t n, i
 
 int64_t vsiq_lsq_part_records(int64_t n) {
   if (n <= 0) return VSIQ_E_ARG;
-  return lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane());
+  return lsq_grid(cdiv(n, 4), lsq_part_groups_per_lane(n));
 }
 
 int vsiq_act_lsq_bwd_part_f32(const float *g, const float *c, float *gc, int64_t n, int act,
