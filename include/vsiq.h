@@ -107,8 +107,6 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
                                           1: grid-stride, vsiq_act_observe_part_f32's records */
 #define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = default (2) */
 #define VSIQ_TUNE_K2O_BLOCK 17         /* K2o one-shot lanes per workgroup 256/512/1024, 0 = default */
-#define VSIQ_TUNE_LSQ_PART_G1_BELOW 18 /* records-only K4 (K4d): 1 group per lane for tensors under
-                                          N Mi elements (default 0: always 2) */
 #define VSIQ_TUNE_OBS_TEMPORAL_MB 16   /* K2 (per-call observer): cached loads for tensors under N MB
                                           (the fake quant re-reading it may hit the 256 MB
                                           Infinity Cache); default 256, 0 = nontemporal always */

@@ -69,22 +69,11 @@ def main():
             return sorted(out)[1]
 
         row = {"K4d": t(k4d)}
-        k4d(0)
-        gx2, s2 = ys[0].clone(), rec.view(-1, 2).sum(0)
-        H.set_tuning(H.TUNE_LSQ_PART_G1_BELOW, 1 << 10)   # K4d at 1 group per lane
-        nrec1 = int(lib.vsiq_lsq_part_records(H.c_i64(n)))
-        rec = torch.empty(2 * nrec1, dtype=torch.float64, device=dev)
-        row["K4d G=1"] = t(k4d)
-        k4d(0)
-        s1 = rec.view(-1, 2).sum(0)
-        assert torch.equal(ys[0], gx2) and torch.allclose(s1, s2, rtol=1e-12, atol=0), (s1, s2)
-        H.set_tuning(H.TUNE_LSQ_PART_G1_BELOW, 0)
-        rec = torch.empty(2 * nrec, dtype=torch.float64, device=dev)
         for G in (1, 2, 4, 8):
             row[f"2:1 G={G}"] = t(plain(G))
         best = min(v for k, v in row.items() if not k.startswith("K4d"))
         cells = "  ".join(f"{k} {v:8.2f} us {12 * n / v / 1e3:6.0f} GB/s" for k, v in row.items())
-        print(f"n={n:10d} {cells}  K4d/best-plain {best / row['K4d']:.3f} G=1 {best / row['K4d G=1']:.3f} (frac K4d {12 * n / row['K4d'] / 8e6:.3f})",
+        print(f"n={n:10d} {cells}  K4d/best-plain {best / row['K4d']:.3f} (frac K4d {12 * n / row['K4d'] / 8e6:.3f})",
               flush=True)
         del gs, xs, ys
         torch.cuda.empty_cache()

@@ -42,7 +42,6 @@ TUNE_STORE_GATE = 11
 TUNE_GATE_AUTOTUNE = 12
 TUNE_XCD_ORDER = 13
 TUNE_K2O_FORM, TUNE_K2O_GROUPS, TUNE_OBS_TEMPORAL_MB, TUNE_K2O_BLOCK = 14, 15, 16, 17
-TUNE_LSQ_PART_G1_BELOW = 18
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 

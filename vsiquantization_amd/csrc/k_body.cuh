@@ -82,11 +82,27 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
 #ifndef VSIQ_EXP_K4
 #define VSIQ_EXP_K4 0
 #endif
-  if ((VSIQ_EXP_K4 & 1) == 0 && valid) {
-    acc.t += (double)t1 + (double)t2;
-    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
+  // lanes past the tensor's end (valid false) add +0 terms: selects, not exec branches
+  // (acc starts at +0.0, so adding +0.0 never changes its bits)
+#ifndef VSIQ_EXP_K4_SEL
+#define VSIQ_EXP_K4_SEL 1   // experiments: 0 = exec branches on valid / m (round 3)
+#endif
+  if (!VSIQ_EXP_K4_SEL) {
+    if ((VSIQ_EXP_K4 & 1) == 0 && valid) {
+      acc.t += (double)t1 + (double)t2;
+      if (ZPL) acc.z += (double)gm + (double)(-gq);
+    }
+    if (STEQ) return m ? ste_quot_d(g, p.d) : 0.0f * p.d.r;
+    return fdiv_t<IEEE>(gm, p.d);
   }
-  if (STEQ) return m ? ste_quot_d(g, p.d) : 0.0f * p.d.r;   // DivBackward0 (self); 0/s signed like IEEE
+  if ((VSIQ_EXP_K4 & 1) == 0) {
+    acc.t += valid ? (double)t1 + (double)t2 : 0.0;
+    if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;   // AddBackward0 + SubBackward0 (other)
+  }
+  if (STEQ) {   // DivBackward0 (self); 0/s signed like IEEE.  Both sides computed, then selected
+    const float qd = ste_quot_d(g, p.d);
+    return m ? qd : 0.0f * p.d.r;
+  }
   return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
 }
 
@@ -205,8 +221,9 @@ __device__ __forceinline__ void lsq_store_block(float *__restrict__ gx, int64_t 
 
 // Block sum of the K4 terms with the waves split (wave_arrive): DPP wave sums -> LDS;
 // waves 1..3 store their grad_x and return false; wave 0 passes an LDS-only barrier
-// and gets the block record {sum t, sum z} (fixed order) in every lane.
-template <bool VEC, bool NT, int G>
+// and gets the block record {sum t, sum z} (fixed order) in every lane.  STORE false:
+// the caller stored every wave's grad_x already (records-only K4d).
+template <bool VEC, bool NT, int G, bool STORE = true>
 __device__ __forceinline__ bool lsq_block_record(LsqAcc c, float *__restrict__ gx, int64_t n, int64_t blk,
                                                  const f4 (&o)[G], double (&rec)[2]) {
   __shared__ double s[kWaves][2];
@@ -214,7 +231,7 @@ __device__ __forceinline__ bool lsq_block_record(LsqAcc c, float *__restrict__ g
   c.z = wave_reduce(c.z, AddD());
   const int w = threadIdx.x / kWave;
   if (threadIdx.x % kWave == 0) { s[w][0] = c.t; s[w][1] = c.z; }
-  if (w != 0) lsq_store_block<VEC, NT, G>(gx, n, blk, o);
+  if (STORE && w != 0) lsq_store_block<VEC, NT, G>(gx, n, blk, o);
   lds_barrier();
   if (w != 0) return false;
   rec[0] = s[0][0]; rec[1] = s[0][1];

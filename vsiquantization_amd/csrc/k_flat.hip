@@ -1277,10 +1277,6 @@ int vsiq_set_tuning(int key, int value) {
       if (value != 0 && (value < 1 || value > kMaxReduceGrid)) return VSIQ_E_ARG;
       g_tune.obs_grid = value;
       return 0;
-    case VSIQ_TUNE_LSQ_PART_G1_BELOW:
-      if (value < 0 || value > 1 << 20) return VSIQ_E_ARG;
-      g_tune.lsq_part_g1_below = value;
-      return 0;
     case VSIQ_TUNE_LSQ_GROUPS:
       if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16) return VSIQ_E_ARG;
       g_tune.lsq_groups = value;

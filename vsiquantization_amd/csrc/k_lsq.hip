@@ -19,6 +19,22 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   LsqAcc c{0.0, 0.0};
   f4 o[G];
   lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o, L);
+#ifndef VSIQ_EXP_K4D_STORE_FIRST
+#define VSIQ_EXP_K4D_STORE_FIRST 1   // experiments: 0 = PART stores after the block record (round 3)
+#endif
+  if (PART && VSIQ_EXP_K4D_STORE_FIRST) {
+    // no arrival to order against: every wave issues its grad_x stores first, so the
+    // block reduction runs while they drain (the one-round grids of small layers end
+    // with it otherwise on the critical path)
+    lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
+    double rec[2];
+    if (!lsq_block_record<VEC, NT, G, false>(c, gx, n, blockIdx.x, o, rec)) return;
+    if (threadIdx.x == 0) {
+      ws[2 * (int64_t)blockIdx.x] = rec[0];
+      ws[2 * (int64_t)blockIdx.x + 1] = rec[1];
+    }
+    return;
+  }
   double rec[2], f[2];
   if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
   if (PART) {
@@ -71,12 +87,11 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
 // -> 105M elements: 9.9 / 16.2 / 28.0 / 51.7 / 101.0 / 205.3 us at 2 per lane against
 // 11.1 / 16.6 / 28.4 / 54.2 / 103.2 / 207.9 us at K4's 4 / 8, profiles/r03g_c4_groups.txt);
 // the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
-// Tensors under lsq_part_g1_below MiB-elements (knob, default 0 = never) run 1 group per
-// lane: twice the workgroups for the small C4 layers, whose grids are one round.
-inline int lsq_part_groups_per_lane(int64_t n) {
+// (1 group per lane for the small layers measured slower still: 10.4 against 9.8 us at
+// 3.3M elements, 214 against 201 us at 105M, profiles/r04h_c4_k4d.txt.)
+inline int lsq_part_groups_per_lane(int64_t) {
   const int g = g_tune.lsq_groups;
-  if (g > 0) return g;
-  return n < ((int64_t)g_tune.lsq_part_g1_below << 20) ? 1 : 2;
+  return g > 0 ? g : 2;
 }
 
 template <int ACT, bool VEC, bool NT>
@@ -90,8 +105,6 @@ void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const 
     launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 4)
     launch_lsq_g<ACT, VEC, NT, 4>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
-  else if (per_lane == 1 && !counter)   // records-only small tensors (lsq_part_g1_below)
-    launch_lsq_g<ACT, VEC, NT, 1>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else
     launch_lsq_g<ACT, VEC, NT, 2>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
 }

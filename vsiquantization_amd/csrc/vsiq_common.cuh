@@ -74,7 +74,6 @@ struct Tuning {
   std::atomic<int> k2o_form{0};            // K2o: 0 one-shot (one record per workgroup), 1 grid-stride (K2p's records)
   std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = default 2)
   std::atomic<int> k2o_block{0};           // K2o one-shot lanes per workgroup 256 / 512 / 1024 (0 = default 256)
-  std::atomic<int> lsq_part_g1_below{0};    // K4d: 1 group per lane below this many Mi elements
   std::atomic<int> obs_temporal_mb{256};   // K2: cached (temporal) loads for tensors under this many MB
 };
 extern Tuning g_tune;
