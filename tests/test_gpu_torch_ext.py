@@ -55,6 +55,46 @@ def test_pc_observe_quantize_ext_equals_python(shape, sym, monkeypatch):
         assert torch.equal(_bits(u), _bits(v))
 
 
+def test_pc_observe_quantize_bound_op_and_its_fallbacks(monkeypatch):
+    """The public-API step's bound C++ op (PcObserveFqOp: its own eligibility checks, one
+    allocation for scale / zp / mask): a sequence of calls that takes it, then calls it
+    must hand back (no grad mode, x without grad, a non-contiguous x, another row count),
+    gives the same y / grad / scale / zp / running state bits as the Python Functions,
+    and every call's scale / zp are new tensors (an earlier call's values stay as they were)."""
+    g0 = torch.Generator(device=DEV).manual_seed(3)
+    ws = [torch.randn(64, 16, 3, 3, device=DEV, generator=g0) * s for s in (0.05, 0.2, 0.01)]
+    w_other = torch.randn(32, 16, 3, 3, device=DEV, generator=g0) * 0.1
+    g = torch.randn(64, 16, 3, 3, device=DEV, generator=g0)
+
+    def run():
+        obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
+        out, kept = [], []
+        for i, w in enumerate(ws * 2):
+            x = w.clone().requires_grad_(True)
+            y, _ = obs.observe_quantize(x, q)
+            y.backward(g)
+            out += [y, x.grad, obs.scale, obs.zero_point, obs.run_min, obs.run_max]
+            kept.append((obs.scale, obs.scale.clone(), obs.zero_point, obs.zero_point.clone()))
+        with torch.no_grad():
+            out += list(obs.observe_quantize(ws[0].clone().requires_grad_(True), q)[:1])
+        out += list(obs.observe_quantize(ws[1], q)[:1])
+        xt = ws[2].transpose(2, 3).requires_grad_(True)    # non-contiguous
+        y, _ = obs.observe_quantize(xt, q)
+        y.backward(g)
+        out += [y, xt.grad, obs.scale]
+        xo = w_other.clone().requires_grad_(True)   # another row count: the state restarts
+        y, _ = obs.observe_quantize(xo, q)
+        out += [y, obs.scale, obs.run_min]
+        for s, s0, z, z0 in kept:
+            assert torch.equal(_bits(s), _bits(s0)) and torch.equal(_bits(z), _bits(z0))
+        return out
+
+    a, b = both(run, monkeypatch)
+    assert len(a) == len(b)
+    for u, v in zip(a, b):
+        assert u.shape == v.shape and torch.equal(_bits(u), _bits(v))
+
+
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("kind", ["float", "cuda", "cpu", "qp"])
 def test_fixed_ext_equals_python(kind, act, monkeypatch):

@@ -31,7 +31,7 @@ def main():
     g = torch.randn(shape, device=dev)
     obs, q = V.PerChannelMinMaxObserver(False), V.PerChannelUniformQuantizer(8, False)
     obs.observe_quantize(x, q)
-    op = obs._op[1]
+    op = obs._op[2]
 
     def ours_step():
         x.grad = None

@@ -1,0 +1,8 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+timeout -k 10 300 python3 -u tools/exp/launch_host.py > gpurun_out/launch_host.log 2>&1 || { echo "rc=$?"; tail gpurun_out/launch_host.log; exit 1; }
+cat gpurun_out/launch_host.log
+timeout -k 10 300 python3 -u tools/exp/api_host.py > gpurun_out/api_host_m.log 2>&1 || { echo "rc=$?"; tail gpurun_out/api_host_m.log; exit 1; }
+cat gpurun_out/api_host_m.log

@@ -31,6 +31,7 @@
 #include <torch/csrc/autograd/functions/utils.h>
 #include <torch/csrc/autograd/saved_variable.h>
 #include <c10/hip/HIPStream.h>
+#include <ATen/hip/EmptyTensor.h>
 
 #include <list>
 #include <map>
@@ -132,7 +133,7 @@ struct PcObserveFqBackward : public Node {
     TORCH_CHECK(mask.defined(), "PcObserveFqBackward: backward through the graph a second time");
     if (!grads[0].defined()) return {Tensor()};
     const Tensor g = grads[0].contiguous();
-    Tensor gx = at::empty_like(g);
+    Tensor gx = at::detail::empty_cuda(g.sizes(), at::kFloat, g.device(), std::nullopt);
     const int64_t C = scale.numel();   // one scale per row
     const int64_t rowlen = C > 0 ? g.numel() / C : 0;
     check(vsiq_ste_bwd_f32(ptr<float>(g), ptr<uint64_t>(mask), ptr<float>(gx), g.numel(), ptr<double>(scale), rowlen,
@@ -170,17 +171,52 @@ std::vector<Tensor> pc_observe_fq(Tensor x, Tensor run_min, Tensor run_max, bool
   return {y, scale, zp, rs};
 }
 
+// A 1-D typed alias of part of `buf`'s storage, built without the dispatcher (the way
+// at::alias makes its TensorImpl): for internal buffers with no autograd history.
+Tensor part_of(const Tensor &buf, at::ScalarType dt, int64_t offset, int64_t n) {
+  auto impl = c10::make_intrusive<c10::TensorImpl>(c10::TensorImpl::VIEW, c10::Storage(buf.storage()), buf.key_set(),
+                                                   c10::scalarTypeToTypeMeta(dt));
+  impl->set_sizes_contiguous({n});
+  impl->set_storage_offset(offset);
+  return Tensor(std::move(impl));
+}
+
 // The per-channel observe + fake quant bound to one observer state and quantizer range:
-// the public-API C2 step calls it with the tensor alone (one pybind argument instead of
-// nine, a 3-tuple back instead of a 4-element list: host time per call).
+// the public-API C2 step calls it with the tensor alone.  Host time per call is the
+// point (the step's kernels are ~13 us each way, torch's own trivial step is the bar):
+// the eligibility checks run here instead of in Python (None back when x is not a
+// contiguous grad-requiring CUDA f32 tensor of this state's rows under grad mode, and the
+// caller takes the general path), y comes from the allocator without the dispatcher, and
+// scale, zp and the STE mask share ONE allocation (aliases made without the dispatcher).
+// The mask's bytes then live as long as the returned scale / zp (~1/32 of x).
 struct PcObserveFqOp {
   Tensor run_min, run_max;
   bool sym;
   int64_t qmin, qmax;
   double qden, eps;
-  std::tuple<Tensor, Tensor, Tensor> call(const Tensor &x) const {
-    auto r = pc_observe_fq(x, run_min, run_max, sym, qmin, qmax, qden, eps, false);
-    return {r[0], r[1], r[2]};
+  pybind11::object call(pybind11::handle h) const {
+    if (!THPVariable_Check(h.ptr())) return pybind11::none();
+    const Tensor &x = THPVariable_Unpack(h.ptr());
+    if (!x.is_cuda() || x.scalar_type() != at::kFloat || !x.requires_grad() || !at::GradMode::is_enabled() ||
+        x.dim() == 0 || !x.is_contiguous() || x.size(0) != run_min.numel() || x.device() != run_min.device())
+      return pybind11::none();
+    const int64_t C = x.size(0);
+    const int64_t rowlen = x.numel() / std::max<int64_t>(C, 1);
+    const int64_t words = std::max<int64_t>(vsiq_mask_words(C, rowlen), 1);
+    Tensor y = at::detail::empty_cuda(x.sizes(), at::kFloat, x.device(), std::nullopt);
+    Tensor buf = at::detail::empty_cuda({2 * C + words}, at::kDouble, x.device(), std::nullopt);
+    Tensor scale = part_of(buf, at::kDouble, 0, C), zp = part_of(buf, at::kDouble, C, C);
+    Tensor mask = part_of(buf, at::kLong, 2 * C, words);
+    check(vsiq_pc_observe_fq_f32(ptr<float>(x), ptr<float>(y), nullptr, ptr<uint64_t>(mask), C, rowlen,
+                                 ptr<float>(run_min), ptr<float>(run_max), ptr<double>(scale), ptr<double>(zp),
+                                 nullptr, sym ? 1 : 0, (int)qmin, (int)qmax, qden, eps, stream_of(x)),
+          "vsiq_pc_observe_fq_f32");
+    auto node = std::shared_ptr<PcObserveFqBackward>(new PcObserveFqBackward(), torch::autograd::deleteNode);
+    node->set_next_edges(torch::autograd::collect_next_edges(x));
+    node->mask = mask;
+    node->scale = scale;
+    torch::autograd::set_history(y, node);
+    return pybind11::make_tuple(std::move(y), std::move(scale), std::move(zp));
   }
 };
 
@@ -605,7 +641,9 @@ PYBIND11_MODULE(_vsiq_torch, m) {
   pybind11::class_<PcObserveFqOp>(m, "PcObserveFqOp")
       .def(pybind11::init([](Tensor run_min, Tensor run_max, bool sym, int64_t qmin, int64_t qmax, double qden,
                              double eps) { return PcObserveFqOp{run_min, run_max, sym, qmin, qmax, qden, eps}; }))
-      .def("__call__", &PcObserveFqOp::call, "(y, scale, zp) of pc_observe_fq(x) with the bound state / range");
+      .def("__call__", &PcObserveFqOp::call,
+           "(y, scale, zp) of pc_observe_fq(x) with the bound state / range, or None when x is not a "
+           "contiguous grad-requiring CUDA float32 tensor of the state's rows under grad mode");
   m.def("fq_fixed", &fq_fixed, "K1/K5 fake quant with fixed qparams; STE backward");
   m.def("fq_learn", &fq_learn, "K1/K5 learnable fake quant; K4 backward", pybind11::arg("x"), pybind11::arg("scale"),
         pybind11::arg("scale_host"), pybind11::arg("zp"), pybind11::arg("zp_host"), pybind11::arg("qmin"),

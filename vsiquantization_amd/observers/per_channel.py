@@ -79,19 +79,29 @@ class PerChannelMinMaxObserver(BaseObserver):
         """Fused observe + fake quant of ``x`` with ``quantizer``'s integer range (one pass).
 
         Returns (y, row_stats | None); y carries the STE gradient."""
+        # the training step's call (public-API C2 step): straight to a C++ op bound to this
+        # observer's state and the quantizer's range, which checks x itself (None back: the
+        # general path below); rebuilt when the state or the range changes
+        op = self.__dict__.get("_op")
+        if (op is not None and not want_row_stats and op[0] is self.run_min
+                and op[1] == (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax)
+                and H.torch_ext_enabled()):
+            r = op[2](x)
+            if r is not None:
+                y, self.scale, self.zero_point = r
+                return y, None
         if (not want_row_stats and H.torch_ext_enabled() and isinstance(x, torch.Tensor) and x.is_cuda
                 and x.dtype == torch.float32 and x.requires_grad and x.is_contiguous() and torch.is_grad_enabled()):
-            # the training step's call (public-API C2 step): straight to a C++ op bound to
-            # this observer's state and the quantizer's range (rebuilt when either changes)
             mn, mx = self._state(x)
-            key = (mn, self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax)
-            op = self.__dict__.get("_op")
-            if op is None or op[0][0] is not mn or op[0][1:] != key[1:]:
-                op = self._op = (key, H.torch_ext().PcObserveFqOp(
-                    mn, mx, bool(self.symmetric), int(quantizer.qmin), int(quantizer.qmax),
-                    qden(self.symmetric, self.num_bits, self.eps), float(self.eps)))
-            y, self.scale, self.zero_point = op[1](x)
-            return y, None
+            op = self._op = (mn, (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax),
+                             H.torch_ext().PcObserveFqOp(mn, mx, bool(self.symmetric), int(quantizer.qmin),
+                                                         int(quantizer.qmax),
+                                                         qden(self.symmetric, self.num_bits, self.eps),
+                                                         float(self.eps)))
+            r = op[2](x)
+            if r is not None:
+                y, self.scale, self.zero_point = r
+                return y, None
         if _host.is_host(x):
             mn, mx = self._state(x)
             args = (self.symmetric, quantizer.qmin, quantizer.qmax, self.num_bits, self.eps, mn, mx)
@@ -106,15 +116,14 @@ class PerChannelMinMaxObserver(BaseObserver):
             return y, rs
         x = H.require_device_f32(x)
         mn, mx = self._state(x)
-        if x.requires_grad and torch.is_grad_enabled():
-            if H.torch_ext_enabled():   # C++ autograd node (_vsiq_torch.so)
-                y, s, z, rs = H.torch_ext().pc_observe_fq(x, mn, mx, bool(self.symmetric), int(quantizer.qmin),
-                                                          int(quantizer.qmax),
-                                                          qden(self.symmetric, self.num_bits, self.eps),
-                                                          float(self.eps), bool(want_row_stats))
-            else:
-                y, s, z, rs = PerChannelObserveFQFn.apply(x, self.symmetric, quantizer.qmin, quantizer.qmax,
-                                                          self.num_bits, self.eps, mn, mx, want_row_stats)
+        if H.torch_ext_enabled():   # C++ op (_vsiq_torch.so): an autograd node when x needs one
+            y, s, z, rs = H.torch_ext().pc_observe_fq(x, mn, mx, bool(self.symmetric), int(quantizer.qmin),
+                                                      int(quantizer.qmax), qden(self.symmetric, self.num_bits, self.eps),
+                                                      float(self.eps), bool(want_row_stats))
+            rs = rs if want_row_stats else None
+        elif x.requires_grad and torch.is_grad_enabled():   # VSIQ_TORCH_EXT=0: the Python Function over ctypes
+            y, s, z, rs = PerChannelObserveFQFn.apply(x, self.symmetric, quantizer.qmin, quantizer.qmax,
+                                                      self.num_bits, self.eps, mn, mx, want_row_stats)
             rs = rs if want_row_stats else None
         else:
             r = per_channel_observe_fq(x, symmetric=self.symmetric, qmin=quantizer.qmin,
