@@ -1273,7 +1273,7 @@ def gate_retunes(H):
                if t.startswith("retunes="))
 
 
-def _interleaved_us(fns, steps=40, reps=9, warmup=30):
+def _interleaved_us(fns, steps=100, reps=11, warmup=30):
     """Host + GPU time per call (us) of each step function, the reps interleaved so that
     both see the same host load: (median, min) per function."""
     for f in fns:
@@ -1294,7 +1294,7 @@ def _interleaved_us(fns, steps=40, reps=9, warmup=30):
 def api_timings(dev):
     """Public-API step timings, interleaved so every step function sees the same host load
     (host time on the shared boxes moves 2x between processes and minutes): median (and
-    min) of 9 runs of 40 steps each, us per step.
+    min) of 11 runs of 100 steps each, us per step.
 
     * api_us_per_step: the C2 step through the PUBLIC Python API (what a QAT user runs):
       PerChannelMinMaxObserver.observe_quantize(W, PerChannelUniformQuantizer(8, False)) +

@@ -179,16 +179,16 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     sel.gate = (uint32_t)forced;
     return sel;
   }
-  const int64_t cus = device_cus();
-  if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return sel;
-  const int khz = device_wall_clock_khz();
-  const double est = (double)read_bytes / 7.5e12 * 1e3 * (double)khz;
-  if (!g_tune.gate_autotune) {
-    sel.gate = clamp_ticks(kDefault * est, khz);
-    return sel;
-  }
-  int dev = 0;
+  int dev = 0;   // one device query per launch (the attribute caches are per device)
   if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    dev = -1;
+  }
+  const int64_t cus = device_cus(dev);
+  if (grid < 2 * cus || occ <= 0 || grid > (int64_t)occ * cus) return sel;
+  const int khz = device_wall_clock_khz(dev);
+  const double est = (double)read_bytes / 7.5e12 * 1e3 * (double)khz;
+  if (!g_tune.gate_autotune || dev < 0) {
     sel.gate = clamp_ticks(kDefault * est, khz);
     return sel;
   }

@@ -1164,9 +1164,14 @@ int occupancy_blocks(const void *kernel, int block) {
 // per-device attribute caches: relaxed atomics (any thread may fill them; the value
 // is the same whoever wins)
 int device_wall_clock_khz() {
-  static std::atomic<int> khz[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 100000;
+  if (hipGetDevice(&dev) != hipSuccess) return 100000;
+  return device_wall_clock_khz(dev);
+}
+
+int device_wall_clock_khz(int dev) {
+  static std::atomic<int> khz[64];
+  if (dev < 0 || dev >= 64) return 100000;
   if (!khz[dev]) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) != hipSuccess || v <= 0) v = 100000;
@@ -1176,9 +1181,14 @@ int device_wall_clock_khz() {
 }
 
 int device_cus() {
-  static std::atomic<int> cus[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  return device_cus(dev);
+}
+
+int device_cus(int dev) {
+  static std::atomic<int> cus[64];
+  if (dev < 0 || dev >= 64) return 256;
   if (!cus[dev]) {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;

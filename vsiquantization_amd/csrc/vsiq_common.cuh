@@ -1306,8 +1306,10 @@ __device__ __forceinline__ void gate_pass(uint32_t gate, const GateClk &c) {
 // off; VSIQ_TUNE_GATE_AUTOTUNE 0 = the 1.05 x estimate without tuning.
 constexpr uint32_t kGateAuto = 0xffffffffu;   // PCArgs::gate: resolved at launch
 int device_cus();
+int device_cus(int dev);
 int occupancy_blocks(const void *kernel, int block);
 int device_wall_clock_khz();
+int device_wall_clock_khz(int dev);
 struct GateSel {
   uint32_t gate = 0;    // wall-clock ticks for the launch (0 = no gate)
   void *timing = nullptr;   // tuner sample in flight (record its end after the launch)
