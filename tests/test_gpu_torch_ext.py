@@ -95,6 +95,32 @@ def test_pc_observe_quantize_bound_op_and_its_fallbacks(monkeypatch):
         assert u.shape == v.shape and torch.equal(_bits(u), _bits(v))
 
 
+def test_pc_observer_with_bound_op_copies_and_pickles(tmp_path):
+    """An observer that has run the public-API step (its bound C++ op cached) deep-copies
+    (ModelEMA, utils/util.py:386) and pickles (torch.save of a whole model): the copy runs
+    on its own running state, and both continue exactly like an uncopied observer."""
+    import copy
+    g0 = torch.Generator(device=DEV).manual_seed(5)
+    w1, w2 = (torch.randn(32, 8, 3, 3, device=DEV, generator=g0) * s for s in (0.05, 0.3))
+    q = V.PerChannelUniformQuantizer(8, False)
+    obs = V.PerChannelMinMaxObserver(False)
+    obs.observe_quantize(w1.clone().requires_grad_(True), q)
+    assert obs.__dict__.get("_op") is not None
+    ref = copy.deepcopy(obs)   # the copy to compare with
+    cp = copy.deepcopy(obs)
+    path = tmp_path / "obs.pt"
+    torch.save(obs, path)
+    ld = torch.load(path, weights_only=False)   # our own file (written just above)
+    for o in (cp, ld):
+        assert "_op" not in o.__dict__ and o.run_min.data_ptr() != obs.run_min.data_ptr()
+    y0, _ = obs.observe_quantize(w2.clone().requires_grad_(True), q)
+    for o in (cp, ld, ref):
+        y, _ = o.observe_quantize(w2.clone().requires_grad_(True), q)
+        assert torch.equal(_bits(y), _bits(y0))
+        assert torch.equal(_bits(o.run_max), _bits(obs.run_max))
+        assert torch.equal(_bits(o.scale), _bits(obs.scale))
+
+
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("kind", ["float", "cuda", "cpu", "qp"])
 def test_fixed_ext_equals_python(kind, act, monkeypatch):

@@ -214,3 +214,22 @@ def test_silu_layout_state_dict_round_trip():
             act = b[0]._silu_act("silu")
         assert any("SiLU reference layout" in str(x.message) for x in w)
     assert act == "silu" and act.layout == (32, 16) and H.act_code(act) == (H.ACT_SILU | (32 << 8) | (16 << 16))
+
+
+def test_per_channel_observer_state_drops_its_bound_op():
+    """The per-channel observer's cached C++ op (set by the public-API step on a GPU) is
+    left out of its pickled / deep-copied state: copies rebuild their own."""
+    import copy
+    import pickle
+
+    class Unpicklable:
+        def __reduce__(self):
+            raise TypeError("not picklable")
+
+    obs = V.PerChannelMinMaxObserver(False)
+    obs.observe(torch.randn(4, 6))
+    obs._op = (obs.run_min, (), Unpicklable())
+    for c in (copy.deepcopy(obs), pickle.loads(pickle.dumps(obs))):
+        assert "_op" not in c.__dict__
+        assert torch.equal(c.run_min, obs.run_min) and torch.equal(c.scale, obs.scale)
+    assert "_op" in obs.__dict__

@@ -55,6 +55,14 @@ class PerChannelMinMaxObserver(BaseObserver):
     def reset(self):
         self.run_min = self.run_max = self.scale = self.zero_point = None
 
+    def __getstate__(self):
+        # the bound C++ op (_op) is a cache of this state: not picklable, and a copy must
+        # not keep launching on the original's running min / max -- rebuilt on first use
+        # (deepcopy, e.g. ModelEMA's of a model holding this observer, and torch.save)
+        state = self.__dict__.copy()
+        state.pop("_op", None)
+        return state
+
     # ------------------------------------------------------------------ protocol
     def observe(self, x, want_row_stats=False):
         x = x if _host.is_host(x) else H.require_device_f32(x)
