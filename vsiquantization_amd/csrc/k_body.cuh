@@ -118,6 +118,30 @@ __device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
   return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
 }
 
+// The STEQ test of lsq_fast_ok<true> for a whole group, as two integer range trees
+// instead of per-element compares: every x, u = x/s and in-range g is +-0 or has
+// |bits| in [2^-40, 2^63] -- the intersection of fdiv_ok's [2^-63, 2^63] (x, u) and
+// ste_ok's [2^-40, 2^64) (g), so a group passing it passes lsq_fast_ok<true> (stricter
+// only for values the fallback paths compute with the same bits).  NaN / inf fail
+// (their bits are above 2^63).  Zeros wrap to 0xffffffff in the "- 1" tree.  The caller
+// checked ste_fast_s (which implies d.fast).
+__device__ __forceinline__ uint32_t lsq_fast_ok4(f4 xv, f4 gv, const QP &p) {
+  constexpr uint32_t kLo = 0x2b800000u, kHi = 0x5f000000u;   // 2^-40, 2^63
+  const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+  uint32_t hi = 0u, lo = 0xffffffffu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float u = fdiv_fast(xs[k], p.d);
+    const float r = __builtin_rintf(u + p.z);
+    const bool m = (r >= p.lo && r <= p.hi);
+    const uint32_t a = __float_as_uint(xs[k]) & 0x7fffffffu, b = __float_as_uint(u) & 0x7fffffffu;
+    const uint32_t c = m ? (__float_as_uint(gs[k]) & 0x7fffffffu) : 0x3f800000u;   // 1.0: g unused
+    hi = max(hi, max(a, max(b, c)));
+    lo = min(lo, min(a - 1u, min(b - 1u, c - 1u)));
+  }
+  return (hi <= kHi && lo >= kLo - 1u) ? 1u : 0u;
+}
+
 struct LsqFold {   // partial record {sum t, sum z}
   static constexpr int K = 2;
   __device__ static void init(double (&a)[2]) { a[0] = a[1] = 0.0; }
@@ -152,9 +176,13 @@ __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4
 #ifndef VSIQ_EXP_K4_STEQ
 #define VSIQ_EXP_K4_STEQ 1   // experiments: 0 = grad_x by the general fast division (round 3)
 #endif
+#ifndef VSIQ_EXP_K4_GRPCHK
+#define VSIQ_EXP_K4_GRPCHK 1   // experiments: 0 = per-element lsq_fast_ok<true> compares
+#endif
   if (VSIQ_EXP_K4_STEQ && ste_fast_s(p.d) &&
-      (lsq_fast_ok<true>(xv.x, gv.x, p) & lsq_fast_ok<true>(xv.y, gv.y, p) & lsq_fast_ok<true>(xv.z, gv.z, p) &
-       lsq_fast_ok<true>(xv.w, gv.w, p))) {
+      (VSIQ_EXP_K4_GRPCHK ? lsq_fast_ok4(xv, gv, p)
+                          : (lsq_fast_ok<true>(xv.x, gv.x, p) & lsq_fast_ok<true>(xv.y, gv.y, p) &
+                             lsq_fast_ok<true>(xv.z, gv.z, p) & lsq_fast_ok<true>(xv.w, gv.w, p)))) {
     o.x = lsq_elem<ZPL, false, true>(xv.x, gv.x, p, c, nv > 0);
     o.y = lsq_elem<ZPL, false, true>(xv.y, gv.y, p, c, nv > 1);
     o.z = lsq_elem<ZPL, false, true>(xv.z, gv.z, p, c, nv > 2);
