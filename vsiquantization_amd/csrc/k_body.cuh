@@ -66,10 +66,59 @@ __device__ __forceinline__ float ste_quot_d(float g, const FastDiv &d) {
   return __builtin_copysignf(__builtin_fmaf(e, d.r, g), p);
 }
 
+#ifndef VSIQ_EXP_K4
+#define VSIQ_EXP_K4 0   // experiments: bit 1 = no f64 accumulation, bit 2 = no range check
+#endif
+#ifndef VSIQ_EXP_K4_LEAN
+#define VSIQ_EXP_K4_LEAN 1   // experiments: 0 = the STEQ element through lsq_elem's general form
+#endif
+
+// RN(a/b) up to the sign of a zero quotient (fdiv_fast without its signed-zero select),
+// for quotients whose zero sign cannot matter: the STEQ element's x/s (it only enters
+// rint(u + z), where +-0 + z gives the same r, and u/s) and u/s (it only multiplies into
+// a gradient term whose zero sign the f64 sum absorbs: the accumulator is never -0).
+// Same conditions as fdiv_fast (fdiv_ok; a == +-0 gives a zero).
+__device__ __forceinline__ float fdiv_fast_nz(float a, const FastDiv &d) {
+  const float q0 = a * d.r;
+  const float e0 = __builtin_fmaf(-q0, d.b, a);
+  const float q1 = __builtin_fmaf(e0, d.r, q0);
+  const float e1 = __builtin_fmaf(-q1, d.b, a);
+  return __builtin_fmaf(e1, d.r, q1);
+}
+
+// r = rint(u + z) and its clamp q = clamp(r, lo, hi) as one med3, m = (q == r): the same
+// m as r in [lo, hi] for every r (NaN: false either way), the same q for finite r (the
+// only r the fast paths use; a zero's sign in q - z is absorbed like fdiv_fast_nz's)
+struct RQM {
+  float r, q;
+  bool m;
+};
+__device__ __forceinline__ RQM lsq_rqm(float u, const QP &p) {
+  RQM o;
+  o.r = __builtin_rintf(u + p.z);
+  o.q = __builtin_amdgcn_fmed3f(o.r, p.lo, p.hi);
+  o.m = o.q == o.r;
+  return o;
+}
+
 // one element of the learnable backward; returns grad_x, adds the f64 gradient terms
 // (STEQ: grad_x by ste_quot_d -- the caller checked ste_fast_s and ste_ok(g))
 template <bool ZPL, bool IEEE, bool STEQ = false>
 __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
+  if (STEQ && VSIQ_EXP_K4_LEAN) {   // the fast path's element (every quotient in range, x finite)
+    const float u = fdiv_fast_nz(x, p.d);
+    const RQM e = lsq_rqm(u, p);
+    const float gq = g * p.s;                 // MulBackward0 (self)
+    const float gm = e.m ? gq : 0.0f;         // ClampBackward1
+    const float t1 = g * (e.q - p.z);         // MulBackward0 (other)
+    const float t2 = (-gm) * fdiv_fast_nz(u, p.d);   // DivBackward0 (other): -(gm) * ((x/s)/s)
+    if ((VSIQ_EXP_K4 & 1) == 0) {
+      acc.t += valid ? (double)t1 + (double)t2 : 0.0;
+      if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;
+    }
+    const float qd = ste_quot_d(g, p.d);
+    return e.m ? qd : 0.0f * p.d.r;          // DivBackward0 (self); 0/s signed like IEEE
+  }
   const float u = fdiv_t<IEEE>(x, p.d);
   const float r = __builtin_rintf(u + p.z);
   const float q = fq_clamp(r, p.lo, p.hi);
@@ -79,9 +128,6 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
   const float t1 = g * (q - p.z);           // MulBackward0 (other)
   const float xs = fdiv_t<IEEE>(u, p.d);    // (self / other) / other
   const float t2 = (-gm) * xs;              // DivBackward0 (other)
-#ifndef VSIQ_EXP_K4
-#define VSIQ_EXP_K4 0
-#endif
   // lanes past the tensor's end (valid false) add +0 terms: selects, not exec branches
   // (acc starts at +0.0, so adding +0.0 never changes its bits)
 #ifndef VSIQ_EXP_K4_SEL
@@ -131,9 +177,11 @@ __device__ __forceinline__ uint32_t lsq_fast_ok4(f4 xv, f4 gv, const QP &p) {
   uint32_t hi = 0u, lo = 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float u = fdiv_fast(xs[k], p.d);
-    const float r = __builtin_rintf(u + p.z);
-    const bool m = (r >= p.lo && r <= p.hi);
+    const float u = VSIQ_EXP_K4_LEAN ? fdiv_fast_nz(xs[k], p.d) : fdiv_fast(xs[k], p.d);
+    const bool m = VSIQ_EXP_K4_LEAN ? lsq_rqm(u, p).m : [&] {
+      const float r = __builtin_rintf(u + p.z);
+      return r >= p.lo && r <= p.hi;
+    }();
     const uint32_t a = __float_as_uint(xs[k]) & 0x7fffffffu, b = __float_as_uint(u) & 0x7fffffffu;
     const uint32_t c = m ? (__float_as_uint(gs[k]) & 0x7fffffffu) : 0x3f800000u;   // 1.0: g unused
     hi = max(hi, max(a, max(b, c)));
