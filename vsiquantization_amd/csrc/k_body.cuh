@@ -106,18 +106,22 @@ __device__ __forceinline__ RQM lsq_rqm(float u, const QP &p) {
 template <bool ZPL, bool IEEE, bool STEQ = false>
 __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
   if (STEQ && VSIQ_EXP_K4_LEAN) {   // the fast path's element (every quotient in range, x finite)
+    // a lane past the tensor's end takes g = 0: its terms are +-0, which the accumulator
+    // absorbs (it starts at +0 and never becomes -0), and its grad_x is not stored
+    g = valid ? g : 0.0f;
     const float u = fdiv_fast_nz(x, p.d);
     const RQM e = lsq_rqm(u, p);
-    const float gq = g * p.s;                 // MulBackward0 (self)
+    const float gq = g * p.d.b;               // MulBackward0 (self); d.b is s
     const float gm = e.m ? gq : 0.0f;         // ClampBackward1
     const float t1 = g * (e.q - p.z);         // MulBackward0 (other)
     const float t2 = (-gm) * fdiv_fast_nz(u, p.d);   // DivBackward0 (other): -(gm) * ((x/s)/s)
     if ((VSIQ_EXP_K4 & 1) == 0) {
-      acc.t += valid ? (double)t1 + (double)t2 : 0.0;
-      if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;
+      acc.t += (double)t1 + (double)t2;
+      if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
     }
-    const float qd = ste_quot_d(g, p.d);
-    return e.m ? qd : 0.0f * p.d.r;          // DivBackward0 (self); 0/s signed like IEEE
+    // DivBackward0 (self): ste_quot_d from the product already formed; 0/s signed like IEEE
+    const float qd = __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-g, p.d.b, gq), p.d.r, g), gq);
+    return e.m ? qd : 0.0f * p.d.r;
   }
   const float u = fdiv_t<IEEE>(x, p.d);
   const float r = __builtin_rintf(u + p.z);
