@@ -194,6 +194,28 @@ __device__ __forceinline__ uint32_t lsq_fast_ok4(f4 xv, f4 gv, const QP &p) {
   return (hi <= kHi && lo >= kLo - 1u) ? 1u : 0u;
 }
 
+// lsq_fast_ok4 with u's range implied by x's instead of tested: with s in (2^-60, 2^60)
+// (ste_fast_s), |x| in [s * 2^-61, s * 2^61] (both products exact: s * 2^-61 > 2^-121 is
+// normal) gives |x/s| in [2^-61, 2^61], so RN(x/s) is inside fdiv_ok's [2^-63, 2^63];
+// x = +-0 gives u = +-0.  One tree over x and the in-range g with the bounds
+// [max(2^-40, s * 2^-61), min(2^63, s * 2^61)] -- inside fdiv_ok (x) and ste_ok (g).
+__device__ __forceinline__ uint32_t lsq_fast_ok4x(f4 xv, f4 gv, const QP &p) {
+  const uint32_t lo = max(0x2b800000u, __float_as_uint(p.d.b * 0x1p-61f));
+  const uint32_t hi = min(0x5f000000u, __float_as_uint(p.d.b * 0x1p61f));
+  const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+  uint32_t mx = 0u, mn = 0xffffffffu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float u = fdiv_fast_nz(xs[k], p.d);
+    const bool m = lsq_rqm(u, p).m;
+    const uint32_t a = __float_as_uint(xs[k]) & 0x7fffffffu;
+    const uint32_t c = m ? (__float_as_uint(gs[k]) & 0x7fffffffu) : 0x3f800000u;   // 1.0: g unused
+    mx = max(mx, max(a, c));
+    mn = min(mn, min(a - 1u, c - 1u));
+  }
+  return (mx <= hi && mn >= lo - 1u) ? 1u : 0u;
+}
+
 struct LsqFold {   // partial record {sum t, sum z}
   static constexpr int K = 2;
   __device__ static void init(double (&a)[2]) { a[0] = a[1] = 0.0; }
@@ -229,10 +251,11 @@ __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4
 #define VSIQ_EXP_K4_STEQ 1   // experiments: 0 = grad_x by the general fast division (round 3)
 #endif
 #ifndef VSIQ_EXP_K4_GRPCHK
-#define VSIQ_EXP_K4_GRPCHK 1   // experiments: 0 = per-element lsq_fast_ok<true> compares
+#define VSIQ_EXP_K4_GRPCHK 2   // experiments: 0 = per-element lsq_fast_ok<true> compares, 1 = u tested too
 #endif
   if (VSIQ_EXP_K4_STEQ && ste_fast_s(p.d) &&
-      (VSIQ_EXP_K4_GRPCHK ? lsq_fast_ok4(xv, gv, p)
+      (VSIQ_EXP_K4_GRPCHK == 2 && VSIQ_EXP_K4_LEAN ? lsq_fast_ok4x(xv, gv, p)
+       : VSIQ_EXP_K4_GRPCHK ? lsq_fast_ok4(xv, gv, p)
                           : (lsq_fast_ok<true>(xv.x, gv.x, p) & lsq_fast_ok<true>(xv.y, gv.y, p) &
                              lsq_fast_ok<true>(xv.z, gv.z, p) & lsq_fast_ok<true>(xv.w, gv.w, p)))) {
     o.x = lsq_elem<ZPL, false, true>(xv.x, gv.x, p, c, nv > 0);
