@@ -263,3 +263,59 @@ def test_deepcopy_of_enabled_model_defers_its_own_managers():
         assert torch.equal(res[0][1][n], res[1][1][n]), n
     for h in hs:
         h.remove()
+
+
+def _edge_values(s):
+    """x and g values at and just past the K4 fast path's bounds for scale s (k_body.cuh
+    lsq_fast_ok4x: |x| in [max(2^-40, s 2^-61), min(2^63, s 2^61)], in-range |g| in
+    [2^-40, 2^63], or zero), plus subnormals and zeros of both signs."""
+    f = np.float32
+    up = lambda v: np.nextafter(f(v), f(np.inf))     # noqa: E731
+    dn = lambda v: np.nextafter(f(v), f(0))          # noqa: E731
+    lo, hi = max(2.0 ** -40, s * 2.0 ** -61), min(2.0 ** 63, s * 2.0 ** 61)
+    xs = [0.0, -0.0, lo, dn(lo), hi, up(hi), -hi, 2.0 ** -40, dn(2.0 ** -40), 2.0 ** 63, up(2.0 ** 63),
+          1e-45, -1e-40, s * 3.5, -s * 7.5, s * 0.5, s * 1.5]
+    gs = [0.0, -0.0, 2.0 ** -40, dn(2.0 ** -40), 2.0 ** 20, -(2.0 ** 20), 1e-45, -3e-39, 0.7, -1.3, 5.0]
+    return np.array(xs, dtype=np.float32), np.array(gs, dtype=np.float32)
+
+
+@pytest.mark.parametrize("s", [2.0 ** -59.5, 1e-3, 0.03, 1.0, 2.0 ** 40, 2.0 ** 59.5])
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_fast_path_bounds_k4_k4d(s, act):
+    """Elements at and past every bound of the K4 / K4d fast-path test, in random groups of
+    four among ordinary values (so groups take the fast path, the general fast division or
+    IEEE): grad_x bit for bit equal to the oracle (no act) and between K4 and K4d, the scale
+    gradient to f64 order (bounded by the sum of the terms' magnitudes)."""
+    rng = np.random.default_rng(int(s * 1e3) % 9973 + (act is not None))
+    ex, eg = _edge_values(s)
+    n = 4 * 2048 + 3
+    x = (rng.standard_normal(n) * 4 * s).astype(np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    idx = rng.choice(n, size=600, replace=False)
+    x[idx] = ex[rng.integers(0, ex.size, idx.size)]
+    idx = rng.choice(n, size=600, replace=False)
+    g[idx] = eg[rng.integers(0, eg.size, idx.size)]
+    qmin, qmax, gscale = -8, 7, 0.37
+    xd, gd = torch.from_numpy(x).to(DEV), torch.from_numpy(g).to(DEV)
+    sd = torch.tensor(s, dtype=torch.float64, device=DEV)
+    gx4, grads4 = FQ.lsq_backward(gd, xd, sd, 0.0, qmin, qmax, gscale, False, act=act)
+    e = D._Fold()
+    e.nrec = int(H.lib().vsiq_lsq_part_records(H.c_i64(n)))
+    e.records = torch.full((2 * e.nrec,), float("nan"), dtype=torch.float64, device=DEV)
+    gxd, e.zd, e.zh = D.lsq_backward_part(gd, xd, sd, 0.0, qmin, qmax, False, act, e.records)
+    e.gscale, e.qmin, e.qmax, e.learn_zp = gscale, qmin, qmax, False
+    e.out = torch.empty(2, dtype=torch.float64, device=DEV)
+    D.fold([e])
+    torch.cuda.synchronize()
+    assert torch.equal(gx4.view(torch.int32), gxd.view(torch.int32))
+    bound = 1e-13 * 2 * float(np.abs(g.astype(np.float64)).sum()) * (qmax + 2) * gscale
+    g4, gd_ = float(grads4[0]), float(e.out[0])
+
+    def close(a, b, rel):   # NaN where the terms hold 0 * inf (x / s / s overflows at tiny s), as in torch
+        return (np.isnan(a) and np.isnan(b)) or abs(a - b) <= bound + rel * abs(b)
+
+    assert close(g4, gd_, 1e-12), (g4, gd_)
+    if act is None:
+        _, gxo, gso, _ = O.lsq_forward_backward(x, g, s, 0.0, qmin, qmax, gscale)
+        G.assert_bitwise_f32(gx4.cpu().numpy(), gxo, "grad_x")
+        assert close(g4, gso, 1e-9), (g4, gso)
