@@ -977,11 +977,13 @@ def cpu_baseline(workload, seconds, bits=(2, 4)):
     # C4's whole workload (547M elements fwd + bwd) takes ~5 s per run on 16 host CPUs, so
     # a `seconds` budget held one timed run; a quarter of its images (same per-element
     # work) gives min-of-several like the other configs
-    fn, n, desc = cpu_workload(workload, bits, frac=4 if workload == "c4" else 1)
+    frac = 4 if workload == "c4" else 1
+    fn, n, desc = cpu_workload(workload, bits, frac=frac)
+    what = "whole workload" if frac == 1 else f"1/{frac} sample of the workload"
     prev = torch.get_num_threads()
     tried, runs = {}, {}
     for th in counts:
-        progress(f"cpu baseline {workload}: whole workload at {th} threads")
+        progress(f"cpu baseline {workload}: {what} at {th} threads")
         torch.set_num_threads(th)
         t, runs[th] = _best_time(fn, seconds)
         tried[th] = n / t / 1e6

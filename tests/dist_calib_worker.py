@@ -83,6 +83,13 @@ def main():
             qm.dist_defer = mode == "deferred"
         observe(cfg, mgrs, acts, shard=(rank, world))
         if mode == "deferred":
+            # a read before the sync needs every rank's records: it raises on every
+            # rank (no collective from one rank), and the sync still works afterwards
+            try:
+                float(mgrs[0].scale)
+                res["deferred_read_raises"] = False
+            except RuntimeError as e:
+                res["deferred_read_raises"] = "sync_calibration" in str(e)
             sync_calibration(torch.nn.ModuleList(mgrs))
             for qm in mgrs:
                 qm.dist_defer = False

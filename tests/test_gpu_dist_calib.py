@@ -83,6 +83,7 @@ def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name, backend, r
     _same(one, _oracle(cfg, acts), "1 GPU vs oracle")
     for mode in ("per_call", "deferred"):
         _same(got[mode], one, f"{ranks} ranks ({backend}) {mode} vs 1 GPU")
+    assert got["deferred_read_raises"] is True   # a read before sync_calibration, every rank
     if backend == "nccl":
         assert got["graph"]["replays_equal_eager"], got["graph"]
     if name == "small":
@@ -104,8 +105,10 @@ def test_sharded_calibration_two_ranks_equals_one_gpu(tmp_path, name, backend, r
 
 def test_c5_one_batch_full_size():
     """C5 per GPU: one calibration batch of 128 images (3x320x320 network input; 274M
-    activation elements over the 27 layers) through the deferred observers
-    (calibrate_qat_model's default path: K2p + one sync) against the oracle."""
+    activation elements over the 27 layers) through the deferred observers -- the
+    default path of calibrate_qat_model: each fused-ReLU call goes to K2o
+    (QuantizationManager._observe_deferred_act -> fakequant.observe_parts_out, which also
+    writes ReLU(x)), then one sync -- against the oracle."""
     import bench
     from vsiquantization_amd.distributed import sync_calibration
     cfg = Config("c5")

@@ -37,6 +37,10 @@ def _host_number(v: float):
 
 @register_class
 class MinMaxObserver(BaseObserver):
+    # weakref to the QuantizationManager whose deferred calibration calls (not folded yet)
+    # hold this observer's later updates: any read or update folds them first
+    _defer_owner = None
+
     def __init__(self, symmetric=True, num_bits=8, eps=1e-8):
         self.symmetric = symmetric
         self.eps = eps
@@ -54,7 +58,16 @@ class MinMaxObserver(BaseObserver):
                 torch.cuda.current_stream(self._state.device).wait_stream(self._obs_stream)
             self._obs_stream = None
 
+    def _fold_owner(self):
+        owner = self._defer_owner()
+        if owner is None:
+            self._defer_owner = None
+        else:
+            owner._fold_pending()
+
     def _sync(self):
+        if self._defer_owner is not None:
+            self._fold_owner()
         self._join()
         if self._dirty:
             mn, mx = self._state.tolist()
@@ -95,6 +108,8 @@ class MinMaxObserver(BaseObserver):
         return self._state
 
     def reset(self):
+        if self._defer_owner is not None:
+            self._fold_owner()
         self._state = None
         self._host = [0, 0]
         self._dirty = False
@@ -103,6 +118,8 @@ class MinMaxObserver(BaseObserver):
     def observe_device(self, x, want_stats=True, want_qp=True, act=None):
         """One K2 pass: update the running state, return (qp f64[4], stats f64[10]) on x.device.
         ``act``: observe act(x) (fused ReLU/SiLU, K5) without materializing it."""
+        if self._defer_owner is not None:
+            self._fold_owner()
         if host.is_host(x):   # CPU tensor: the native host pass (host.py), CPU fp32[2] state
             dev = x.device
         else:
