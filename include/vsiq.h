@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 9
+#define VSIQ_ABI_VERSION 10
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -81,11 +81,10 @@ int64_t vsiq_workspace_doubles(int64_t n);
 int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
 
 /* Performance knobs (process-wide; results are identical for every setting). */
-#define VSIQ_TUNE_PC_ROWS_PER_BLOCK 1  /* K3 rows per workgroup, 0 = auto */
+/* (keys 1, 5, 8 and 16 -- K3 rows per workgroup / workgroup size, K2 grid, K2 cached-load
+   threshold -- were removed in ABI 10: their values are fixed; vsiq_set_tuning rejects them) */
 #define VSIQ_TUNE_NONTEMPORAL 2        /* 1 = nontemporal streamed loads/stores (default) */
-#define VSIQ_TUNE_PC_BLOCK 5           /* K3 workgroup size 256 / 512 / 1024, 0 = auto */
 #define VSIQ_TUNE_OBS_KERNEL 7         /* K2 observer: 0 auto, 1 one-shot, 2 grid-stride */
-#define VSIQ_TUNE_OBS_GRID 8           /* K2 grid-stride workgroups, 0 = auto (512), max 2048 */
 #define VSIQ_TUNE_LSQ_GROUPS 9         /* K4 groups per lane 2 / 4 / 8 / 16, 0 = by size */
 #define VSIQ_TUNE_PC_PACKED 10         /* per-channel fq with given qparams + K6: 1 = packed short
                                           rows / channel columns for K6 on axis 1 (default),
@@ -107,9 +106,6 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
                                           1: grid-stride, vsiq_act_observe_part_f32's records */
 #define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = default (2) */
 #define VSIQ_TUNE_K2O_BLOCK 17         /* K2o one-shot lanes per workgroup 256/512/1024, 0 = default */
-#define VSIQ_TUNE_OBS_TEMPORAL_MB 16   /* K2 (per-call observer): cached loads for tensors under N MB
-                                          (the fake quant re-reading it may hit the 256 MB
-                                          Infinity Cache); default 256, 0 = nontemporal always */
 int vsiq_set_tuning(int key, int value);
 
 /*
@@ -598,6 +594,19 @@ int vsiq_host_pc_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int
 int vsiq_host_pc_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                              const double *scale, const double *zp, int zp_learn, int qmin, int qmax, double gscale,
                              double *grad_scale_out, double *grad_zp_out);
+/* Per-channel along axis 1 ([N, C, ...] activations, LSQFakeQuantize's broadcast of
+ * [1, C, 1, ...] parameters, quantizers/lsq_module.py:141-143) on the host, in the device
+ * ABI's vsiq_pcm_* layout: rows = N * channels rows of rowlen elements, row r in channel
+ * r % channels; scale / zp f64[channels]; grad_*_out f64[channels], each the f64 sum of
+ * the channel's rows in row order times gscale.  channels == rows is the vsiq_host_pc_*
+ * call (the same bits). */
+int vsiq_host_pcm_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen, int64_t channels,
+                             const double *scale, const double *zp, int zp_round, int qmin, int qmax);
+int vsiq_host_pcm_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
+                              int64_t channels, const double *scale);
+int vsiq_host_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                              int64_t channels, const double *scale, const double *zp, int zp_learn, int qmin, int qmax,
+                              double gscale, double *grad_scale_out, double *grad_zp_out);
 int vsiq_host_threads(void);
 int vsiq_host_simd(void);   /* 1: the AVX-512 loops are in use */
 

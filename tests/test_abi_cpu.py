@@ -145,9 +145,11 @@ def test_tuning_keys_match_header_and_bounds():
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
                             "vsiq.h")).read()
     keys = dict(re.findall(r"#define VSIQ_(TUNE_\w+) (\d+)", hdr))
-    for name in ("TUNE_PC_ROWS_PER_BLOCK", "TUNE_NONTEMPORAL", "TUNE_PC_BLOCK", "TUNE_STORE_DEFER", "TUNE_OBS_KERNEL",
-                 "TUNE_OBS_GRID", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED", "TUNE_STORE_GATE", "TUNE_GATE_AUTOTUNE",
-                 "TUNE_XCD_ORDER"):
+    names = ("TUNE_NONTEMPORAL", "TUNE_STORE_DEFER", "TUNE_OBS_KERNEL", "TUNE_LSQ_GROUPS", "TUNE_PC_PACKED",
+             "TUNE_STORE_GATE", "TUNE_GATE_AUTOTUNE", "TUNE_XCD_ORDER", "TUNE_K2O_FORM", "TUNE_K2O_GROUPS",
+             "TUNE_K2O_BLOCK")
+    assert sorted(keys) == sorted(names)   # every key the header declares, and no other
+    for name in names:
         assert int(keys[name]) == getattr(H, name), name
     assert int(re.search(r"#define VSIQ_COUNTER_WORDS (\d+)", hdr).group(1)) == H.COUNTER_WORDS
     assert int(re.search(r"#define VSIQ_ABI_VERSION (\d+)", hdr).group(1)) == H.ABI_VERSION
@@ -156,7 +158,8 @@ def test_tuning_keys_match_header_and_bounds():
     assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, -2) != 0
     assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, 4) == 0
     assert lib.vsiq_set_tuning(H.TUNE_STORE_DEFER, -1) == 0
-    assert lib.vsiq_set_tuning(H.TUNE_PC_BLOCK, 384) != 0
+    for key in H.REMOVED_TUNE_KEYS:   # ABI 10 removed them: rejected for every value
+        assert lib.vsiq_set_tuning(key, 0) != 0 and lib.vsiq_set_tuning(key, 1) != 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 3) != 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 2) == 0
     assert lib.vsiq_set_tuning(H.TUNE_GATE_AUTOTUNE, 2) != 0

@@ -279,7 +279,10 @@ def _edge_values(s):
     return np.array(xs, dtype=np.float32), np.array(gs, dtype=np.float32)
 
 
-@pytest.mark.parametrize("s", [2.0 ** -59.5, 1e-3, 0.03, 1.0, 2.0 ** 40, 2.0 ** 59.5])
+# ste_fast_s admits the closed range [2^-60, 2^60]: both ends and the floats just outside
+@pytest.mark.parametrize("s", [float(np.nextafter(np.float32(2.0 ** -60), np.float32(0))), 2.0 ** -60,
+                               2.0 ** -59.5, 1e-3, 0.03, 1.0, 2.0 ** 40, 2.0 ** 59.5, 2.0 ** 60,
+                               float(np.nextafter(np.float32(2.0 ** 60), np.float32(np.inf)))])
 @pytest.mark.parametrize("act", [None, "relu"])
 def test_fast_path_bounds_k4_k4d(s, act):
     """Elements at and past every bound of the K4 / K4d fast-path test, in random groups of

@@ -508,3 +508,42 @@ def test_golden_per_channel_learnable(case):
     np.testing.assert_allclose(npy(scale.grad), G.arr(case["scale_grad"]), rtol=1e-4, atol=3e-6)
     if not sym:
         np.testing.assert_allclose(npy(zp.grad), G.arr(case["zp_grad"]), rtol=1e-4, atol=3e-6)
+
+
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_nontemporal_off_equals_default(act):
+    """VSIQ_TUNE_NONTEMPORAL 0 (cached loads / stores in every streamed kernel, the knob an
+    operator A/B-tests on a box) gives the default's bits: K3 per-channel observe + fake
+    quant and its STE backward, K2 + K1 per tensor, K4, K2o deferred records."""
+    g0 = torch.Generator(device=DEV).manual_seed(31)
+    w = torch.randn(256, 64, 3, 3, device=DEV, generator=g0) * 0.05
+    x = torch.randn(8, 32, 40, 40, device=DEV, generator=g0)
+    gy = torch.randn(8, 32, 40, 40, device=DEV, generator=g0)
+
+    def run():
+        out = []
+        r = FQ.per_channel_observe_fq(w, symmetric=False, qmin=0, qmax=255, want_mask=True)
+        out += [r["y"], r["scale"], r["zp"]]
+        qp, st = FQ.observe_tensor(x, symmetric=True, act=act)
+        y, mask, _ = FQ.fake_quant(x, None, None, -128, 127, qp=qp, want_mask=True, act=act)
+        out += [qp, st, y, FQ.ste_backward(gy, mask, qp[H.QP_SCALE:H.QP_SCALE + 1], pre=x if act else None,
+                                            act=act)]
+        gx, grads = FQ.lsq_backward(gy, x, 0.02, 3.0, -8, 7, 0.37, True, act=act)
+        out += [gx, grads]
+        yo, slot = FQ.observe_parts_out(x, act or "relu")
+        out += [yo, FQ.fold_parts(slot.reshape(1, -1))]
+        torch.cuda.synchronize()
+        return [o.detach().clone() for o in out]
+
+    base = run()
+    H.set_tuning(H.TUNE_NONTEMPORAL, 0)
+    try:
+        off = run()
+    finally:
+        H.set_tuning(H.TUNE_NONTEMPORAL, 1)
+    for i, (a, b) in enumerate(zip(base, off)):
+        a, b = a.reshape(-1), b.reshape(-1)
+        if a.dtype == torch.float64:
+            assert torch.equal(a.view(torch.int64), b.view(torch.int64)) or torch.allclose(a, b, rtol=1e-15), i
+        else:
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), i

@@ -121,6 +121,26 @@ def test_pc_observer_with_bound_op_copies_and_pickles(tmp_path):
         assert torch.equal(_bits(o.scale), _bits(obs.scale))
 
 
+def test_pc_observer_bound_op_follows_a_replaced_run_max():
+    """The bound op is keyed on BOTH running tensors: replacing run_max alone (a state
+    restore, a sync that reassigns it) rebuilds it, so the next step updates and reads
+    the new tensor -- equal to a fresh observer started from the same state."""
+    g0 = torch.Generator(device=DEV).manual_seed(7)
+    w1, w2 = (torch.randn(16, 8, 3, 3, device=DEV, generator=g0) * s for s in (0.05, 0.3))
+    q = V.PerChannelUniformQuantizer(8, False)
+    obs = V.PerChannelMinMaxObserver(False)
+    obs.observe_quantize(w1.clone().requires_grad_(True), q)
+    assert obs.__dict__.get("_op") is not None
+    new_max = torch.full_like(obs.run_max, 5.0)
+    obs.run_max = new_max
+    ref = V.PerChannelMinMaxObserver(False)
+    ref.run_min, ref.run_max = obs.run_min.clone(), new_max.clone()
+    y, _ = obs.observe_quantize(w2.clone().requires_grad_(True), q)
+    y_ref, _ = ref.observe_quantize(w2.clone().requires_grad_(True), q)
+    assert obs.run_max is new_max and torch.all(new_max == 5.0)
+    assert torch.equal(_bits(y), _bits(y_ref)) and torch.equal(_bits(obs.scale), _bits(ref.scale))
+
+
 @pytest.mark.parametrize("act", [None, "relu", "silu"])
 @pytest.mark.parametrize("kind", ["float", "cuda", "cpu", "qp"])
 def test_fixed_ext_equals_python(kind, act, monkeypatch):

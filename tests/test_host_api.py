@@ -228,7 +228,7 @@ def test_per_channel_observer_state_drops_its_bound_op():
 
     obs = V.PerChannelMinMaxObserver(False)
     obs.observe(torch.randn(4, 6))
-    obs._op = (obs.run_min, (), Unpicklable())
+    obs._op = (obs.run_min, obs.run_max, (), Unpicklable())
     for c in (copy.deepcopy(obs), pickle.loads(pickle.dumps(obs))):
         assert "_op" not in c.__dict__
         assert torch.equal(c.run_min, obs.run_min) and torch.equal(c.scale, obs.scale)

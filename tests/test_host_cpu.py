@@ -262,3 +262,102 @@ def test_per_channel_host_rows_parallel_equal_single_rows():
             assert float(obs.scale[c]) == s and float(obs.zero_point[c]) == z
             G.assert_bitwise_f32(npy(y[c]), npy(V.UniformQuantizer(8, False).quantize(t(w[c]), s, z, False)),
                                  f"row {c}")
+
+
+def _lsq_module(per_channel, config_act):
+    if per_channel:
+        return V.LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                                 observer=torch.quantization.MovingAveragePerChannelMinMaxObserver,
+                                 quant_min=0, quant_max=255, dtype=torch.quint8,
+                                 qscheme=torch.per_channel_affine, reduce_range=False,
+                                 averaging_constant=0.01, ch_axis=1)
+    return V.LSQFakeQuantize(learn_scale=True, config_act=config_act,
+                             observer=torch.quantization.MovingAverageMinMaxObserver, quant_min=0,
+                             quant_max=255, dtype=torch.quint8, qscheme=torch.per_tensor_affine,
+                             reduce_range=False)
+
+
+@pytest.mark.parametrize("case", G.cases("lsq_fake_quantize"), ids=lambda c: c["key"])
+def test_golden_lsq_fake_quantize_on_cpu(case):
+    """LSQFakeQuantize's learnable path on CPU tensors (host loops: per channel the [N, C, ...]
+    rows of vsiq_host_pcm_*) == the reference goldens: y / grad_x bitwise, parameter
+    gradients to the reference's fp32 sums (1e-4) and the oracle's f64 form (1e-9)."""
+    fq = _lsq_module(case["per_channel"], case["config_act"])
+    x, g = G.arr(case["x"]), G.arr(case["g"])
+    fq(t(x))                                        # registers scale_param / zero_point_param_float
+    fq.scale_param.data.copy_(t(G.arr(case["scale"])))
+    fq.zero_point_param_float.data.copy_(t(G.arr(case["zp"])))
+    fq.disable_observer()
+    xg = t(x, grad=True)
+    y = fq(xg)
+    y.backward(t(g))
+    G.assert_bitwise_f32(npy(y), G.arr(case["y"]), "y")
+    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["grad_x"]), "grad_x")
+    np.testing.assert_allclose(npy(fq.scale_param.grad), G.arr(case["scale_grad"]), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(npy(fq.zero_point_param_float.grad), G.arr(case["zp_grad"]), rtol=1e-4, atol=1e-6)
+    if case["per_channel"]:
+        s, z = G.arr(case["scale"]).reshape(-1), G.arr(case["zp"]).reshape(-1)
+        gsc = O.lsq_module_grad_scale(x.shape, case["qmax"], True, case["config_act"])
+        _, _, gso, gzo = O.pc_lsq_forward_backward(x, g, s, z, case["qmin"], case["qmax"], gsc, axis=1)
+        np.testing.assert_allclose(npy(fq.scale_param.grad).reshape(-1), gso, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(npy(fq.zero_point_param_float.grad).reshape(-1), gzo, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("shape,axis", [((6, 3, 7, 5), 1), ((2, 5, 7), 1), ((3, 5), 1), ((1, 4, 70000), 1),
+                                        ((9, 16, 4, 4), 1), ((12, 27), 0), ((3, 70000), 0)])
+def test_pc_lsq_host_vs_oracle(shape, axis):
+    """host.PcLearnFn on either axis vs the oracle's pc_lsq_forward_backward: y / grad_x
+    bitwise, f64 [C] gradients <= 1e-9 of the oracle's (f64 sums in another order)."""
+    rng = np.random.default_rng(sum(shape) + axis)
+    x = (rng.standard_normal(shape) * 2).astype(np.float32)
+    g = rng.standard_normal(shape).astype(np.float32)
+    C = shape[axis]
+    s = rng.uniform(0.01, 0.1, C)
+    z = np.rint(rng.uniform(0, 255, C)) + 0.2
+    gscale = (255 * x.size / C) ** -0.5
+    sp = torch.nn.Parameter(torch.tensor(s, dtype=torch.float64))
+    zp = torch.nn.Parameter(torch.tensor(z, dtype=torch.float64))
+    xg = t(x, grad=True)
+    y = host.PcLearnFn.apply(xg, sp, zp, 0, 255, gscale, True, axis)
+    y.backward(t(g))
+    yo, gxo, gso, gzo = O.pc_lsq_forward_backward(x, g, s, z, 0, 255, gscale, axis=axis)
+    G.assert_bitwise_f32(npy(y), yo, "y")
+    G.assert_bitwise_f32(npy(xg.grad), gxo, "grad_x")
+    np.testing.assert_allclose(npy(sp.grad), gso, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(npy(zp.grad), gzo, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("shape", [(4, 6, 5, 5), (2, 3, 70000)])
+def test_lsq_fake_quantize_fixed_per_channel_on_cpu(shape):
+    """LSQFakeQuantize with the observer's scale / zero_point buffers (no learning) on CPU:
+    the host loops' per-channel fake quant == the reference's broadcast expression
+    scale * (clamp(round(x / scale + zp)) - zp), bitwise; grad_x the STE mask."""
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal(shape) * 3).astype(np.float32)
+    fq = V.LSQFakeQuantize(learn_scale=False, observer=torch.quantization.MovingAveragePerChannelMinMaxObserver,
+                           quant_min=0, quant_max=255, dtype=torch.quint8, qscheme=torch.per_channel_affine,
+                           ch_axis=1)
+    fq(t(x))
+    fq.disable_observer()
+    xg = t(x, grad=True)
+    y = fq(xg)
+    view = [1, -1] + [1] * (len(shape) - 2)
+    s, z = fq.scale.view(view), fq.zero_point.view(view)
+    want = s * (torch.clamp(torch.round(t(x) / s + z), 0, 255) - z)
+    G.assert_bitwise_f32(npy(y), npy(want), "y")
+    gy = torch.ones_like(y)
+    y.backward(gy)
+    inr = (torch.round(t(x) / s + z) >= 0) & (torch.round(t(x) / s + z) <= 255)
+    G.assert_bitwise_f32(npy(xg.grad), npy(inr.float()), "grad_x")
+
+
+def test_host_pcm_abi_rejects_bad_channel_counts():
+    lib = H.lib()
+    x = torch.zeros(12)
+    s = torch.ones(4, dtype=torch.float64)
+    assert lib.vsiq_host_pcm_fq_fwd_f32(H.ptr(x), H.ptr(x), None, H.c_i64(6), H.c_i64(2), H.c_i64(4), H.ptr(s),
+                                        None, 0, 0, 255) != 0   # 6 rows are not whole images of 4 channels
+    assert lib.vsiq_host_pcm_fq_fwd_f32(H.ptr(x), H.ptr(x), None, H.c_i64(6), H.c_i64(2), H.c_i64(0), H.ptr(s),
+                                        None, 0, 0, 255) != 0
+    assert lib.vsiq_host_pcm_fq_fwd_f32(H.ptr(x), torch.empty(12).data_ptr(), None, H.c_i64(4), H.c_i64(3),
+                                        H.c_i64(2), H.ptr(s), None, 0, 0, 255) == 0

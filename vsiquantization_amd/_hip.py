@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 COUNTER_GRID_ERRORS = 35   # VSIQ_COUNTER_GRID_ERRORS (K10's barrier-timeout count)
 
@@ -36,12 +36,13 @@ PART_LEN = 8   # VSIQ_PART_LEN: doubles per K2p partial record
 PART_MAX_RECORDS = 4096   # VSIQ_PART_MAX_RECORDS
 QP_SCALE, QP_ZP, QP_MIN, QP_MAX = range(4)
 QP_LEN = 4
-TUNE_PC_ROWS_PER_BLOCK, TUNE_NONTEMPORAL, TUNE_PC_BLOCK, TUNE_STORE_DEFER = 1, 2, 5, 6
-TUNE_OBS_KERNEL, TUNE_OBS_GRID, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 8, 9, 10
+TUNE_NONTEMPORAL, TUNE_STORE_DEFER = 2, 6
+TUNE_OBS_KERNEL, TUNE_LSQ_GROUPS, TUNE_PC_PACKED = 7, 9, 10
 TUNE_STORE_GATE = 11
 TUNE_GATE_AUTOTUNE = 12
 TUNE_XCD_ORDER = 13
-TUNE_K2O_FORM, TUNE_K2O_GROUPS, TUNE_OBS_TEMPORAL_MB, TUNE_K2O_BLOCK = 14, 15, 16, 17
+TUNE_K2O_FORM, TUNE_K2O_GROUPS, TUNE_K2O_BLOCK = 14, 15, 17
+REMOVED_TUNE_KEYS = (1, 5, 8, 16)   # ABI 10: K3 rows / workgroup size, K2 grid, K2 cached-load threshold
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 ACT_CODES = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
@@ -174,6 +175,10 @@ _SIGS = {
                                      c_int], c_int),
     "vsiq_host_pc_fq_fwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int], c_int),
     "vsiq_host_pc_ste_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p], c_int),
+    "vsiq_host_pcm_fq_fwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int], c_int),
+    "vsiq_host_pcm_ste_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p], c_int),
+    "vsiq_host_pcm_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p, c_p],
+                                  c_int),
     "vsiq_host_pc_lsq_bwd_f32": ([c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_int, c_int, c_int, c_d, c_p, c_p],
                                  c_int),
     "vsiq_host_threads": ([], c_int),

@@ -53,25 +53,12 @@ struct LsqAcc {
 
 // grad_x's division RN(RN(g*s)/s) in one Markstein step from g (the STE backward's
 // quotient, vsiq_common.cuh ste_quot: g is a faithful quotient of RN(g*s)/s) -- for s in
-// (2^-60, 2^60), positive (ste_fast_s, uniform), and g inside ste_ok; 4 instead of ~8
-// instructions per element.  Bitwise RN(gm/s) there (vsiq_selftest_fq mode 1 proves the
-// quotient over all 2^32 gradients).
+// [2^-60, 2^60] (both ends included), positive (ste_fast_s, uniform), and g inside
+// ste_ok; 4 instead of ~8 instructions per element.  Bitwise RN(gm/s) there
+// (vsiq_selftest_fq mode 1 proves the quotient over all 2^32 gradients).
 __device__ __forceinline__ uint32_t ste_fast_s(const FastDiv &d) {
   return (__float_as_uint(d.b) - 0x21800000u) <= (0x5d800000u - 0x21800000u) ? 1u : 0u;
 }
-
-__device__ __forceinline__ float ste_quot_d(float g, const FastDiv &d) {
-  const float p = g * d.b;
-  const float e = __builtin_fmaf(-g, d.b, p);
-  return __builtin_copysignf(__builtin_fmaf(e, d.r, g), p);
-}
-
-#ifndef VSIQ_EXP_K4
-#define VSIQ_EXP_K4 0   // experiments: bit 1 = no f64 accumulation, bit 2 = no range check
-#endif
-#ifndef VSIQ_EXP_K4_LEAN
-#define VSIQ_EXP_K4_LEAN 1   // experiments: 0 = the STEQ element through lsq_elem's general form
-#endif
 
 // RN(a/b) up to the sign of a zero quotient (fdiv_fast without its signed-zero select),
 // for quotients whose zero sign cannot matter: the STEQ element's x/s (it only enters
@@ -102,10 +89,11 @@ __device__ __forceinline__ RQM lsq_rqm(float u, const QP &p) {
 }
 
 // one element of the learnable backward; returns grad_x, adds the f64 gradient terms
-// (STEQ: grad_x by ste_quot_d -- the caller checked ste_fast_s and ste_ok(g))
+// (STEQ: grad_x by the one-step STE quotient -- the caller checked ste_fast_s and the
+// group test lsq_fast_ok4x)
 template <bool ZPL, bool IEEE, bool STEQ = false>
 __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc &acc, bool valid) {
-  if (STEQ && VSIQ_EXP_K4_LEAN) {   // the fast path's element (every quotient in range, x finite)
+  if (STEQ) {   // the fast path's element (every quotient in range, x finite)
     // a lane past the tensor's end takes g = 0: its terms are +-0, which the accumulator
     // absorbs (it starts at +0 and never becomes -0), and its grad_x is not stored
     g = valid ? g : 0.0f;
@@ -115,10 +103,8 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
     const float gm = e.m ? gq : 0.0f;         // ClampBackward1
     const float t1 = g * (e.q - p.z);         // MulBackward0 (other)
     const float t2 = (-gm) * fdiv_fast_nz(u, p.d);   // DivBackward0 (other): -(gm) * ((x/s)/s)
-    if ((VSIQ_EXP_K4 & 1) == 0) {
-      acc.t += (double)t1 + (double)t2;
-      if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
-    }
+    acc.t += (double)t1 + (double)t2;
+    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
     // DivBackward0 (self): ste_quot_d from the product already formed; 0/s signed like IEEE
     const float qd = __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-g, p.d.b, gq), p.d.r, g), gq);
     return e.m ? qd : 0.0f * p.d.r;
@@ -134,71 +120,29 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
   const float t2 = (-gm) * xs;              // DivBackward0 (other)
   // lanes past the tensor's end (valid false) add +0 terms: selects, not exec branches
   // (acc starts at +0.0, so adding +0.0 never changes its bits)
-#ifndef VSIQ_EXP_K4_SEL
-#define VSIQ_EXP_K4_SEL 1   // experiments: 0 = exec branches on valid / m (round 3)
-#endif
-  if (!VSIQ_EXP_K4_SEL) {
-    if ((VSIQ_EXP_K4 & 1) == 0 && valid) {
-      acc.t += (double)t1 + (double)t2;
-      if (ZPL) acc.z += (double)gm + (double)(-gq);
-    }
-    if (STEQ) return m ? ste_quot_d(g, p.d) : 0.0f * p.d.r;
-    return fdiv_t<IEEE>(gm, p.d);
-  }
-  if ((VSIQ_EXP_K4 & 1) == 0) {
-    acc.t += valid ? (double)t1 + (double)t2 : 0.0;
-    if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;   // AddBackward0 + SubBackward0 (other)
-  }
-  if (STEQ) {   // DivBackward0 (self); 0/s signed like IEEE.  Both sides computed, then selected
-    const float qd = ste_quot_d(g, p.d);
-    return m ? qd : 0.0f * p.d.r;
-  }
+  acc.t += valid ? (double)t1 + (double)t2 : 0.0;
+  if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;   // AddBackward0 + SubBackward0 (other)
   return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
 }
 
-// all three divisions of an element inside the fast-division range?  (STEQ: grad_x's by
-// the one-step STE quotient, valid for g inside ste_ok; the scale's range is the caller's)
-template <bool STEQ = false>
+// all three divisions of an element inside the fast-division range?
 __device__ __forceinline__ uint32_t lsq_fast_ok(float x, float g, const QP &p) {
   const float u = fdiv_fast(x, p.d);
   const float r = __builtin_rintf(u + p.z);
   const bool m = (r >= p.lo && r <= p.hi);
-  if (STEQ) return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & (m ? ste_ok(g) : 1u);
   const float gm = m ? g * p.s : 0.0f;
   return fdiv_ok(x, p.d) & fdiv_ok(u, p.d) & fdiv_ok(gm, p.d);
 }
 
-// The STEQ test of lsq_fast_ok<true> for a whole group, as two integer range trees
-// instead of per-element compares: every x, u = x/s and in-range g is +-0 or has
-// |bits| in [2^-40, 2^63] -- the intersection of fdiv_ok's [2^-63, 2^63] (x, u) and
-// ste_ok's [2^-40, 2^64) (g), so a group passing it passes lsq_fast_ok<true> (stricter
-// only for values the fallback paths compute with the same bits).  NaN / inf fail
-// (their bits are above 2^63).  Zeros wrap to 0xffffffff in the "- 1" tree.  The caller
-// checked ste_fast_s (which implies d.fast).
-__device__ __forceinline__ uint32_t lsq_fast_ok4(f4 xv, f4 gv, const QP &p) {
-  constexpr uint32_t kLo = 0x2b800000u, kHi = 0x5f000000u;   // 2^-40, 2^63
-  const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
-  uint32_t hi = 0u, lo = 0xffffffffu;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float u = VSIQ_EXP_K4_LEAN ? fdiv_fast_nz(xs[k], p.d) : fdiv_fast(xs[k], p.d);
-    const bool m = VSIQ_EXP_K4_LEAN ? lsq_rqm(u, p).m : [&] {
-      const float r = __builtin_rintf(u + p.z);
-      return r >= p.lo && r <= p.hi;
-    }();
-    const uint32_t a = __float_as_uint(xs[k]) & 0x7fffffffu, b = __float_as_uint(u) & 0x7fffffffu;
-    const uint32_t c = m ? (__float_as_uint(gs[k]) & 0x7fffffffu) : 0x3f800000u;   // 1.0: g unused
-    hi = max(hi, max(a, max(b, c)));
-    lo = min(lo, min(a - 1u, min(b - 1u, c - 1u)));
-  }
-  return (hi <= kHi && lo >= kLo - 1u) ? 1u : 0u;
-}
-
-// lsq_fast_ok4 with u's range implied by x's instead of tested: with s in (2^-60, 2^60)
-// (ste_fast_s), |x| in [s * 2^-61, s * 2^61] (both products exact: s * 2^-61 > 2^-121 is
-// normal) gives |x/s| in [2^-61, 2^61], so RN(x/s) is inside fdiv_ok's [2^-63, 2^63];
-// x = +-0 gives u = +-0.  One tree over x and the in-range g with the bounds
-// [max(2^-40, s * 2^-61), min(2^63, s * 2^61)] -- inside fdiv_ok (x) and ste_ok (g).
+// The STEQ element's conditions for a whole group, as two integer range trees instead
+// of per-element compares: every x/s and u/s inside fdiv_ok's [2^-63, 2^63] and every
+// in-range g inside ste_ok's [2^-40, 2^64).  u's range is implied by x's instead of
+// tested: with s in [2^-60, 2^60] (ste_fast_s), |x| in [s * 2^-61, s * 2^61] (both
+// products exact: s * 2^-61 >= 2^-121 is normal) gives |x/s| in [2^-61, 2^61], so RN(x/s)
+// is inside [2^-63, 2^63]; x = +-0 gives u = +-0.  One tree over x and the in-range g
+// with the bounds [max(2^-40, s * 2^-61), min(2^63, s * 2^61)] -- inside fdiv_ok (x) and
+// ste_ok (g).  NaN / inf fail (their bits are above 2^63); zeros wrap to 0xffffffff in
+// the "- 1" tree.  The caller checked ste_fast_s (which implies d.fast).
 __device__ __forceinline__ uint32_t lsq_fast_ok4x(f4 xv, f4 gv, const QP &p) {
   const uint32_t lo = max(0x2b800000u, __float_as_uint(p.d.b * 0x1p-61f));
   const uint32_t hi = min(0x5f000000u, __float_as_uint(p.d.b * 0x1p61f));
@@ -247,25 +191,15 @@ __device__ __forceinline__ f4 lsq_group_out(int64_t i, int64_t ng, int64_t n, f4
   const f4 xv = act_fwd4_at<ACT>(xc, 4 * i, L);
   const int nv = i < ng ? valid_in_group(i, n) : 0;
   f4 o;
-#ifndef VSIQ_EXP_K4_STEQ
-#define VSIQ_EXP_K4_STEQ 1   // experiments: 0 = grad_x by the general fast division (round 3)
-#endif
-#ifndef VSIQ_EXP_K4_GRPCHK
-#define VSIQ_EXP_K4_GRPCHK 2   // experiments: 0 = per-element lsq_fast_ok<true> compares, 1 = u tested too
-#endif
-  if (VSIQ_EXP_K4_STEQ && ste_fast_s(p.d) &&
-      (VSIQ_EXP_K4_GRPCHK == 2 && VSIQ_EXP_K4_LEAN ? lsq_fast_ok4x(xv, gv, p)
-       : VSIQ_EXP_K4_GRPCHK ? lsq_fast_ok4(xv, gv, p)
-                          : (lsq_fast_ok<true>(xv.x, gv.x, p) & lsq_fast_ok<true>(xv.y, gv.y, p) &
-                             lsq_fast_ok<true>(xv.z, gv.z, p) & lsq_fast_ok<true>(xv.w, gv.w, p)))) {
+  if (ste_fast_s(p.d) && lsq_fast_ok4x(xv, gv, p)) {
     o.x = lsq_elem<ZPL, false, true>(xv.x, gv.x, p, c, nv > 0);
     o.y = lsq_elem<ZPL, false, true>(xv.y, gv.y, p, c, nv > 1);
     o.z = lsq_elem<ZPL, false, true>(xv.z, gv.z, p, c, nv > 2);
     o.w = lsq_elem<ZPL, false, true>(xv.w, gv.w, p, c, nv > 3);
     return act_bwd4_at<ACT>(o, xc, 4 * i, L);
   }
-  const uint32_t ok = (VSIQ_EXP_K4 & 2) ? 1u : (lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) &
-                  lsq_fast_ok(xv.z, gv.z, p) & lsq_fast_ok(xv.w, gv.w, p));
+  const uint32_t ok = lsq_fast_ok(xv.x, gv.x, p) & lsq_fast_ok(xv.y, gv.y, p) & lsq_fast_ok(xv.z, gv.z, p) &
+                      lsq_fast_ok(xv.w, gv.w, p);
   if (ok) {
     o.x = lsq_elem<ZPL, false>(xv.x, gv.x, p, c, nv > 0);
     o.y = lsq_elem<ZPL, false>(xv.y, gv.y, p, c, nv > 1);

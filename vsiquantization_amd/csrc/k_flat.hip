@@ -632,11 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_observe_fq_grid(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-#ifndef VSIQ_EXP_K10
-#define VSIQ_EXP_K10 0   // experiments: 1 = no grid barrier, 2 = no record fold (wrong results; timing only)
-#endif
-  if (threadIdx.x == 0 && (VSIQ_EXP_K10 & 1)) s_ok = 1;
-  if (threadIdx.x == 0 && !(VSIQ_EXP_K10 & 1)) {   // grid barrier
+  if (threadIdx.x == 0) {   // grid barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(counter + kGridBarArrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t0 = wall_clock64();
@@ -657,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void k_observe_fq_grid(
   const int nrec = (int)gridDim.x * kWaves;
   double f[6];
   ObsFold::init(f);
-  for (int i = threadIdx.x; i < ((VSIQ_EXP_K10 & 2) ? 0 : nrec); i += kBlock) {
+  for (int i = threadIdx.x; i < nrec; i += kBlock) {
     const double *r = parts + (int64_t)i * VSIQ_PART_LEN;
     const double rr[6] = {partial_load(r + 0), partial_load(r + 1), partial_load(r + 2),
                           partial_load(r + 3), partial_load(r + 4), partial_load(r + 5)};
@@ -1049,6 +1045,9 @@ void launch_observe_loop(const float *x, int64_t n, double *stats_out, float *ru
 // workgroup and skip the record / arrival / fold chain.  (At 64K elements a single
 // workgroup's 8 serial load rounds cost more than the chain: 12.5 vs 6.8 us, MI355X.)
 constexpr int64_t kObsSingle = (int64_t)kBlock * kObsU;
+// K2 (per-call observer) reads tensors under this many MB with cached loads: the fake
+// quant re-reading it right after may hit the 256 MB Infinity Cache
+constexpr int64_t kObsTemporalMB = 256;
 
 // one-shot K2 has 2 / 4 / 16 groups-per-lane instances: K4's 8 runs as 4
 inline int obs_groups_per_lane(int64_t ng) {
@@ -1058,10 +1057,8 @@ inline int obs_groups_per_lane(int64_t ng) {
 
 inline int64_t observe_grid(int64_t ng) {
   if (g_tune.obs_kernel == 1) return lsq_grid(ng, obs_groups_per_lane(ng));
-  if (ng <= kObsSingle && g_tune.obs_grid == 0) return 1;
-  const int og = g_tune.obs_grid;
-  const int64_t cap = og > 0 ? og : kObsGrid;
-  return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(ng, (int64_t)kBlock * kObsU)));
+  if (ng <= kObsSingle) return 1;
+  return std::min<int64_t>(kObsGrid, std::max<int64_t>(1, cdiv(ng, (int64_t)kBlock * kObsU)));
 }
 
 template <int ACT>
@@ -1100,9 +1097,8 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
   const int64_t grid = observe_grid(cdiv(n, 4));
   if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
   if (ws_len < fold_records(grid) * kPartials) return VSIQ_E_WS;
-  // a tensor that fits the 256 MB Infinity Cache can be read with cached loads, so the fake
-  // quant that re-reads it right after (observe + quantize, K2 -> K1) may hit there
-  const bool nt = g_tune.nontemporal != 0 && !((n * 4) >> 20 < (int64_t)g_tune.obs_temporal_mb);
+  // kObsTemporalMB: observe + quantize (K2 -> K1) may re-read x from the Infinity Cache
+  const bool nt = g_tune.nontemporal != 0 && !((n * 4) >> 20 < kObsTemporalMB);
   VSIQ_ACT(act, launch_observe, vec, nt, x, n, stats_out, run_minmax, qp_out,
            symmetric, qden, eps, ws, counter, act_lay(act, n), (hipStream_t)stream);
   return launch_rc();
@@ -1111,14 +1107,7 @@ int observe(const float *x, int64_t n, int act, double *stats_out, float *run_mi
 // K2p groups per lane per step: 8 while the grid reaches 512 workgroups, else fewer so
 // that small layers still spread over >= ~512 workgroups (all CUs issuing; a 1.6M-
 // element layer at 8 per lane was 200 workgroups).  Fixed per n: deterministic.
-#ifndef VSIQ_EXP_PART_U
-#define VSIQ_EXP_PART_U 0          // experiments: force K2p groups per lane
-#endif
-#ifndef VSIQ_EXP_PART_CAP
-#define VSIQ_EXP_PART_CAP (VSIQ_PART_MAX_RECORDS / kWaves)   // experiments: K2p grid cap
-#endif
 inline int observe_part_u(int64_t n) {
-  if (VSIQ_EXP_PART_U) return VSIQ_EXP_PART_U;
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);   // lanes' worth of groups
   return units >= 512 * 8 ? 8 : (units >= 512 * 4 ? 4 : 2);
 }
@@ -1128,9 +1117,8 @@ inline int64_t observe_part_grid(int64_t n) {
   const int64_t units = cdiv(cdiv(n, 4), (int64_t)kBlock);
   const int u = observe_part_u(n);
   // large tensors: kObsGrid workgroups striding over the tensor; small: one step each
-  const int og = g_tune.obs_grid;
-  int64_t cap = og > 0 ? og : (u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS / kWaves);
-  cap = std::min<int64_t>(cap, VSIQ_EXP_PART_CAP);
+  static_assert(kObsGrid <= VSIQ_PART_MAX_RECORDS / kWaves, "K2p records");
+  const int64_t cap = u == 8 ? kObsGrid : VSIQ_PART_MAX_RECORDS / kWaves;
   return std::min<int64_t>(cap, std::max<int64_t>(1, cdiv(units, u)));
 }
 
@@ -1277,15 +1265,10 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen) {
 
 int vsiq_set_tuning(int key, int value) {
   switch (key) {
-    case VSIQ_TUNE_PC_ROWS_PER_BLOCK: g_tune.pc_rows_per_block = value; return 0;
     case VSIQ_TUNE_NONTEMPORAL: g_tune.nontemporal = value; return 0;
     case VSIQ_TUNE_OBS_KERNEL:
       if (value < 0 || value > 2) return VSIQ_E_ARG;
       g_tune.obs_kernel = value;
-      return 0;
-    case VSIQ_TUNE_OBS_GRID:
-      if (value != 0 && (value < 1 || value > kMaxReduceGrid)) return VSIQ_E_ARG;
-      g_tune.obs_grid = value;
       return 0;
     case VSIQ_TUNE_LSQ_GROUPS:
       if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16) return VSIQ_E_ARG;
@@ -1311,10 +1294,6 @@ int vsiq_set_tuning(int key, int value) {
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.xcd_order = value;
       return 0;
-    case VSIQ_TUNE_OBS_TEMPORAL_MB:
-      if (value < 0 || value > 4096) return VSIQ_E_ARG;
-      g_tune.obs_temporal_mb = value;
-      return 0;
     case VSIQ_TUNE_K2O_FORM:
       if (value != 0 && value != 1) return VSIQ_E_ARG;
       g_tune.k2o_form = value;
@@ -1326,10 +1305,6 @@ int vsiq_set_tuning(int key, int value) {
     case VSIQ_TUNE_K2O_BLOCK:
       if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
       g_tune.k2o_block = value;
-      return 0;
-    case VSIQ_TUNE_PC_BLOCK:
-      if (value != 0 && value != 256 && value != 512 && value != 1024) return VSIQ_E_ARG;
-      g_tune.pc_block = value;
       return 0;
     default: return VSIQ_E_ARG;
   }

@@ -30,8 +30,8 @@ namespace vsiq {
 namespace host {
 
 constexpr int64_t kChunk = 1 << 16;
-constexpr int64_t kPoolMinChunks = 4;
-constexpr int kLanes = 16;               // host_simd.cpp's accumulator lanes (one __m512 of fp32)   // below this the pool's wake-up costs more than it saves
+constexpr int64_t kPoolMinChunks = 4;   // below this the pool's wake-up costs more than it saves
+constexpr int kLanes = 16;               // host_simd.cpp's accumulator lanes (one __m512 of fp32)
 
 // VSIQ_HOST_THREADS, else the CPUs this process may run on: the affinity mask capped by
 // the cgroup v2 CPU quota (a shared GPU box can grant 16 CPUs' worth of time on a
@@ -61,8 +61,13 @@ inline int usable_cpus() {
 
 // Persistent workers (created on first use, usable_cpus() - 1 of them; the caller is the
 // last): run(nc, f) calls f(0..nc-1), each chunk exactly once, and returns when all are
-// done.  A call made while the pool is busy (another thread's host op) or in a forked
-// child (the workers do not exist there; DataLoader workers fork) runs serially.
+// done.  A call made while the pool is busy (another thread's host op), in a forked
+// child (the workers do not exist there; DataLoader workers fork) or from inside a chunk
+// of a running job (a per-channel row's own chunk loop, on a worker or on the caller)
+// runs serially; the last case is known from a thread-local flag, without the mutex.
+// A job of fewer than kPoolMinChunks chunks runs serially WITHOUT holding the pool, so
+// the calls inside its chunks can still use it (2 rows of 50M elements: both rows'
+// chunk loops on every worker).
 // Every job has its own counters (Job, held by shared_ptr): a worker still inside work()
 // for an earlier job only ever touches that job's counters, whose next >= nc, so it can
 // neither take a chunk of the new job nor miscount its completion.
@@ -75,8 +80,12 @@ class Pool {
 
   template <class F>
   void run(int64_t nc, F &&f) {
+    if (inside_ || nc < kPoolMinChunks || getpid() != pid_ || workers_.empty()) {
+      for (int64_t c = 0; c < nc; ++c) f(c);
+      return;
+    }
     std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-    if (!busy.owns_lock() || getpid() != pid_ || workers_.empty() || nc < kPoolMinChunks) {
+    if (!busy.owns_lock()) {
       for (int64_t c = 0; c < nc; ++c) f(c);
       return;
     }
@@ -89,7 +98,9 @@ class Pool {
       ++gen_;
     }
     cv_.notify_all();
+    inside_ = true;
     work(*job);
+    inside_ = false;
     {
       std::unique_lock<std::mutex> lk(job->mu);
       job->cv.wait(lk, [&] { return job->done.load() == nc; });
@@ -134,6 +145,7 @@ class Pool {
   }
 
   void loop() {
+    inside_ = true;   // a worker only ever runs chunks of a job
     uint64_t seen = 0;
     for (;;) {
       std::shared_ptr<Job> j;
@@ -148,6 +160,7 @@ class Pool {
     }
   }
 
+  static thread_local bool inside_;   // this thread is running a chunk of a job
   const pid_t pid_;
   std::vector<std::thread> workers_;
   std::mutex run_mu_, mu_;
@@ -156,6 +169,8 @@ class Pool {
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
+
+thread_local bool Pool::inside_ = false;
 
 // f(chunk, begin, end) over the fixed chunks of [0, n)
 template <class F>
@@ -399,8 +414,8 @@ int vsiq_host_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t n, 
 // state per row, quantizers/uniform.py:34-56 / 95 with the row's qparams), so every row
 // runs exactly the per-tensor host code above (the same bits as vsiq_host_observe_f32 /
 // _fq_fwd_f32 / _ste_bwd_f32 / _lsq_bwd_f32 on that row alone).  Rows go to the pool
-// (a row's own chunk loop then runs serially inside it), or, for fewer than 4 rows, one
-// after the other with the pool inside each row.
+// (a row's own chunk loop then runs serially inside it), or, for fewer than
+// kPoolMinChunks rows, one after the other with the pool inside each row.
 int vsiq_host_pc_observe_fq_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
                                 float *run_min, float *run_max, double *scale_out, double *zp_out,
                                 double *row_stats, int symmetric, double qden, double eps, int qmin, int qmax) {
@@ -431,45 +446,77 @@ int vsiq_host_pc_observe_fq_f32(const float *x, float *y, uint8_t *mask, int64_t
 
 int vsiq_host_pc_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen,
                             const double *scale, const double *zp, int zp_round, int qmin, int qmax) {
-  if (rows < 0 || rowlen < 0 || (rows > 0 && (!x || !y || !scale)) || qmin > qmax) return VSIQ_E_ARG;
+  return vsiq_host_pcm_fq_fwd_f32(x, y, mask, rows, rowlen, rows > 0 ? rows : 1, scale, zp, zp_round, qmin, qmax);
+}
+
+int vsiq_host_pc_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale) {
+  return vsiq_host_pcm_ste_bwd_f32(g, mask, gx, rows, rowlen, rows > 0 ? rows : 1, scale);
+}
+
+int vsiq_host_pc_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                             const double *scale, const double *zp, int zp_learn, int qmin, int qmax, double gscale,
+                             double *grad_scale_out, double *grad_zp_out) {
+  return vsiq_host_pcm_lsq_bwd_f32(g, x, gx, rows, rowlen, rows, scale, zp, zp_learn, qmin, qmax, gscale,
+                                   grad_scale_out, grad_zp_out);
+}
+
+// Axis 1 ([N, C, ...]): row r = n * channels + c in channel c, each row the per-tensor host
+// call with its channel's qparams; the learnable gradients summed per channel over its
+// rows in row order (f64), then times gscale once -- for channels == rows exactly the
+// per-row t * gscale of vsiq_host_lsq_bwd_f32.
+int vsiq_host_pcm_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t rows, int64_t rowlen, int64_t channels,
+                             const double *scale, const double *zp, int zp_round, int qmin, int qmax) {
+  if (rows < 0 || rowlen < 0 || channels <= 0 || rows % channels || (rows > 0 && (!x || !y || !scale)) ||
+      qmin > qmax)
+    return VSIQ_E_ARG;
   std::atomic<int> rc{0};
   Pool::get().run(rows, [&](int64_t r) {
+    const int64_t c = r % channels;
     const int e = vsiq_host_fq_fwd_f32(x + r * rowlen, y + r * rowlen, nullptr, mask ? mask + r * rowlen : nullptr,
-                                       rowlen, kActNone, nullptr, scale[r], zp ? zp[r] : 0.0, zp_round, 0, qmin,
+                                       rowlen, kActNone, nullptr, scale[c], zp ? zp[c] : 0.0, zp_round, 0, qmin,
                                        qmax);
     if (e) rc.store(e);
   });
   return rc.load();
 }
 
-int vsiq_host_pc_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
-                             const double *scale) {
-  if (rows < 0 || rowlen < 0 || (rows > 0 && (!g || !mask || !gx || !scale))) return VSIQ_E_ARG;
+int vsiq_host_pcm_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, int64_t rows, int64_t rowlen,
+                              int64_t channels, const double *scale) {
+  if (rows < 0 || rowlen < 0 || channels <= 0 || rows % channels || (rows > 0 && (!g || !mask || !gx || !scale)))
+    return VSIQ_E_ARG;
   std::atomic<int> rc{0};
   Pool::get().run(rows, [&](int64_t r) {
     const int64_t o = r * rowlen;
-    const int e = vsiq_host_ste_bwd_f32(g + o, mask + o, nullptr, gx + o, rowlen, kActNone, scale[r]);
+    const int e = vsiq_host_ste_bwd_f32(g + o, mask + o, nullptr, gx + o, rowlen, kActNone, scale[r % channels]);
     if (e) rc.store(e);
   });
   return rc.load();
 }
 
-int vsiq_host_pc_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
-                             const double *scale, const double *zp, int zp_learn, int qmin, int qmax, double gscale,
-                             double *grad_scale_out, double *grad_zp_out) {
-  if (rows <= 0 || rowlen <= 0 || !g || !x || !gx || !scale || !grad_scale_out || qmin > qmax ||
-      (zp_learn && !zp) || zp_learn < 0 || zp_learn > 1)
+int vsiq_host_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
+                              int64_t channels, const double *scale, const double *zp, int zp_learn, int qmin, int qmax,
+                              double gscale, double *grad_scale_out, double *grad_zp_out) {
+  if (rows <= 0 || rowlen <= 0 || channels <= 0 || rows % channels || !g || !x || !gx || !scale || !grad_scale_out ||
+      qmin > qmax || (zp_learn && !zp) || zp_learn < 0 || zp_learn > 1)
     return VSIQ_E_ARG;
+  std::vector<double> part((size_t)rows * 2);
   std::atomic<int> rc{0};
   Pool::get().run(rows, [&](int64_t r) {
-    const int64_t o = r * rowlen;
-    double go[2];
-    const int e = vsiq_host_lsq_bwd_f32(g + o, x + o, gx + o, rowlen, kActNone, scale[r], zp ? zp[r] : 0.0,
-                                        zp_learn, qmin, qmax, gscale, go);
-    grad_scale_out[r] = go[0];
-    if (grad_zp_out) grad_zp_out[r] = go[1];
+    const int64_t o = r * rowlen, c = r % channels;
+    const int e = vsiq_host_lsq_bwd_f32(g + o, x + o, gx + o, rowlen, kActNone, scale[c], zp ? zp[c] : 0.0,
+                                        zp_learn, qmin, qmax, 1.0, &part[(size_t)r * 2]);
     if (e) rc.store(e);
   });
+  for (int64_t c = 0; c < channels; ++c) {   // row order: independent of the thread count
+    double t = 0.0, z = 0.0;
+    for (int64_t r = c; r < rows; r += channels) {
+      t += part[(size_t)r * 2];
+      z += part[(size_t)r * 2 + 1];
+    }
+    grad_scale_out[c] = t * gscale;
+    if (grad_zp_out) grad_zp_out[c] = z * gscale;
+  }
   return rc.load();
 }
 

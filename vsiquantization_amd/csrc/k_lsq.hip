@@ -19,10 +19,7 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   LsqAcc c{0.0, 0.0};
   f4 o[G];
   lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o, L);
-#ifndef VSIQ_EXP_K4D_STORE_FIRST
-#define VSIQ_EXP_K4D_STORE_FIRST 1   // experiments: 0 = PART stores after the block record (round 3)
-#endif
-  if (PART && VSIQ_EXP_K4D_STORE_FIRST) {
+  if (PART) {
     // no arrival to order against: every wave issues its grad_x stores first, so the
     // block reduction runs while they drain (the one-round grids of small layers end
     // with it otherwise on the critical path)
@@ -37,18 +34,6 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   }
   double rec[2], f[2];
   if (!lsq_block_record<VEC, NT, G>(c, gx, n, blockIdx.x, o, rec)) return;   // waves 1..3 done
-  if (PART) {
-    if (threadIdx.x == 0) {
-      ws[2 * (int64_t)blockIdx.x] = rec[0];
-      ws[2 * (int64_t)blockIdx.x + 1] = rec[1];
-    }
-    lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
-    return;
-  }
-  if (VSIQ_EXP_K4 & 4) {   // experiment: no arrival / fold (gradient not produced)
-    lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);
-    return;
-  }
   const bool last = wave_arrive<LsqFold>(ws, 0, gridDim.x, blockIdx.x, counter, rec, f, [&]() {
     lsq_store_block<VEC, NT, G>(gx, n, blockIdx.x, o);   // wave 0's grad_x, after its arrival
   });

@@ -39,16 +39,15 @@ __device__ __forceinline__ void rowsums_add4(RowSums &r, f4 v, int nv) {
   r.s2 += (double)p2;
 }
 
-// Row reduction -> running state -> f64 qparams, returned to every lane.
-// LDS partials are double-buffered by `par`, so one barrier per row suffices.
+// Row reduction -> running state -> f64 qparams, returned to every lane (one barrier:
+// a workgroup reduces one row).
 template <bool STATS, int BS = kBlock>
 __device__ __forceinline__ QP pc_row_qparams(float mn, float mx, uint32_t nan, RowSums rs,
-                                             float rmn, float rmx, int64_t row, int par,
-                                             const PCArgs &a) {
+                                             float rmn, float rmx, int64_t row, const PCArgs &a) {
   constexpr int NW = BS / kWave;
-  __shared__ float s_mn[2][NW], s_mx[2][NW];
-  __shared__ uint32_t s_nan[2][NW];
-  __shared__ double s_rs[2][3][NW];
+  __shared__ float s_mn[NW], s_mx[NW];
+  __shared__ uint32_t s_nan[NW];
+  __shared__ double s_rs[3][NW];
   mn = wave_reduce(mn, MinOp());
   mx = wave_reduce(mx, MaxOp());
   nan = wave_reduce(nan, OrU());
@@ -59,14 +58,14 @@ __device__ __forceinline__ QP pc_row_qparams(float mn, float mx, uint32_t nan, R
   }
   const int w = threadIdx.x / kWave;
   if (threadIdx.x % kWave == 0) {
-    s_mn[par][w] = mn; s_mx[par][w] = mx; s_nan[par][w] = nan;
-    if (STATS) { s_rs[par][0][w] = rs.sa; s_rs[par][1][w] = rs.s1; s_rs[par][2][w] = rs.s2; }
+    s_mn[w] = mn; s_mx[w] = mx; s_nan[w] = nan;
+    if (STATS) { s_rs[0][w] = rs.sa; s_rs[1][w] = rs.s1; s_rs[2][w] = rs.s2; }
   }
   __syncthreads();
-  mn = s_mn[par][0]; mx = s_mx[par][0]; nan = s_nan[par][0];
+  mn = s_mn[0]; mx = s_mx[0]; nan = s_nan[0];
 #pragma unroll
   for (int i = 1; i < NW; ++i) {
-    mn = fminf(mn, s_mn[par][i]); mx = fmaxf(mx, s_mx[par][i]); nan |= s_nan[par][i];
+    mn = fminf(mn, s_mn[i]); mx = fmaxf(mx, s_mx[i]); nan |= s_nan[i];
   }
   if (!nan) {                         // minmax.py:44-47, strict compares
     if (mn < rmn) rmn = mn;
@@ -80,8 +79,8 @@ __device__ __forceinline__ QP pc_row_qparams(float mn, float mx, uint32_t nan, R
     a.scale_out[row] = s;
     a.zp_out[row] = z;
     if (STATS) {
-      double sa = s_rs[par][0][0], s1 = s_rs[par][1][0], s2 = s_rs[par][2][0];
-      for (int i = 1; i < NW; ++i) { sa += s_rs[par][0][i]; s1 += s_rs[par][1][i]; s2 += s_rs[par][2][i]; }
+      double sa = s_rs[0][0], s1 = s_rs[1][0], s2 = s_rs[2][0];
+      for (int i = 1; i < NW; ++i) { sa += s_rs[0][i]; s1 += s_rs[1][i]; s2 += s_rs[2][i]; }
       a.row_stats[row * 3 + 0] = sa;
       a.row_stats[row * 3 + 1] = s1;
       a.row_stats[row * 3 + 2] = s2;
@@ -112,7 +111,7 @@ __device__ __forceinline__ void pc_load_row(f4 (&v)[NV], const float *x, int64_t
 
 template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS>
 __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, float rmx,
-                                               int64_t row, int par, float *__restrict__ y,
+                                               int64_t row, float *__restrict__ y,
                                                uint8_t *__restrict__ codes,
                                                uint64_t *__restrict__ mask, const PCArgs &a,
                                                GateClk gc = GateClk{0}) {
@@ -131,7 +130,7 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
       if (STATS) rowsums_add4(rs, w, VEC ? 4 : valid_in_group(i, a.rowlen));
     }
   }
-  const QP p = pc_row_qparams<STATS, BS>(mn, mx, nan, rs, rmn, rmx, row, par, a);
+  const QP p = pc_row_qparams<STATS, BS>(mn, mx, nan, rs, rmn, rmx, row, a);
   if (!y) return;
   float *yr = y + row * a.rowlen;
   uint8_t *cr = CODES ? codes + row * a.rowlen : nullptr;
@@ -159,34 +158,22 @@ __device__ __forceinline__ void pc_process_row(const f4 (&v)[NV], float rmn, flo
   }
 }
 
-// RPB rows per workgroup (rows RPB*b .. RPB*b + RPB-1), straight-line code: every
-// row's loads are issued up front, so a workgroup's writes of row k overlap its
-// reads of row k+1 and hipcc's s_waitcnt counts stay exact (no loop).
+// One row per workgroup, straight-line code: the row's loads are all issued up front and
+// hipcc's s_waitcnt counts stay exact (no loop).  RPB (rows per workgroup) is 1: the
+// two-row form measured no faster (its parameter stays in the kernel's name, which the
+// profiles and tools/pmc_to_traffic.py match).
 template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS, int RPB>
 __global__ __launch_bounds__(BS) void k_pc_observe_fq(const float *__restrict__ x,
                                                       float *__restrict__ y,
                                                       uint8_t *__restrict__ codes,
                                                       uint64_t *__restrict__ mask, PCArgs a) {
+  static_assert(RPB == 1, "rows per block");
   const GateClk gc = gate_begin(a.gate);
-  const int64_t row0 = (int64_t)blockIdx.x * RPB;
-  const int64_t last = a.rows - 1;
-  f4 v[RPB][NV];
-  float rmn[RPB], rmx[RPB];
-#pragma unroll
-  for (int r = 0; r < RPB; ++r) {
-    const int64_t row = row0 + r < last ? row0 + r : last;
-    pc_load_row<NV, VEC, NT, BS>(v[r], x, row, a);
-    rmn[r] = a.run_min[row];
-    rmx[r] = a.run_max[row];
-  }
-  // RPB is 1 or 2; written out because the unroller refuses the (large) loop body
-  static_assert(RPB == 1 || RPB == 2, "rows per block");
-  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[0], rmn[0], rmx[0], row0, 0, y, codes, mask, a, gc);
-  if constexpr (RPB == 2) {
-    if (row0 + 1 <= last)   // uniform
-      pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v[RPB - 1], rmn[RPB - 1], rmx[RPB - 1],
-                                                          row0 + 1, 1, y, codes, mask, a);
-  }
+  const int64_t row = blockIdx.x;
+  f4 v[NV];
+  pc_load_row<NV, VEC, NT, BS>(v, x, row, a);
+  const float rmn = a.run_min[row], rmx = a.run_max[row];
+  pc_process_row<NV, VEC, NT, STATS, MASK, CODES, BS>(v, rmn, rmx, row, y, codes, mask, a, gc);
 }
 
 // Rows too long for registers: two passes over the row (the second from L2).
@@ -210,8 +197,8 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
     if (a.row_stats) rowsums_add4(rs, w, valid_in_group(i, a.rowlen));
   }
   const QP p = a.row_stats
-                   ? pc_row_qparams<true>(mn, mx, nan, rs, a.run_min[row], a.run_max[row], row, 0, a)
-                   : pc_row_qparams<false>(mn, mx, nan, rs, a.run_min[row], a.run_max[row], row, 0, a);
+                   ? pc_row_qparams<true>(mn, mx, nan, rs, a.run_min[row], a.run_max[row], row, a)
+                   : pc_row_qparams<false>(mn, mx, nan, rs, a.run_min[row], a.run_max[row], row, a);
   if (!y) return;
   float *yr = y + row * a.rowlen;
   uint64_t *mr = mask ? mask + row * mask_words_per_row(a.rowlen) : nullptr;
@@ -239,54 +226,40 @@ __global__ __launch_bounds__(kBlock) void k_pc_observe_fq_long(const float *__re
 }
 
 
-template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS, int RPB>
+template <int NV, bool VEC, bool NT, bool STATS, bool MASK, bool CODES, int BS>
 void launch_pc_k(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
-  const auto kern = k_pc_observe_fq<NV, VEC, NT, STATS, MASK, CODES, BS, RPB>;
+  const auto kern = k_pc_observe_fq<NV, VEC, NT, STATS, MASK, CODES, BS, 1>;
   PCArgs b = a;
   GateSel gs;
   if (a.gate == kGateAuto) {
     // one-round grids of >= 2 rows per CU: stores wait for the grid's read phase
     static const int occ = occupancy_blocks(reinterpret_cast<const void *>(kern), BS);
-    gs = store_gate_select("k3_pc_observe_fq", reinterpret_cast<const void *>(kern), cdiv(a.rows, RPB), occ,
+    gs = store_gate_select("k3_pc_observe_fq", reinterpret_cast<const void *>(kern), a.rows, occ,
                            a.rows * a.rowlen * (int64_t)sizeof(float), st);
     b.gate = gs.gate;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)cdiv(a.rows, RPB)), dim3(BS), 0, st, x, y, c, m, b);
+  hipLaunchKernelGGL(kern, dim3((unsigned)a.rows), dim3(BS), 0, st, x, y, c, m, b);
   store_gate_launched(gs, st);
 }
 
-template <int NV, bool VEC, bool NT, bool STATS, int BS, int RPB>
-void launch_pc_rpb(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
-  if (c && m) launch_pc_k<NV, VEC, NT, STATS, true, true, BS, RPB>(x, y, c, m, a, st);
-  else if (c) launch_pc_k<NV, VEC, NT, STATS, false, true, BS, RPB>(x, y, c, m, a, st);
-  else if (m) launch_pc_k<NV, VEC, NT, STATS, true, false, BS, RPB>(x, y, c, m, a, st);
-  else launch_pc_k<NV, VEC, NT, STATS, false, false, BS, RPB>(x, y, c, m, a, st);
-}
-
 template <int NV, bool VEC, bool NT, bool STATS, int BS>
-void launch_pc_nv(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int rpb,
-                  hipStream_t st) {
-  // two rows per workgroup only where the register file allows it
-  if constexpr (NV <= 9) {
-    if (rpb >= 2) {
-      launch_pc_rpb<NV, VEC, NT, STATS, BS, 2>(x, y, c, m, a, st);
-      return;
-    }
-  }
-  launch_pc_rpb<NV, VEC, NT, STATS, BS, 1>(x, y, c, m, a, st);
+void launch_pc_nv(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
+  if (c && m) launch_pc_k<NV, VEC, NT, STATS, true, true, BS>(x, y, c, m, a, st);
+  else if (c) launch_pc_k<NV, VEC, NT, STATS, false, true, BS>(x, y, c, m, a, st);
+  else if (m) launch_pc_k<NV, VEC, NT, STATS, true, false, BS>(x, y, c, m, a, st);
+  else launch_pc_k<NV, VEC, NT, STATS, false, false, BS>(x, y, c, m, a, st);
 }
 
 // groups per lane -> register-resident instantiation; false if the row is too long
 template <bool VEC, bool NT, bool STATS, int BS>
-bool launch_pc_bs(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, int rpb,
-                  hipStream_t st) {
+bool launch_pc_bs(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
   const int64_t per_lane = cdiv(cdiv(a.rowlen, 4), BS);
-  if (per_lane <= 1) launch_pc_nv<1, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
-  else if (per_lane <= 2) launch_pc_nv<2, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
-  else if (per_lane <= 3) launch_pc_nv<3, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
-  else if (per_lane <= 5) launch_pc_nv<5, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
-  else if (per_lane <= 9) launch_pc_nv<9, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
-  else if (per_lane <= 12) launch_pc_nv<12, VEC, NT, STATS, BS>(x, y, c, m, a, rpb, st);
+  if (per_lane <= 1) launch_pc_nv<1, VEC, NT, STATS, BS>(x, y, c, m, a, st);
+  else if (per_lane <= 2) launch_pc_nv<2, VEC, NT, STATS, BS>(x, y, c, m, a, st);
+  else if (per_lane <= 3) launch_pc_nv<3, VEC, NT, STATS, BS>(x, y, c, m, a, st);
+  else if (per_lane <= 5) launch_pc_nv<5, VEC, NT, STATS, BS>(x, y, c, m, a, st);
+  else if (per_lane <= 9) launch_pc_nv<9, VEC, NT, STATS, BS>(x, y, c, m, a, st);
+  else if (per_lane <= 12) launch_pc_nv<12, VEC, NT, STATS, BS>(x, y, c, m, a, st);
   else return false;
   return true;
 }

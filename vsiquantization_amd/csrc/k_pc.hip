@@ -3,24 +3,24 @@
 
 namespace vsiq {
 
-extern template bool launch_pc_bs<true, true, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, true, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, true, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, true, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, true, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, true, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<true, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-extern template bool launch_pc_bs<false, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+extern template bool launch_pc_bs<true, true, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 256>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, true, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, true, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, true, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<true, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, true, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+extern template bool launch_pc_bs<false, false, false, 1024>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
 
 template <bool VEC, bool NT, bool STATS>
 int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a, hipStream_t st) {
@@ -28,18 +28,14 @@ int launch_pc(const float *x, float *y, uint8_t *c, uint64_t *m, const PCArgs &a
   // workgroup size: the smallest that holds the row in <= 9 groups per lane
   // (measured on MI355X at 1024 x 9216: 256 lanes x 9 groups 13.0 us, 512 x 5 15.9,
   //  1024 x 3 17.4 -- more rows in flight per CU beats fewer groups per lane)
-  int bs = g_tune.pc_block;
-  if (bs <= 0) bs = ng <= 9 * 256 ? 256 : (ng <= 9 * 512 ? 512 : 1024);
-  // rows per workgroup: >= 2 lets a CU overlap row k's writes with row k+1's reads
-  int rpb = g_tune.pc_rows_per_block;
-  if (rpb <= 0) rpb = 1;
+  const int bs = ng <= 9 * 256 ? 256 : (ng <= 9 * 512 ? 512 : 1024);
   PCArgs b = a;
-  b.defer = (bs == 256 && rpb == 1) ? store_defer_units(a.rows, false) : 0;
+  b.defer = bs == 256 ? store_defer_units(a.rows, false) : 0;
   b.gate = kGateAuto;   // resolved per instantiation (launch_pc_k)
   bool ok = false;
-  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, b, rpb, st);
-  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, b, rpb, st);
-  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, b, rpb, st);
+  if (bs == 1024) ok = launch_pc_bs<VEC, NT, STATS, 1024>(x, y, c, m, b, st);
+  else if (bs == 512) ok = launch_pc_bs<VEC, NT, STATS, 512>(x, y, c, m, b, st);
+  else ok = launch_pc_bs<VEC, NT, STATS, 256>(x, y, c, m, b, st);
   if (!ok)
     hipLaunchKernelGGL((k_pc_observe_fq_long<VEC, NT>), dim3((unsigned)a.rows), dim3(kBlock), 0, st, x,
                        y, c, m, a);

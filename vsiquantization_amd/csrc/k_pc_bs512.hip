@@ -2,10 +2,10 @@
 #include "k_pc.cuh"
 
 namespace vsiq {
-template bool launch_pc_bs<true, true, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-template bool launch_pc_bs<true, true, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-template bool launch_pc_bs<true, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-template bool launch_pc_bs<true, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-template bool launch_pc_bs<false, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
-template bool launch_pc_bs<false, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, int, hipStream_t);
+template bool launch_pc_bs<true, true, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+template bool launch_pc_bs<true, true, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+template bool launch_pc_bs<true, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+template bool launch_pc_bs<true, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+template bool launch_pc_bs<false, false, true, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
+template bool launch_pc_bs<false, false, false, 512>(const float *, float *, uint8_t *, uint64_t *, const PCArgs &, hipStream_t);
 }  // namespace vsiq

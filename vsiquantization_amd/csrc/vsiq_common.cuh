@@ -60,13 +60,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // tuning knobs (vsiq_set_tuning); -1 / 0 = automatic.  Atomics: vsiq_set_tuning may run
 // on one host thread while another (autograd's backward thread) launches.
 struct Tuning {
-  std::atomic<int> pc_rows_per_block{0};   // K3 rows per workgroup (0 = auto)
-  std::atomic<int> pc_block{0};            // K3 workgroup size 256/512/1024 (0 = auto)
   std::atomic<int> nontemporal{1};         // nt hints on streamed loads/stores
   std::atomic<int> store_defer{-1};        // deferred store phase, units of 512 clocks (-1 = auto, 0 = off)
   std::atomic<int> pc_packed{1};           // per-channel with given qparams / K6: packed short rows (0 = per-row grid)
   std::atomic<int> obs_kernel{0};          // K2: 0 auto (grid-stride), 1 one-shot, 2 grid-stride
-  std::atomic<int> obs_grid{0};            // K2 grid-stride workgroups (0 = kObsGrid)
   std::atomic<int> lsq_groups{0};          // K4 groups per lane 2 / 4 / 8 / 16 (0 = by size)
   std::atomic<int> store_gate{-1};         // store gate ticks (10 ns) for one-round grids (-1 = auto, 0 = off)
   std::atomic<int> gate_autotune{1};       // store gate tuned online per launch site (0 = fixed estimate)
@@ -74,7 +71,6 @@ struct Tuning {
   std::atomic<int> k2o_form{0};            // K2o: 0 one-shot (one record per workgroup), 1 grid-stride (K2p's records)
   std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = default 2)
   std::atomic<int> k2o_block{0};           // K2o one-shot lanes per workgroup 256 / 512 / 1024 (0 = default 256)
-  std::atomic<int> obs_temporal_mb{256};   // K2: cached (temporal) loads for tensors under this many MB
 };
 extern Tuning g_tune;
 

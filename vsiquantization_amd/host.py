@@ -146,12 +146,27 @@ def observe_tensor(x, *, symmetric, num_bits=8, eps=1e-8, run_minmax=None, want_
     return qp, st
 
 
-# --------------------------------------------------------------------------- per-channel (axis 0)
+# --------------------------------------------------------------------------- per-channel
 def _rows(x):
     C = x.shape[0] if x.dim() > 0 else 1
     if C == 0 or x.numel() == 0:
         raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
     return C, x.numel() // C
+
+
+def _pc_view(x, axis):
+    """(rows, rowlen, channels) of per-channel ``axis`` 0 ([C, ...] weights: one row per
+    channel) or 1 ([N, C, ...] activations: N * C rows, row r in channel r % C) -- the
+    device path's view (fakequant._pc_view)."""
+    if axis == 0:
+        C, rowlen = _rows(x)
+        return C, rowlen, C
+    if axis != 1 or x.dim() < 2:
+        raise ValueError(f"per-channel axis must be 0 or 1 of a tensor with more dims, got {axis}")
+    C, rows = x.shape[1], x.shape[0] * x.shape[1]
+    if rows == 0 or x.numel() == 0:
+        raise RuntimeError("min(): Expected reduction dim to be specified for input.numel() == 0.")
+    return rows, x.numel() // rows, C
 
 
 def _row_f64(v, C, what):
@@ -193,43 +208,47 @@ def pc_observe_fq(x, *, symmetric, qmin, qmax, obs_bits=8, eps=1e-8, run_min=Non
                 row_stats=rstats)
 
 
-def pc_fake_quant(x, scale, zp, qmin, qmax, *, zp_round=False, want_mask=False):
-    """Per-channel (axis 0) fake quant with given [C] qparams on the host: (y, mask | None)."""
+def pc_fake_quant(x, scale, zp, qmin, qmax, *, zp_round=False, want_mask=False, axis=0):
+    """Per-channel fake quant with given [C] qparams along ``axis`` 0 or 1 on the host:
+    (y, mask | None)."""
     x = _f32(x)
-    C, rowlen = _rows(x)
+    rows, rowlen, C = _pc_view(x, axis)
     s = _row_f64(scale, C, "scale")
     z = _row_f64(zp, C, "zero point") if zp is not None else None
     y = torch.empty_like(x)
     mask = torch.empty(x.shape, dtype=torch.uint8) if want_mask else None
-    rc = H.lib().vsiq_host_pc_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(mask), _i64(C), _i64(rowlen), H.ptr(s), H.ptr(z),
-                                         int(bool(zp_round)), int(qmin), int(qmax))
-    H.check(rc, "vsiq_host_pc_fq_fwd_f32")
+    rc = H.lib().vsiq_host_pcm_fq_fwd_f32(H.ptr(x), H.ptr(y), H.ptr(mask), _i64(rows), _i64(rowlen), _i64(C),
+                                          H.ptr(s), H.ptr(z), int(bool(zp_round)), int(qmin), int(qmax))
+    H.check(rc, "vsiq_host_pcm_fq_fwd_f32")
     return y, mask
 
 
-def pc_ste_backward(g, mask, scale):
+def pc_ste_backward(g, mask, scale, axis=0):
     g = _f32(g, "grad_output")
-    C, rowlen = _rows(g)
+    rows, rowlen, C = _pc_view(g, axis)
     s = _row_f64(scale, C, "scale")
     gx = torch.empty_like(g)
-    rc = H.lib().vsiq_host_pc_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(gx), _i64(C), _i64(rowlen), H.ptr(s))
-    H.check(rc, "vsiq_host_pc_ste_bwd_f32")
+    rc = H.lib().vsiq_host_pcm_ste_bwd_f32(H.ptr(g), H.ptr(mask), H.ptr(gx), _i64(rows), _i64(rowlen), _i64(C),
+                                           H.ptr(s))
+    H.check(rc, "vsiq_host_pcm_ste_bwd_f32")
     return gx
 
 
 class PcFixedFn(torch.autograd.Function):
-    """Per-channel fake quant with given [C] qparams and the STE backward, on the host."""
+    """Per-channel fake quant with given [C] qparams and the STE backward, on the host
+    (``axis`` 0 or 1)."""
 
     @staticmethod
-    def forward(ctx, x, scale, zp, qmin, qmax):
-        y, mask = pc_fake_quant(x, scale, zp, qmin, qmax, want_mask=True)
-        ctx.save_for_backward(mask, _row_f64(scale, mask.shape[0], "scale"))
+    def forward(ctx, x, scale, zp, qmin, qmax, axis=0):
+        y, mask = pc_fake_quant(x, scale, zp, qmin, qmax, want_mask=True, axis=axis)
+        ctx.save_for_backward(mask, _row_f64(scale, _pc_view(x, axis)[2], "scale"))
+        ctx.axis = axis
         return y
 
     @staticmethod
     def backward(ctx, gy):
         mask, s = ctx.saved_tensors
-        return pc_ste_backward(gy, mask, s), None, None, None, None
+        return pc_ste_backward(gy, mask, s, ctx.axis), None, None, None, None, None
 
 
 class PcObserveFQFn(torch.autograd.Function):
@@ -251,39 +270,42 @@ class PcObserveFQFn(torch.autograd.Function):
 
 
 class PcLearnFn(torch.autograd.Function):
-    """Learnable per-channel (axis 0) fake quant on the host: each row the per-tensor
-    learnable host path with its own scale / zero point; [C] gradients times gscale."""
+    """Learnable per-channel fake quant on the host (``axis`` 0: [C, ...] weights, 1:
+    [N, C, ...] activations -- LSQFakeQuantize): each row the per-tensor learnable host
+    path with its channel's scale / zero point; [C] gradients (f64 sums over each channel's
+    rows) times gscale."""
 
     @staticmethod
-    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp):
+    def forward(ctx, x, scale, zero_point, qmin, qmax, gscale, learn_zp, axis=0):
         x = _f32(x)
-        y, _ = pc_fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp)
+        y, _ = pc_fake_quant(x, scale, zero_point, qmin, qmax, zp_round=learn_zp, axis=axis)
         ctx.save_for_backward(x)
         ctx.scale, ctx.zp = scale, zero_point
-        ctx.args = (int(qmin), int(qmax), float(gscale), int(bool(learn_zp)))
+        ctx.args = (int(qmin), int(qmax), float(gscale), int(bool(learn_zp)), axis)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
-        qmin, qmax, gscale, learn_zp = ctx.args
+        qmin, qmax, gscale, learn_zp, axis = ctx.args
         s, z = ctx.scale, ctx.zp
         g = _f32(gy, "grad_output")
-        C, rowlen = _rows(x)
+        rows, rowlen, C = _pc_view(x, axis)
         sr = _row_f64(s, C, "scale")
         zr = _row_f64(z, C, "zero point") if z is not None else None
         gx = torch.empty_like(g)
         gs = torch.empty(C, dtype=torch.float64)
         gz = torch.empty(C, dtype=torch.float64)
-        rc = H.lib().vsiq_host_pc_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(C), _i64(rowlen), H.ptr(sr),
-                                              H.ptr(zr), learn_zp, qmin, qmax, gscale, H.ptr(gs), H.ptr(gz))
-        H.check(rc, "vsiq_host_pc_lsq_bwd_f32")
+        rc = H.lib().vsiq_host_pcm_lsq_bwd_f32(H.ptr(g), H.ptr(x), H.ptr(gx), _i64(rows), _i64(rowlen), _i64(C),
+                                               H.ptr(sr), H.ptr(zr), learn_zp, qmin, qmax, gscale, H.ptr(gs),
+                                               H.ptr(gz))
+        H.check(rc, "vsiq_host_pcm_lsq_bwd_f32")
         out_s = out_z = None
         if isinstance(s, torch.Tensor) and ctx.needs_input_grad[1]:
             out_s = gs.to(device=s.device, dtype=s.dtype).reshape(s.shape)
         if learn_zp and isinstance(z, torch.Tensor) and ctx.needs_input_grad[2]:
             out_z = gz.to(device=z.device, dtype=z.dtype).reshape(z.shape)
-        return gx, out_s, out_z, None, None, None, None
+        return gx, out_s, out_z, None, None, None, None, None
 
 
 def threads() -> int:

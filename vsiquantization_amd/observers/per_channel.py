@@ -89,24 +89,24 @@ class PerChannelMinMaxObserver(BaseObserver):
         Returns (y, row_stats | None); y carries the STE gradient."""
         # the training step's call (public-API C2 step): straight to a C++ op bound to this
         # observer's state and the quantizer's range, which checks x itself (None back: the
-        # general path below); rebuilt when the state or the range changes
+        # general path below); rebuilt when either running tensor or the range changes
         op = self.__dict__.get("_op")
-        if (op is not None and not want_row_stats and op[0] is self.run_min
-                and op[1] == (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax)
+        if (op is not None and not want_row_stats and op[0] is self.run_min and op[1] is self.run_max
+                and op[2] == (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax)
                 and H.torch_ext_enabled()):
-            r = op[2](x)
+            r = op[3](x)
             if r is not None:
                 y, self.scale, self.zero_point = r
                 return y, None
         if (not want_row_stats and H.torch_ext_enabled() and isinstance(x, torch.Tensor) and x.is_cuda
                 and x.dtype == torch.float32 and x.requires_grad and x.is_contiguous() and torch.is_grad_enabled()):
             mn, mx = self._state(x)
-            op = self._op = (mn, (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax),
+            op = self._op = (mn, mx, (self.symmetric, self.num_bits, self.eps, quantizer.qmin, quantizer.qmax),
                              H.torch_ext().PcObserveFqOp(mn, mx, bool(self.symmetric), int(quantizer.qmin),
                                                          int(quantizer.qmax),
                                                          qden(self.symmetric, self.num_bits, self.eps),
                                                          float(self.eps)))
-            r = op[2](x)
+            r = op[3](x)
             if r is not None:
                 y, self.scale, self.zero_point = r
                 return y, None

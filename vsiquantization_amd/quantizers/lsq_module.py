@@ -16,15 +16,18 @@ batch (and ``theta`` / ``gamma`` for weights), and ``forward`` flow:
 The fake quant itself runs in the HIP kernels: per-tensor K1 forward + K4 backward,
 per-channel (the reference broadcasts the parameters along dim 1,
 lsq_module.py:141-143) K3-fixed forward + K6 backward -- bit-exact fp32 forward and
-grad_x, f64-summed parameter gradients.  The observer (torch.ao, third-party) and
-the experimental adaptive rounding (``flag_adaptive``, theta/gamma) keep the
-reference's torch implementation.
+grad_x, f64-summed parameter gradients.  CPU tensors take the native host loops
+(host.py: per tensor vsiq_host_*, per channel vsiq_host_pcm_* over the [N, C, ...]
+rows), with the same bits.  The observer (torch.ao, third-party) and the experimental
+adaptive rounding (``flag_adaptive``, theta/gamma; the reference never sets it,
+lsq_module.py:93) keep the reference's torch implementation.
 """
 from __future__ import annotations
 
 import torch
 from torch.ao.quantization import FakeQuantize, MovingAverageMinMaxObserver
 
+from .. import host as _host
 from ..fakequant import PerChannelFQFn, PerChannelLearnFn, fake_quant_fixed, fake_quant_learn
 
 
@@ -116,13 +119,17 @@ class LSQFakeQuantize(FakeQuantize):
                     return self._adaptive_reference(X, grad_scale, qmin, qmax)
                 return self._learnable(X, grad_scale, qmin, qmax)
             scale, zero_point = self.scale, self.zero_point
-            if self.flag_adaptive or (self.is_per_channel and X.device.type == "cpu"):
+            if self.flag_adaptive:
                 if self.is_per_channel:
                     view = [1] + [-1] + [1] * (len(X.shape) - 2)
                     scale, zero_point = scale.view(view), zero_point.view(view)
                 return self._fq_reference(X, scale, zero_point, qmin, qmax)
             if self.is_per_channel:
                 self._check_channels(X, scale)
+                if X.device.type == "cpu":   # the host loops, [N, C, ...] rows
+                    if X.requires_grad and torch.is_grad_enabled():
+                        return _host.PcFixedFn.apply(X, scale, zero_point, qmin, qmax, 1)
+                    return _host.pc_fake_quant(X, scale, zero_point, qmin, qmax, axis=1)[0]
                 return PerChannelFQFn.apply(X, scale, zero_point, qmin, qmax, 1)
             return fake_quant_fixed(X, scale, zero_point, qmin, qmax)
         return X
@@ -135,10 +142,10 @@ class LSQFakeQuantize(FakeQuantize):
 
     def _learnable(self, X, grad_scale, qmin, qmax):
         s, z = self.scale_param, self.zero_point_param_float
-        if self.is_per_channel and X.device.type == "cpu":   # no per-channel host loops: torch's CPU ops
-            return self._adaptive_reference(X, grad_scale, qmin, qmax)
         if self.is_per_channel:
             self._check_channels(X, s)
+            if X.device.type == "cpu":   # the host loops, [N, C, ...] rows
+                return _host.PcLearnFn.apply(X, s, z, qmin, qmax, float(grad_scale), True, 1)
             return PerChannelLearnFn.apply(X, s, z, qmin, qmax, float(grad_scale), True, 1)
         return fake_quant_learn(X, s, z, qmin, qmax, float(grad_scale), True)
 
