@@ -1067,9 +1067,12 @@ def settle_gates(W, cap=4000, world=1):
     for line in H.gate_report().splitlines():
         f = line.split()
         kv = dict(x.split("=") for x in f[1:] if "=" in x)
+        # every candidate gate the tuner timed at this site: [ticks, median us] (ticks 0 = no
+        # gate), so a line shows whether another gate would have won on its box
+        cands = [[int(t), float(us)] for t, us in (x.split(":") for x in f[1:] if ":" in x)]
         sites.append({"site": f[0], "grid": int(kv["grid"]), "read_bytes": int(kv["bytes"]),
                       "est_ticks": int(float(kv["est"])), "gate_ticks": int(kv["best"]),
-                      "tuned": kv["done"] == "1"})
+                      "tuned": kv["done"] == "1", "retunes": int(kv.get("retunes", 0)), "candidates": cands})
     return n, sites
 
 
@@ -1588,7 +1591,12 @@ def compact_summary(out) -> str:
     if "batched_act_quant" in out:
         parts.append(leg("act", out["batched_act_quant"]))
     api = {k: round(v, 1) for k, v in out.items() if k.startswith("api_") and isinstance(v, (int, float))}
-    gates = ",".join(f"{s['site']}:{s['gate_ticks']}" for s in out.get("store_gate", {}).get("sites", []))
+    def gate(s):   # chosen gate (its median us / the no-gate median us)
+        c = dict((t, us) for t, us in s.get("candidates", []))
+        if s["gate_ticks"] in c and 0 in c:
+            return f"{s['site']}:{s['gate_ticks']}({c[s['gate_ticks']]:.2f}/{c[0]:.2f}us)"
+        return f"{s['site']}:{s['gate_ticks']}"
+    gates = ",".join(gate(s) for s in out.get("store_gate", {}).get("sites", []))
     return "[bench summary] " + " | ".join(parts) + f" | api {api} | gates {gates}"
 
 

@@ -127,3 +127,21 @@ def test_compact_summary_is_short_and_complete():
     assert s.startswith("[bench summary]") and len(s) < 1500
     assert "pc_observe_fq_fwd=0.740" in s and "alt=" not in s and "k3:515" in s and "api_us_per_step" in s
     assert "c5 " in s and "act " in s and "cpu=100.0" in s
+    out["store_gate"]["sites"][0]["candidates"] = [[0, 13.41], [489, 12.93], [515, 12.71], [541, 12.80]]
+    assert "k3:515(12.71/13.41us)" in bench.compact_summary(out)
+
+
+def test_gate_report_candidates_parsed(monkeypatch):
+    """settle_gates keeps every timed candidate of a site ([ticks, median us])."""
+    from vsiquantization_amd import _hip as H
+    rep = "k3_pc_observe_fq dev=0 grid=1024 bytes=37748736 est=503 done=1 best=528 retunes=1 watch=256 0:13.41 453:12.95 528:12.70\n"
+    monkeypatch.setattr(H, "gate_tuning_pending", lambda: 0)
+    monkeypatch.setattr(H, "gate_report", lambda: rep)
+    monkeypatch.setattr(bench.torch.cuda, "synchronize", lambda *a: None)
+
+    class W:
+        def launch(self, i):
+            return 0
+    n, sites = bench.settle_gates(W())
+    assert n == 8 and sites[0]["gate_ticks"] == 528 and sites[0]["retunes"] == 1
+    assert sites[0]["candidates"] == [[0, 13.41], [453, 12.95], [528, 12.70]]

@@ -32,7 +32,7 @@ def test_tuned_gate_bits_identical_to_oracle(shape):
     rowlen = w.size // shape[0]
     _reset()
     ys, gxs = [], []
-    for i in range(140):   # > 12 candidates x 8 samples per site
+    for i in range(200):   # > 12 candidates x 8 samples + 3 finalists x 8 more, per site
         r = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255, want_mask=True)
         gx = FQ.ste_backward(gd, r["mask"], r["scale"], rowlen)
         if i % 7 == 0:
@@ -110,14 +110,14 @@ def test_gate_retune_api_retunes_every_site_bits_identical():
     the moment); the outputs stay bit-identical throughout."""
     x, want = _k3_inputs()
     _reset()
-    for _ in range(140):
+    for _ in range(200):
         FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)
     torch.cuda.synchronize()
     assert H.gate_tuning_pending() == 0 and " done=1 " in _site_line("k3_pc_observe_fq")
     assert H.gate_retune() >= 1
     assert " done=0 " in _site_line("k3_pc_observe_fq")
     ys = []
-    for i in range(140):
+    for i in range(200):
         y = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"]
         if i % 10 == 0:
             ys.append(y.clone())
@@ -136,7 +136,7 @@ def test_gate_drift_under_concurrent_load_retunes():
     about 2048 launches), so the site re-tunes by itself; the outputs stay bit-identical."""
     x, want = _k3_inputs()
     _reset()
-    for i in range(140):
+    for i in range(200):
         FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)
         if i % 16 == 15:
             torch.cuda.synchronize()

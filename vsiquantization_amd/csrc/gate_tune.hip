@@ -6,8 +6,14 @@
 // a pair of HIP events on the launch stream; later calls harvest finished pairs
 // (hipEventQuery, never a host sync; the events skip the system-scope fence, so timing a
 // launch neither writes back / invalidates the caches nor slows the launches after it),
-// and once every candidate has kSamples times the
-// smallest median wins and is used from then on.  All state is behind one mutex
+// and once every candidate has kSamples times, the kFinal candidates with the smallest
+// medians are timed kSamples more each (round 5: neighbouring gates differ by less than
+// the spread of 8 samples on some boxes) and the smallest median over all of a
+// finalist's samples wins and is used from then on.  The candidates are issued in a
+// fresh pseudo-random order every pass (round 5): sites launched alternately (K3 then the
+// STE backward in a training step) would otherwise always time candidate i of one site
+// right after candidate i of the other, and a gate's median would carry its partner's
+// tail.  All state is behind one mutex
 // (autograd's backward thread launches too); launches under HIP-graph capture take the
 // current choice and are never timed.
 //
@@ -36,6 +42,7 @@ namespace {
 constexpr double kFactors[] = {0.0, 0.90, 0.95, 0.975, 1.0, 1.025, 1.05, 1.075, 1.10, 1.15, 1.20, 1.30};
 constexpr int kCand = sizeof(kFactors) / sizeof(kFactors[0]);
 constexpr int kSamples = 8;        // timed launches per candidate
+constexpr int kFinal = 3;          // finalists of the refinement round, kSamples more each
 constexpr double kDefault = 1.05;  // before (or without) tuning
 constexpr double kCapUs = 40.0;
 constexpr int kWatchEvery = 128;   // a tuned site times one launch in this many
@@ -51,7 +58,11 @@ struct Site {
   uint32_t ticks[kCand] = {};
   std::vector<float> ms[kCand];
   int issued[kCand] = {};
-  int rr = 0;
+  int perm[kCand] = {};             // this pass's issue order
+  int pos = kCand;                  // next index into perm (kCand: reshuffle)
+  uint64_t rng = 0;                 // xorshift state, seeded per site
+  bool refine = false;              // the finalists' round
+  int target[kCand] = {};           // samples wanted per candidate in this round
   bool done = false;
   uint32_t best = 0;
   float best_ms = 0.0f;             // the winner's median when tuned
@@ -93,15 +104,30 @@ float median(std::vector<float> v) {
   return n % 2 ? v[n / 2] : 0.5f * (v[n / 2 - 1] + v[n / 2]);
 }
 
+void start_round(Site &s) {
+  for (int c = 0; c < kCand; ++c) s.target[c] = kSamples;
+  s.refine = false;
+}
+
 void finish_if_complete(Site &s) {
   if (s.done) return;
   for (int c = 0; c < kCand; ++c)
-    if ((int)s.ms[c].size() < kSamples) return;
-  int bc = 0;
-  float bm = median(s.ms[0]);
-  for (int c = 1; c < kCand; ++c) {
+    if ((int)s.ms[c].size() < s.target[c]) return;
+  if (!s.refine) {   // coarse round complete: the kFinal best medians get kSamples more
+    int order[kCand];
+    float med[kCand];
+    for (int c = 0; c < kCand; ++c) order[c] = c, med[c] = median(s.ms[c]);
+    std::stable_sort(order, order + kCand, [&](int a, int b) { return med[a] < med[b]; });
+    for (int k = 0; k < kFinal; ++k) s.target[order[k]] = 2 * kSamples;
+    s.refine = true;
+    return;
+  }
+  int bc = -1;
+  float bm = 0.0f;
+  for (int c = 0; c < kCand; ++c) {
+    if (s.target[c] <= kSamples) continue;   // not a finalist
     const float m = median(s.ms[c]);
-    if (m < bm) { bm = m; bc = c; }
+    if (bc < 0 || m < bm) { bm = m; bc = c; }
   }
   s.best = s.ticks[bc];
   s.best_ms = bm;
@@ -117,7 +143,8 @@ void retune(Site &s) {
     s.ms[c].clear();
     s.issued[c] = 0;
   }
-  s.rr = 0;
+  start_round(s);
+  s.pos = kCand;
   s.prev_best = s.best;
   s.done = false;
   s.watch.clear();
@@ -202,6 +229,8 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     s.dev = dev;
     s.est = est;
     for (int c = 0; c < kCand; ++c) s.ticks[c] = clamp_ticks(kFactors[c] * est, khz);
+    s.rng = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uintptr_t)kernel ^ ((uint64_t)grid << 20) ^ (uint64_t)read_bytes;
+    start_round(s);
   }
   int cand = -2;
   if (s.done) {
@@ -225,12 +254,21 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
       sel.gate = s.best;
       return sel;
     }
-    for (int k = 0; k < kCand; ++k) {
-      const int j = (s.rr + k) % kCand;
-      if (s.issued[j] < kSamples) { c = j; break; }
+    for (int k = 0; k < 2 * kCand && c < 0; ++k) {
+      if (s.pos == kCand) {   // a new pass: Fisher-Yates over the candidates
+        for (int i = 0; i < kCand; ++i) s.perm[i] = i;
+        for (int i = kCand - 1; i > 0; --i) {
+          s.rng ^= s.rng << 13;
+          s.rng ^= s.rng >> 7;
+          s.rng ^= s.rng << 17;
+          std::swap(s.perm[i], s.perm[s.rng % (uint64_t)(i + 1)]);
+        }
+        s.pos = 0;
+      }
+      const int j = s.perm[s.pos++];
+      if (s.issued[j] < s.target[j]) c = j;
     }
     if (c < 0) return sel;   // every sample issued, results still in flight
-    s.rr = (c + 1) % kCand;
   } else if (!s.done) {
     return sel;   // the harvest above started a re-tune: plain launch this time
   }
