@@ -27,5 +27,10 @@ for W in ${WORKLOADS:-c1 c2 c3 c4 c5}; do
     run pmc_${W}_$C 600 rocprofv3 --pmc $C -d gpurun_out/pmc_${TAG}_${W}_$C -o run --output-format csv \
         -- python3 -u bench.py --workload $W --steps $SP --warmup $WP --no-cpu-baseline || exit $?
   done
+  # reduce on the box (gpurun copies back at most 64 MiB): the PMC passes -> HBM bytes per
+  # launch, then keep only the kernel-stats summaries of the traces
+  python3 tools/pmc_to_traffic.py gpurun_out/pmc_traffic_${TAG}.json \
+      $W=gpurun_out/pmc_${TAG}_${W}_FETCH_SIZE,gpurun_out/pmc_${TAG}_${W}_WRITE_SIZE > /dev/null || exit $?
+  find gpurun_out/prof_${TAG}_$W gpurun_out/pmc_${TAG}_${W}_* -type f ! -name '*kernel_stats.csv' -delete
 done
 exit 0
