@@ -1047,13 +1047,25 @@ def settle_gates(W, cap=4000, world=1):
     time candidate gates.  A choice of delay only -- results are identical for every gate.
     With several ranks the stop is agreed (MAX of the ranks' pending counts), so every
     rank runs the same steps -- a workload whose step holds a collective would otherwise
-    hang.  Returns (steps run, one dict per tuned site)."""
+    hang.  The steps run in the timed region's pattern (launch_group: a group's forwards,
+    then its backwards), so each site is tuned in the order its timed launches run in -- a
+    K3 gate tuned between STE launches is up to 4 % slow for K3 launches that follow K3
+    launches (tools/exp/c2_floor.py).  Returns (steps run, one dict per tuned site)."""
     from vsiquantization_amd import _hip as H
+    grouped = hasattr(W, "launch_group")
+    if grouped:
+        g = max(1, int(W.group))
+        ev = [timing_event() for _ in range(len(W.kernels) + 1)]
     n = 0
     while n < cap:   # at least one round, so that every launch site exists
-        for _ in range(8):
-            assert W.launch(n) == 0
-            n += 1
+        k = 0
+        while k < 8:
+            if grouped:
+                assert W.launch_group(n, g, ev) == 0
+                n, k = n + g, k + g
+            else:
+                assert W.launch(n) == 0
+                n, k = n + 1, k + 1
         torch.cuda.synchronize()
         pending = H.gate_tuning_pending()
         if world > 1:

@@ -179,3 +179,60 @@ def test_calibrate_qat_model_reads_per_batch_equal_per_call_path():
     for qa, qc in zip(_managers(a), _managers(c)):
         assert not qa._pending_records and not qc._pending_records
         assert _read(qa) == _read(qc)
+
+
+@pytest.mark.parametrize("mode", ["queued", "async"])
+def test_reads_with_queued_or_async_deferred_calls(mode, monkeypatch):
+    """The opt-in K2m queue (VSIQ_OBSERVE_BATCH=1: calls observed in batches) and the
+    side-stream observers (async_observers=True): a read mid-calibration flushes / joins
+    first, so the records equal the per-call path's."""
+    import vsiquantization_amd.observe_batch as OB
+
+    def recording(log):
+        def calib(model, loader, device):
+            model.eval()
+            for imgs, _ in loader:
+                model(imgs.to(device).float() / 255.0)
+                log.append([_read(qm) for qm in _managers(model)])
+            model.train()
+        return calib
+
+    a = _model()
+    b = copy.deepcopy(a)
+    la, lb = [], []
+    if mode == "queued":
+        monkeypatch.setenv("VSIQ_OBSERVE_BATCH", "1")
+        calibrate_qat_model(a, _loader(), recording(la), DEV)
+        monkeypatch.delenv("VSIQ_OBSERVE_BATCH")
+        assert OB.pending() == 0
+    else:
+        calibrate_qat_model(a, _loader(), recording(la), DEV, async_observers=True)
+    calibrate_qat_model(b, _loader(), recording(lb), DEV, defer_observers=False)
+    for ra, rb in zip(la, lb):
+        for x, y in zip(ra, rb):
+            _assert_read_equal(x, y)
+
+
+def test_copy_and_pickle_mid_calibration_fold_their_own_records(tmp_path):
+    """A deep copy (EMA / teacher) or a torch.save of a manager taken while its deferred
+    calls are pending: each copy folds its own copied records (the observer re-links to
+    its own manager), the original is untouched by the copy's reads."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    xs = [torch.randn(5, 777, device=DEV, generator=g) * (i + 1) for i in range(3)]
+    qm = _deferred_manager(8, False)
+    for x in xs[:2]:
+        qm.quantize(x)
+    cp = copy.deepcopy(qm)
+    path = tmp_path / "qm.pt"
+    torch.save(qm, path)
+    ld = torch.load(path, weights_only=False)   # our own file, written just above
+    assert cp.observer._defer_owner() is cp and ld.observer._defer_owner() is ld
+    want2 = O.observe_minmax(xs[1].cpu().numpy(), *O.observe_minmax(xs[0].cpu().numpy()))
+    for c in (cp, ld):
+        assert (c.observer.min_val, c.observer.max_val) == want2
+        assert not c._pending_records
+    assert len(qm._pending_records) == 2   # the copies' reads did not fold the original
+    qm.quantize(xs[2])
+    want3 = O.observe_minmax(xs[2].cpu().numpy(), *want2)
+    assert (qm.observer.min_val, qm.observer.max_val) == want3
+    assert len(qm.mean_abs_x) == 3 and len(cp.mean_abs_x) == 2

@@ -50,6 +50,13 @@ class MinMaxObserver(BaseObserver):
         self._dirty = False
         self._obs_stream = None     # side stream with pending updates (async calibration)
 
+    def __getstate__(self):
+        # the owner link is a weakref (not picklable) to the manager this observer belongs
+        # to; a copy's manager re-links its own copy (QuantizationManager.__setstate__)
+        state = self.__dict__.copy()
+        state.pop("_defer_owner", None)
+        return state
+
     # ------------------------------------------------------------------ state
     def _join(self):
         """Make the current stream wait for updates queued on a side stream."""

@@ -171,6 +171,13 @@ class QuantizationManager(nn.Module):
             self._fold_pending()   # the calls before this write happened first
         nn.Module.__setattr__(self, name, value)
 
+    def __setstate__(self, state):
+        # a deep copy / unpickle taken while deferred calls were pending: the copied
+        # observer folds into THIS manager's copied records, never the original's
+        super().__setstate__(state)
+        if self.__dict__.get("_pending_records") and isinstance(self.__dict__.get("observer"), MinMaxObserver):
+            self.observer._defer_owner = weakref.ref(self)
+
     def _defer_begin(self):
         """First deferred call since the last fold: keep the running state the replay
         starts from, and route reads of the qparams / observer state to _fold_pending."""
