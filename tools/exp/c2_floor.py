@@ -4,10 +4,12 @@ vsiq_pc_observe_fq_f32) at the floor of its traffic mix on this box?  At C2's sh
 sweep (ticks of the 100 MHz wall clock; 0 = no gate), R launches back to back, event-timed:
 
   * K3 with the gate forced (VSIQ_TUNE_STORE_GATE),
+  * the STE backward (vsiq_ste_bwd_f32: read g + the mask bits, write grad_x) with the
+    same gate,
   * a plain gated copy of the same grid shape (c2_floor.hip: 9 float4 loads per lane, the
     gate, 9 stores; no reduction, no mask).
 
-Prints us per launch for both and K3 / plain at each gate and at each one's best gate.
+Prints us per launch for each and kernel / plain at each one's best gate.
 usage: python tools/exp/c2_floor.py [reps]"""
 import ctypes
 import os
@@ -44,6 +46,8 @@ def main():
     run = torch.zeros(2, rows, device=dev)
     qp = torch.empty(2, rows, dtype=torch.float64, device=dev)
     qd = qden(False, 8, 1e-8)
+    gs = [torch.randn(rows, rowlen, device=dev, generator=g) for _ in range(sl)]
+    gxs = [torch.empty_like(xs[0]) for _ in range(sl)]
 
     def k3(i):
         j = i % sl
@@ -51,6 +55,11 @@ def main():
                                           H.c_i64(rows), H.c_i64(rowlen), P(run[0].data_ptr()),
                                           P(run[1].data_ptr()), P(qp[0].data_ptr()), P(qp[1].data_ptr()), None, 0,
                                           0, 255, qd, 1e-8, st)
+
+    def ste(i):
+        j = i % sl
+        return lib.vsiq_ste_bwd_f32(P(gs[j].data_ptr()), P(mask.data_ptr()), P(gxs[j].data_ptr()),
+                                    H.c_i64(rows * rowlen), P(qp[0].data_ptr()), H.c_i64(rowlen), 0.0, st)
 
     def plain(gate):
         return lambda i: ex.exp_copy_gated(P(xs[i % sl].data_ptr()), P(ys[i % sl].data_ptr()), rows, rowlen, gate, st)
@@ -74,21 +83,23 @@ def main():
     gates = [0] + list(range(440, 701, 13))
     res = []
     print(f"C2 shape {rows}x{rowlen}, {sl} buffers, {reps} launches per timing (min of 3)")
-    print(" gate   K3 us   plain us   K3/plain(time)")
+    print(" gate   K3 us  STE us  plain us")
     try:
         for gt in gates:
             H.set_tuning(H.TUNE_STORE_GATE, gt)
             a = t(k3)
+            c = t(ste)
             b = t(plain(gt))
-            res.append((gt, a, b))
-            print(f"{gt:5d} {a:7.2f} {b:9.2f}   {b / a:.3f}", flush=True)
+            res.append((gt, a, b, c))
+            print(f"{gt:5d} {a:7.2f} {c:7.2f} {b:9.2f}", flush=True)
     finally:
         H.set_tuning(H.TUNE_STORE_GATE, -1)
-    ka = min(res, key=lambda r: r[1])
     pa = min(res, key=lambda r: r[2])
-    print(f"best K3 {ka[1]:.2f} us at gate {ka[0]} = {alg / ka[1] / 1e6:.0f} GB/s ({alg / ka[1] / 8e6:.3f} of 8 TB/s)")
-    print(f"best plain copy {pa[2]:.2f} us at gate {pa[0]} = {alg / pa[2] / 1e6:.0f} GB/s ({alg / pa[2] / 8e6:.3f})")
-    print(f"K3 at its best / plain at its best: {pa[2] / ka[1]:.3f} of the plain kernel's rate")
+    print(f"best plain copy {pa[2]:.2f} us at gate {pa[0]} = {alg / pa[2] / 1e3:.0f} GB/s ({alg / pa[2] / 8e6:.3f} of 8 TB/s)")
+    for name, col in (("K3", 1), ("STE", 3)):
+        ka = min(res, key=lambda r: r[col])
+        print(f"best {name} {ka[col]:.2f} us at gate {ka[0]} = {alg / ka[col] / 1e3:.0f} GB/s "
+              f"({alg / ka[col] / 8e6:.3f} of 8 TB/s); {pa[2] / ka[col]:.3f} of the plain copy's rate")
 
 
 if __name__ == "__main__":
