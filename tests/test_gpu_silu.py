@@ -193,13 +193,16 @@ def test_silu_act_code_layout():
 
 
 @pytest.mark.parametrize("act", ["relu", "silu", None])
-@pytest.mark.parametrize("n", [7, 4096, 100_003, 3 * 2**20 + 4, 26 * 2**20 + 3])
+@pytest.mark.parametrize("n", [7, 4096, 100_003, 3 * 2**20 + 4, 4_718_592, 6_553_600, 13_107_203, 18_874_368,
+                               26 * 2**20 + 3])
 def test_observe_parts_out_equals_act_then_parts(n, act, pin):
     """K2o (vsiq_act_observe_part_out_f32): y = act(c) and the deferred records in one
     pass.  y == the activation alone == the oracle, bit for bit; the folded records ==
     K2p's fold in min / max / NaN count / n exactly and in the sums to float64 summation
     order (one record per one-shot workgroup instead of one per grid-stride wave); the
-    legacy grid-stride form (VSIQ_TUNE_K2O_FORM 1) gives K2p's records bit for bit."""
+    legacy grid-stride form (VSIQ_TUNE_K2O_FORM 1) gives K2p's records bit for bit.
+    4.7M..18.9M elements take the one-round gated form (C5's 6.6M / 13M layers; its
+    bounds: 2 and 8 workgroups per CU of 9 groups per lane)."""
     pin(32, 7)
     c, _ = _inputs(n, n + 5)
     x = cu(c)

@@ -287,10 +287,13 @@ __global__ __launch_bounds__(kBlock) void k_observe_part_out(const float *__rest
 // reduction runs before the stores (no fence between the y stores and the barrier).
 // Measured on MI355X (profiles/r04b_k2o_*): G = 2 streams best at every C5 size (52M
 // elements: 68.1 us = 0.77 of 8 TB/s, vs 76.8 us at G = 16 and 96 % of the activation
-// alone); BS trades the record count (the sync's fold) against the tail.
+// alone); BS trades the record count (the sync's fold) against the tail.  `gate`: the
+// one-round G = 9 form's store gate (round 5, launch_k2o_gated; 0 = none), like K1's.
 template <bool VEC, bool NT, int ACT, int G, int BS>
 __global__ __launch_bounds__(BS) void k_observe_part_out1(const float *__restrict__ x, float *__restrict__ y,
-                                                           int64_t n, double *__restrict__ parts, SiluLay L) {
+                                                           int64_t n, double *__restrict__ parts, SiluLay L,
+                                                           uint32_t gate) {
+  const GateClk gc = gate_begin(gate);
   constexpr int NW = BS / kWave;
   __shared__ float s_mn[NW], s_mx[NW];
   __shared__ uint32_t s_nan[NW];
@@ -334,6 +337,7 @@ __global__ __launch_bounds__(BS) void k_observe_part_out1(const float *__restric
     s_sa[w] = a.sa; s_s1[w] = a.s1; s_s2[w] = a.s2;
   }
   __syncthreads();
+  gate_pass(gate, gc);
   if (whole) {
     float *yb = y + 4 * base;
 #pragma unroll
@@ -1210,7 +1214,7 @@ template <bool VEC, bool NT, int ACT, int BS>
 void launch_k2o1_bs(int g, int64_t grid, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
                     hipStream_t st) {
 #define K2O1(G_) hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, G_, BS>), dim3((unsigned)grid), dim3(BS), 0, \
-                                    st, c, y, n, parts, L)
+                                    st, c, y, n, parts, L, 0u)
   switch (g) {
     case 1: K2O1(1); break;
     case 2: K2O1(2); break;
@@ -1235,6 +1239,37 @@ void launch_k2o1_act(bool vec, bool nt, int g, int bs, int64_t grid, const float
   if (vec && nt) launch_k2o1<true, true, ACT>(g, bs, grid, c, y, n, parts, L, st);
   else if (vec) launch_k2o1<true, false, ACT>(g, bs, grid, c, y, n, parts, L, st);
   else launch_k2o1<false, false, ACT>(g, bs, grid, c, y, n, parts, L, st);
+}
+
+// K2o's one-round form (round 5): where 9 groups per lane of 256 lanes make a grid of 2..occ
+// workgroups per CU (every workgroup resident at once; on MI355X 4.7M..18.9M elements --
+// C5's 6.6M / 13M layers), one pass of loads, the record, the store gate (tuned online
+// per site like K1's, gate_tune.hip), then the stores: reads and writes as two phases
+// instead of interleaved.  The form is chosen by the shape alone (not by the gate), so a
+// call's records are fixed per n; the gate is only a delay.  Records: one per workgroup,
+// fewer than the G = 2 form's that size the slot (k2o_records).
+template <int ACT, bool VEC, bool NT>
+bool launch_k2o_gated_vn(const float *c, float *y, int64_t n, double *parts, const SiluLay &L, hipStream_t st) {
+  constexpr int kG = 9, kBS = 256;
+  const int64_t ng = cdiv(n, 4);
+  const int64_t grid = cdiv(ng, (int64_t)kBS * kG);
+  const void *kern = reinterpret_cast<const void *>(k_observe_part_out1<VEC, NT, ACT, kG, kBS>);
+  static const int occ = occupancy_blocks(kern, kBS);
+  const int64_t cus = device_cus();
+  if (grid < 2 * cus || grid > (int64_t)occ * cus || grid * kBS * kG - ng > ng / 8) return false;
+  GateSel gs = store_gate_select("k2o_observe_out", kern, grid, occ, 4 * n, st);
+  hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, kG, kBS>), dim3((unsigned)grid), dim3(kBS), 0, st, c, y, n,
+                     parts, L, gs.gate);
+  store_gate_launched(gs, st);
+  return true;
+}
+
+template <int ACT>
+bool launch_k2o_gated(bool vec, bool nt, const float *c, float *y, int64_t n, double *parts, const SiluLay &L,
+                      hipStream_t st) {
+  if (vec && nt) return launch_k2o_gated_vn<ACT, true, true>(c, y, n, parts, L, st);
+  if (vec) return launch_k2o_gated_vn<ACT, true, false>(c, y, n, parts, L, st);
+  return launch_k2o_gated_vn<ACT, false, false>(c, y, n, parts, L, st);
 }
 
 extern "C" {
@@ -1377,6 +1412,10 @@ int vsiq_act_observe_part_out_f32(const float *c, float *y, int64_t n, int act, 
     const int64_t grid = k2o_records(n);
     if (grid > 0x7fffffffLL) return VSIQ_E_ARG;
     if (parts_len < grid * VSIQ_PART_LEN) return VSIQ_E_WS;
+    // default shape knobs: the one-round gated form where the size allows it
+    if (g_tune.k2o_groups == 0 && g_tune.k2o_block == 0 &&
+        VSIQ_ACT(act, launch_k2o_gated, vec, nt, c, y, n, parts, L, st))
+      return launch_rc();
     VSIQ_ACT(act, launch_k2o1_act, vec, nt, k2o_groups(), k2o_block(), grid, c, y, n, parts, L, st);
     return launch_rc();
   }
