@@ -13,7 +13,17 @@
 // fresh pseudo-random order every pass (round 5): sites launched alternately (K3 then the
 // STE backward in a training step) would otherwise always time candidate i of one site
 // right after candidate i of the other, and a gate's median would carry its partner's
-// tail.  All state is behind one mutex
+// tail.
+//
+// Bursts (round 5): where a site is launched back to back -- the next launch of the same
+// site is the next launch through the tuner, on the same stream, within kBurstGapUs of
+// host time -- a sample spans up to kBurst consecutive launches with the same gate (its
+// end event re-recorded after each), and counts their mean.  A lone launch's timing
+// includes how the GPU comes out of the previous, different kernel; launches that stream
+// back to back (a bench's group of one kernel, several layers of one shape in a row)
+// have a different, sharper optimum (tools/exp/c2_floor.py: K3 at C2 12.0 us at 518
+// ticks, 12.95 at 557, where lone-launch medians were flat within their noise).  A
+// training step's launches of one site are a step apart: their samples stay single.  All state is behind one mutex
 // (autograd's backward thread launches too); launches under HIP-graph capture take the
 // current choice and are never timed.
 //
@@ -29,6 +39,7 @@
 #include "vsiq_common.cuh"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -49,6 +60,8 @@ constexpr int kWatchEvery = 128;   // a tuned site times one launch in this many
 constexpr int kWatchMax = 128 * 64;
 constexpr int kWatch = 8;          // samples per drift check
 constexpr double kDrift = 0.15;    // relative change of the median that triggers re-tuning
+constexpr int kBurst = 4;          // launches per burst sample
+constexpr double kBurstGapUs = 25.0;   // host time between the launches of a burst, at most
 
 struct Site {
   std::string label;
@@ -74,6 +87,9 @@ struct Site {
   int retunes = 0;
   int gen = 0;                      // tuning round: retune() starts a new one
   uint64_t last_sel = 0;            // g_sel when this site was last launched
+  struct Sample *open = nullptr;    // burst in progress (not in g_pending yet)
+  uint64_t open_sel = 0;            // g_sel at the burst's last launch
+  std::chrono::steady_clock::time_point open_t;   // host time of the burst's last launch
 };
 
 struct Sample {
@@ -82,7 +98,13 @@ struct Sample {
   int cand = 0;   // -1: a drift sample of the tuned gate
   int dev = 0;
   int gen = 0;    // the site's tuning round when issued: samples of an earlier round are dropped
+  int n = 0;      // launches the sample spans (end event recorded after each)
+  hipStream_t st = nullptr;
 };
+
+double us_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+}
 
 using Key = std::tuple<const void *, int64_t, int64_t, int>;
 
@@ -165,6 +187,19 @@ void watch_sample(Site &s, float ms) {
   if (s.drifting >= 2) retune(s);
 }
 
+// caller holds g_mu: an open burst becomes a sample to harvest
+void close_burst_locked(Site &s) {
+  if (!s.open) return;
+  g_pending.push_back(s.open);
+  s.open = nullptr;
+}
+
+// caller holds g_mu; all: every open burst, else those whose last launch is past the gap
+void close_bursts_locked(bool all) {
+  for (auto &kv : g_sites)
+    if (kv.second.open && (all || us_since(kv.second.open_t) >= kBurstGapUs)) close_burst_locked(kv.second);
+}
+
 // caller holds g_mu
 void harvest_locked() {
   size_t keep = 0;
@@ -177,7 +212,8 @@ void harvest_locked() {
     }
     float ms = 0.0f;
     const bool current = p->gen == p->site->gen;
-    if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f) {
+    if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f && p->n > 0) {
+      ms /= (float)p->n;
       if (!current) {
         // a sample of the round before a re-tune: not counted in the new round's issued[]
       } else if (p->cand < 0) {
@@ -221,6 +257,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   }
   std::lock_guard<std::mutex> lk(g_mu);
   Site &s = g_sites[Key{kernel, grid, read_bytes, dev}];
+  const bool adjacent = s.open && s.open_sel == g_sel;   // no other tuned launch since the burst's last
   s.last_sel = ++g_sel;
   if (s.grid == 0) {
     s.label = label;
@@ -231,6 +268,19 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     for (int c = 0; c < kCand; ++c) s.ticks[c] = clamp_ticks(kFactors[c] * est, khz);
     s.rng = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uintptr_t)kernel ^ ((uint64_t)grid << 20) ^ (uint64_t)read_bytes;
     start_round(s);
+  }
+  if (s.open) {
+    Sample *o = s.open;
+    hipStreamCaptureStatus ocs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(st, &ocs) != hipSuccess || ocs != hipStreamCaptureStatusNone;
+    if (capturing) (void)hipGetLastError();
+    if (adjacent && !capturing && o->st == st && o->n < kBurst && o->gen == s.gen &&
+        us_since(s.open_t) < kBurstGapUs) {   // the burst goes on, same gate
+      sel.gate = o->cand >= 0 ? s.ticks[o->cand] : s.best;
+      sel.timing = o;
+      return sel;
+    }
+    close_burst_locked(s);
   }
   int cand = -2;
   if (s.done) {
@@ -294,6 +344,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   p->cand = c;
   p->dev = dev;
   p->gen = s.gen;
+  p->st = st;
   if (c >= 0) {
     s.issued[c]++;
     sel.gate = s.ticks[c];
@@ -307,18 +358,29 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
   Sample *p = static_cast<Sample *>(sel.timing);
   sel.timing = nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
+  Site &s = *p->site;
   if (hipEventRecord(p->b, st) != hipSuccess) {
     (void)hipGetLastError();
-    if (p->cand >= 0 && p->gen == p->site->gen) p->site->issued[p->cand]--;
+    if (s.open == p) s.open = nullptr;
+    if (p->n > 0) {   // the burst's earlier launches: b holds the last of them
+      g_pending.push_back(p);
+      return;
+    }
+    if (p->cand >= 0 && p->gen == s.gen) s.issued[p->cand]--;
     g_pool[p->dev].emplace_back(p->a, p->b);
     delete p;
     return;
   }
-  g_pending.push_back(p);
+  ++p->n;
+  s.open = p;   // open until kBurst launches, another tuned launch, a gap or a read-out
+  s.open_sel = g_sel;
+  s.open_t = std::chrono::steady_clock::now();
+  if (p->n >= kBurst) close_burst_locked(s);
 }
 
 int gate_sites_tuning() {
   std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
   harvest_locked();
   int n = 0;
   for (auto &kv : g_sites)
@@ -329,6 +391,7 @@ int gate_sites_tuning() {
 
 int64_t gate_report(char *buf, int64_t len) {
   std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
   harvest_locked();
   std::string out;
   char line[512];
@@ -356,6 +419,7 @@ int64_t gate_report(char *buf, int64_t len) {
 
 int gate_retune() {
   std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
   harvest_locked();
   int n = 0;
   for (auto &kv : g_sites) {
@@ -367,6 +431,7 @@ int gate_retune() {
 
 int gate_reset() {
   std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
   harvest_locked();
   if (!g_pending.empty()) return 1;   // samples in flight keep their sites alive
   g_sites.clear();
