@@ -25,7 +25,9 @@ DEV = "cuda:0"
 @pytest.mark.parametrize("learn_zp", [False, True])
 def test_part_and_fold_equal_k4_and_oracle(act, learn_zp):
     rng = np.random.default_rng(17 + int(learn_zp))
-    sizes = [1, 7, 1000, 65536, 1 << 20, 3 * (1 << 20) + 3] + [4096 + 13 * k for k in range(66)]   # 72 calls
+    # + the one-round gated K4d form's sizes (k4d_one_round: 4.7M..9.4M elements, C4's 6.6M layers)
+    sizes = ([1, 7, 1000, 65536, 1 << 20, 3 * (1 << 20) + 3, 4_718_592, 6_553_600 + 5, 9_437_184]
+             + [4096 + 13 * k for k in range(66)])   # 75 calls
     qmin, qmax = (0, 15) if learn_zp else (-8, 7)
     calls = []
     for n in sizes:
