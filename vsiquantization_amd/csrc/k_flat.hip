@@ -1241,27 +1241,36 @@ void launch_k2o1_act(bool vec, bool nt, int g, int bs, int64_t grid, const float
   else launch_k2o1<false, false, ACT>(g, bs, grid, c, y, n, parts, L, st);
 }
 
-// K2o's one-round form (round 5): where 9 groups per lane of 256 lanes make a grid of 2..occ
-// workgroups per CU (every workgroup resident at once; on MI355X 4.7M..18.9M elements --
-// C5's 6.6M / 13M layers), one pass of loads, the record, the store gate (tuned online
-// per site like K1's, gate_tune.hip), then the stores: reads and writes as two phases
-// instead of interleaved.  The form is chosen by the shape alone (not by the gate), so a
-// call's records are fixed per n; the gate is only a delay.  Records: one per workgroup,
-// fewer than the G = 2 form's that size the slot (k2o_records).
-template <int ACT, bool VEC, bool NT>
-bool launch_k2o_gated_vn(const float *c, float *y, int64_t n, double *parts, const SiluLay &L, hipStream_t st) {
-  constexpr int kG = 9, kBS = 256;
+// K2o's one-round forms (round 5): where 9 groups per lane of 256 lanes make a grid of
+// 2..occ workgroups per CU (every workgroup resident at once; on MI355X 4.7M..18.9M
+// elements -- C5's 6.6M / 13M layers), one pass of loads, the record, the store gate
+// (tuned online per site like K1's, gate_tune.hip), then the stores: reads and writes as
+// two phases instead of interleaved.  Smaller calls whose default 2-groups-per-lane grid
+// is one round (C5's 1.6M / 3.3M layers) get the gate on that grid.  The form is chosen
+// by the shape alone (not by the gate), so a call's records are fixed per n; the gate
+// is only a delay.  Records: one per workgroup, never more than the G = 2 form's that
+// size the slot (k2o_records).
+template <int ACT, bool VEC, bool NT, int G>
+bool launch_k2o_gated_g(const float *c, float *y, int64_t n, double *parts, const SiluLay &L, hipStream_t st) {
+  constexpr int kBS = 256;
   const int64_t ng = cdiv(n, 4);
-  const int64_t grid = cdiv(ng, (int64_t)kBS * kG);
-  const void *kern = reinterpret_cast<const void *>(k_observe_part_out1<VEC, NT, ACT, kG, kBS>);
+  const int64_t grid = cdiv(ng, (int64_t)kBS * G);
+  const void *kern = reinterpret_cast<const void *>(k_observe_part_out1<VEC, NT, ACT, G, kBS>);
   static const int occ = occupancy_blocks(kern, kBS);
   const int64_t cus = device_cus();
-  if (grid < 2 * cus || grid > (int64_t)occ * cus || grid * kBS * kG - ng > ng / 8) return false;
+  if (grid < 2 * cus || grid > (int64_t)occ * cus || grid * kBS * G - ng > ng / 8) return false;
   GateSel gs = store_gate_select("k2o_observe_out", kern, grid, occ, 4 * n, st);
-  hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, kG, kBS>), dim3((unsigned)grid), dim3(kBS), 0, st, c, y, n,
+  hipLaunchKernelGGL((k_observe_part_out1<VEC, NT, ACT, G, kBS>), dim3((unsigned)grid), dim3(kBS), 0, st, c, y, n,
                      parts, L, gs.gate);
   store_gate_launched(gs, st);
   return true;
+}
+
+template <int ACT, bool VEC, bool NT>
+bool launch_k2o_gated_vn(const float *c, float *y, int64_t n, double *parts, const SiluLay &L, hipStream_t st) {
+  static_assert(kK2oGroups == 2 && kK2oBlock == 256, "the G = 2 gated form is the default grid");
+  return launch_k2o_gated_g<ACT, VEC, NT, 2>(c, y, n, parts, L, st) ||
+         launch_k2o_gated_g<ACT, VEC, NT, 9>(c, y, n, parts, L, st);
 }
 
 template <int ACT>

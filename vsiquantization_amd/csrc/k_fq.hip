@@ -15,26 +15,35 @@ __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, 
   fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, gc, gate, L);
 }
 
-// One-round grids of 9 groups per lane with the store gate where that applies
-// (store_gate_select: >= 2 workgroups per CU, all resident), else kFlatU groups per lane.
+// One-round grids get the store gate (store_gate_select: >= 2 workgroups per CU, all
+// resident): the kFlatU grid where it is one round (round 5: C4's 3.3M / 6.6M-element
+// layers), else 9 groups per lane where that is (13M), else kFlatU ungated.
 template <bool VEC, bool NT, bool CODES, bool MASK, int ACT>
 void launch_fq_k(const float *x, float *y, uint8_t *codes, uint64_t *mask, int64_t n,
                  const QPSrc &src, const SiluLay &L, hipStream_t st) {
   const int64_t ng = cdiv(n, 4);
-  const int64_t grid9 = cdiv(ng, (int64_t)kBlock * 9);
+  const int64_t grid9 = cdiv(ng, (int64_t)kBlock * 9), gridu = oneshot_grid(ng);
+  const void *kern9 = reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>);
+  const void *kernu = reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>);
+  static const int occ9 = occupancy_blocks(kern9, kBlock);
+  static const int occu = occupancy_blocks(kernu, kBlock);
+  const int64_t cus = device_cus();
   GateSel gs;
-  if (g_tune.store_gate != 0 && grid9 * kBlock * 9 - ng <= ng / 8) {
-    const void *kern = reinterpret_cast<const void *>(k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>);
-    static const int occ = occupancy_blocks(kern, kBlock);
-    gs = store_gate_select("k1_fq_fwd", kern, grid9, occ, 4 * n, st);
+  if (g_tune.store_gate != 0 && gridu >= 2 * cus && gridu <= (int64_t)occu * cus) {
+    gs = store_gate_select("k1_fq_fwd_flat", kernu, gridu, occu, 4 * n, st);
+  } else if (g_tune.store_gate != 0 && grid9 * kBlock * 9 - ng <= ng / 8 && grid9 >= 2 * cus &&
+             grid9 <= (int64_t)occ9 * cus) {
+    gs = store_gate_select("k1_fq_fwd", kern9, grid9, occ9, 4 * n, st);
+    if (gs.gate) {
+      hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), dim3((unsigned)grid9), dim3(kBlock), 0, st,
+                         x, y, codes, mask, n, src, gs.gate, L);
+      store_gate_launched(gs, st);
+      return;
+    }
   }
-  if (gs.gate)
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, 9>), dim3((unsigned)grid9), dim3(kBlock), 0, st,
-                       x, y, codes, mask, n, src, gs.gate, L);
-  else
-    hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>), dim3((unsigned)oneshot_grid(ng)),
-                       dim3(kBlock), 0, st, x, y, codes, mask, n, src, 0u, L);
-  store_gate_launched(gs, st);   // a tuning sample of "no gate" times the kFlatU grid
+  hipLaunchKernelGGL((k_fq_fwd<VEC, NT, CODES, MASK, ACT, kFlatU>), dim3((unsigned)gridu), dim3(kBlock), 0, st, x,
+                     y, codes, mask, n, src, gs.gate, L);
+  store_gate_launched(gs, st);   // for the 9-group site: a tuning sample of "no gate" times the kFlatU grid
 }
 
 template <int ACT, bool VEC, bool NT>

@@ -7,7 +7,7 @@ namespace vsiq {
 // PART: the block record {sum t, sum z} goes to ws[2 * block] with a plain store and
 // the block leaves -- no drain, no arrival, no fold (vsiq_act_lsq_bwd_part_f32: the
 // fold of every layer's records runs later in one launch, k_lsq_fold_multi).  `gate`:
-// the one-round PART form's store gate (round 5, k4d_one_round; 0 = none).
+// the one-round PART grids' store gate (round 5, launch_lsq_g; 0 = none).
 template <bool VEC, bool NT, bool ZPL, int ACT, int G, bool PART = false>
 __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     const float *__restrict__ x,
@@ -54,9 +54,10 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
                   double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                   const SiluLay &L, hipStream_t st) {
   if (!counter) {   // records only (PART)
-    // the one-round form (9 groups per lane, k4d_one_round): the tuned store gate
+    // a one-round grid (store_gate_select takes grids of 2..occ workgroups per CU only):
+    // the tuned store gate between the read and the write phase
     GateSel gs;
-    if constexpr (G == 9) {
+    if constexpr (G == 2) {
       const void *kern = zpl ? reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, true, ACT, G, true>)
                              : reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, false, ACT, G, true>);
       static const int occ_t = occupancy_blocks(reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, true, ACT, G, true>),
@@ -89,20 +90,13 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
 // the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
 // (1 group per lane for the small layers measured slower still: 10.4 against 9.8 us at
 // 3.3M elements, 214 against 201 us at 105M, profiles/r04h_c4_k4d.txt.)
-// Round 5: where 9 groups per lane make a grid of 2..4 workgroups per CU (on MI355X 4.7M
-// ..9.4M elements: C4's 6.6M-element layers), one round of 9 groups per lane with the
-// tuned store gate between the read and the write phase (as K1 / K2o), instead of 2.
-// The rule is the shape's alone (records per call fixed per n: vsiq_lsq_part_records).
-inline bool k4d_one_round(int64_t n) {
-  const int64_t ng = cdiv(n, 4);
-  const int64_t grid = cdiv(ng, (int64_t)kBlock * 9);
-  const int64_t cus = device_cus();
-  return grid >= 2 * cus && grid <= 4 * cus && grid * kBlock * 9 - ng <= ng / 8;
-}
-
-inline int lsq_part_groups_per_lane(int64_t n) {
+// Round 5: where that 2-groups-per-lane grid is one round (2..occ workgroups per CU, all
+// resident: C4's 3.3M / 6.6M-element layers) its stores wait behind the tuned store gate
+// (launch_lsq_g).  A one-round grid of 9 groups per lane with the gate was slower at 6.6M
+// (16.2-16.4 against 15.2 us, profiles/r05/r05j_c4*.log).
+inline int lsq_part_groups_per_lane(int64_t) {
   const int g = g_tune.lsq_groups;
-  return g > 0 ? g : (k4d_one_round(n) ? 9 : 2);
+  return g > 0 ? g : 2;
 }
 
 template <int ACT, bool VEC, bool NT>
@@ -110,9 +104,7 @@ void launch_lsq_act(const float *g, const float *x, float *gx, int64_t n, const 
                     double gscale, double *grad_out, double *ws, uint32_t *counter, int64_t grid,
                     const SiluLay &L, hipStream_t st) {
   const int per_lane = counter ? lsq_groups_per_lane(cdiv(n, 4)) : lsq_part_groups_per_lane(n);
-  if (per_lane == 9 && !counter)
-    launch_lsq_g<ACT, VEC, NT, 9>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
-  else if (per_lane == kLsqGroups)
+  if (per_lane == kLsqGroups)
     launch_lsq_g<ACT, VEC, NT, kLsqGroups>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);
   else if (per_lane == 8)
     launch_lsq_g<ACT, VEC, NT, 8>(g, x, gx, n, src, zpl, gscale, grad_out, ws, counter, grid, L, st);

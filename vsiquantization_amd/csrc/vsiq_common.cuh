@@ -36,24 +36,15 @@ constexpr int kWave = 64;
 constexpr int kWaves = kBlock / kWave;
 constexpr int kMaxReduceGrid = 2048;   // minimum partial-record slots of a workspace
 constexpr int kPartials = 8;           // doubles per partial record
-#ifndef VSIQ_ARRIVE_FLAT
-#define VSIQ_ARRIVE_FLAT 128
-#endif
-constexpr int kArriveFlat = VSIQ_ARRIVE_FLAT;   // grids above this arrive in two levels (arrive_last)
+constexpr int kArriveFlat = 128;       // grids above this arrive in two levels (arrive_last)
 constexpr int kArriveGroups = 32;      // level-1 arrival counters (counter words 1..32)
-#ifndef VSIQ_FOLD_DIRECT
-#define VSIQ_FOLD_DIRECT 2048
-#endif
-constexpr int kFoldDirect = VSIQ_FOLD_DIRECT;   // two-level arrivals up to this grid: one direct fold
+constexpr int kFoldDirect = 2048;      // two-level arrivals up to this grid: one direct fold
 static_assert(1 + kArriveGroups <= VSIQ_COUNTER_WORDS, "counter words");
 constexpr int kObsGrid = 512;          // K2 grid-stride: workgroups (fixed: order independent of device)
 constexpr int kObsU = 8;               // K2 grid-stride: groups per lane per step
 constexpr int kFlatU = 2;              // 4-element groups per lane in the one-shot streaming kernels
 constexpr int kLsqGroups = 16;         // max groups per lane in K4 (fewer workgroups -> fewer partials)
-#ifndef VSIQ_LSQ_PREFETCH
-#define VSIQ_LSQ_PREFETCH 2
-#endif
-constexpr int kLsqPrefetch = VSIQ_LSQ_PREFETCH;   // K4 groups in flight ahead of the one computing
+constexpr int kLsqPrefetch = 2;        // K4 groups in flight ahead of the one computing
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
