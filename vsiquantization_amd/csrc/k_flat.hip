@@ -1269,6 +1269,7 @@ bool launch_k2o_gated_g(const float *c, float *y, int64_t n, double *parts, cons
 template <int ACT, bool VEC, bool NT>
 bool launch_k2o_gated_vn(const float *c, float *y, int64_t n, double *parts, const SiluLay &L, hipStream_t st) {
   static_assert(kK2oGroups == 2 && kK2oBlock == 256, "the G = 2 gated form is the default grid");
+  // (a 16-groups form is not one round at 26M: 5 workgroups per CU by its registers)
   return launch_k2o_gated_g<ACT, VEC, NT, 2>(c, y, n, parts, L, st) ||
          launch_k2o_gated_g<ACT, VEC, NT, 9>(c, y, n, parts, L, st);
 }

@@ -57,7 +57,7 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
     // a one-round grid (store_gate_select takes grids of 2..occ workgroups per CU only):
     // the tuned store gate between the read and the write phase
     GateSel gs;
-    if constexpr (G == 2) {
+    {
       const void *kern = zpl ? reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, true, ACT, G, true>)
                              : reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, false, ACT, G, true>);
       static const int occ_t = occupancy_blocks(reinterpret_cast<const void *>(k_lsq_bwd<VEC, NT, true, ACT, G, true>),
@@ -90,13 +90,15 @@ void launch_lsq_g(const float *g, const float *x, float *gx, int64_t n, const QP
 // the 4x larger record count is folded by the two-stage k_lsq_fold_chunks.
 // (1 group per lane for the small layers measured slower still: 10.4 against 9.8 us at
 // 3.3M elements, 214 against 201 us at 105M, profiles/r04h_c4_k4d.txt.)
-// Round 5: where that 2-groups-per-lane grid is one round (2..occ workgroups per CU, all
-// resident: C4's 3.3M / 6.6M-element layers) its stores wait behind the tuned store gate
-// (launch_lsq_g).  A one-round grid of 9 groups per lane with the gate was slower at 6.6M
-// (16.2-16.4 against 15.2 us, profiles/r05/r05j_c4*.log).
-inline int lsq_part_groups_per_lane(int64_t) {
+// Round 5 (per-dispatch kernel trace of the C4 leg at 2 / 4 / 8 / 16 groups per lane,
+// every one-round grid gated -- launch_lsq_g --, profiles/r05/r05p_k4d_groups.txt): 2 per
+// lane is best or level up to 26M elements (3.3M 8.7 us gated against 9.6-10.6 for 4-16;
+// 6.6M / 13M / 26M within 1 % of 4 per lane; the one-round 8 / 16 grids of 13M / 26M are
+// slower even gated), 4 per lane from ~50M (52M 98.5 against 100.0 us, 105M 195.9
+// against 204.8).
+inline int lsq_part_groups_per_lane(int64_t n) {
   const int g = g_tune.lsq_groups;
-  return g > 0 ? g : 2;
+  return g > 0 ? g : (n >= ((int64_t)48 << 20) ? 4 : 2);
 }
 
 template <int ACT, bool VEC, bool NT>
