@@ -8,8 +8,10 @@ fold in rank order on every rank -- min / max exact, the sums in float64 in a fi
 order, so every rank holds the same bits -- followed by the reference's running
 update (observers/minmax.py:42-47) and the f64 qparams.  min/max and the qparams are
 bit-identical to a 1-GPU run (no activation or ReLU; a fused SiLU follows each rank's
-own shard layout, so SiLU parity with a 1-GPU run is not pinned); the sums differ only
-in float64 summation order.
+own shard layout, as F.silu does under the reference's DDP: pinned per shard against the
+oracle, and against a whole-batch run it differs only where the two layouts pick a
+different exp path -- tests/test_gpu_dist_calib.py::test_sharded_silu_follows_each_ranks_layout);
+the sums differ only in float64 summation order.
 (``allreduce_stats`` -- MAX over [-min, max], SUM over the sums -- is what the
 deferred sync uses over all records of all layers at once.)
 
