@@ -135,7 +135,8 @@ def test_per_channel_observe_fq_beyond_2g_elements():
 
 def test_deferred_records_beyond_2g_elements():
     """The deferred paths at the same size: K2p partial records + fold (calibration), the
-    same tensor inside a K2m multi-tensor launch (records bit-identical), and the
+    same tensor inside a K2m multi-tensor launch (records bit-identical), K2o (ReLU
+    written + its records: exact min / max / n, y bitwise on the windows), and the
     records-only K4 backward + K4d fold against the one-launch K4 gradient."""
     from vsiquantization_amd.quantizers import deferred as D
     n = BIG
@@ -148,6 +149,14 @@ def test_deferred_records_beyond_2g_elements():
     outs = FQ.observe_parts_multi([small, x], None)
     assert torch.equal(outs[1], parts)
     del outs, parts
+    # K2o (calibration's default kernel): ReLU(x) written and its records, past 2^31
+    y, po = FQ.observe_parts_out(x, "relu")
+    sto = FQ.fold_parts(po.view(1, -1))[0].cpu().numpy()
+    assert (sto[H.ST_MIN], sto[H.ST_MAX], sto[H.ST_NAN], sto[H.ST_N]) == (0.0, 60.0, 0, n)
+    torch.cuda.synchronize()
+    for a, b in windows(n):
+        G.assert_bitwise_f32(host(y, a, b), O.act_forward(host(x, a, b), "relu"), f"relu[{a}:{b}]")
+    del y, po
     g = randn(n, 7)
     s, qmin, qmax = 0.05, -128, 127
     gscale = O.grad_scale(qmax, n)
