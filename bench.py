@@ -1557,10 +1557,20 @@ def main(argv=None):
             continue
         steps, warm = EXTRA_STEPS[key]
         progress(f"{key}: build + measure")
-        Wx = build_workload(key, a, dev, rank, world)
-        rx = measure(Wx, steps, warm, world)
-        if hasattr(Wx, "alt_kernels"):
-            rx["kernels"].update(Wx.alt_kernels())
+        try:
+            Wx = build_workload(key, a, dev, rank, world)
+            rx = measure(Wx, steps, warm, world)
+            if hasattr(Wx, "alt_kernels"):
+                rx["kernels"].update(Wx.alt_kernels())
+        except Exception as e:  # noqa: BLE001
+            # a secondary leg that fails (on every rank alike) must not cost the
+            # headline line: record the error in its place and go on
+            progress(f"{key}: FAILED {e!r}"[:400])
+            extras[key] = {"metric": METRICS[key], "error": repr(e)[:400]}
+            Wx = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            continue
         extras[key] = {"metric": METRICS[key], "value": rx["value"], "unit": "Melem/s",
                        "ms_per_step": rx["ms_per_step"], "steps": steps, "warmup": warm,
                        "scaling": "strong" if key == "act" else "weak",
@@ -1575,7 +1585,8 @@ def main(argv=None):
         cpu_key = lambda k: "c3asym" if k == "c3" and a.asym else k   # noqa: E731
         out["cpu_baseline"] = cpu_baseline(cpu_key(a.workload), a.cpu_seconds, bits)
         for key, e in extras.items():
-            e["cpu_baseline"] = cpu_baseline(cpu_key(key), a.cpu_seconds, bits)
+            if "error" not in e:
+                e["cpu_baseline"] = cpu_baseline(cpu_key(key), a.cpu_seconds, bits)
     if "act" in extras:
         out["batched_act_quant"] = extras.pop("act")
     if extras:
@@ -1593,6 +1604,8 @@ def compact_summary(out) -> str:
     a driver that keeps only the tail of a long line still records every config's value
     and roofline fraction, the public-API timings and the chosen store gates."""
     def leg(name, d):
+        if "error" in d:
+            return f"{name} FAILED {d['error'][:120]}"
         ks = ",".join(f"{k}={v['frac']:.3f}" for k, v in d.get("kernels", {}).items()
                       if isinstance(v, dict) and v.get("frac") and v.get("in_step", True))
         cb = (d.get("cpu_baseline") or {}).get("value")

@@ -129,6 +129,8 @@ def test_compact_summary_is_short_and_complete():
     assert "c5 " in s and "act " in s and "cpu=100.0" in s
     out["store_gate"]["sites"][0]["candidates"] = [[0, 13.41], [489, 12.93], [515, 12.71], [541, 12.80]]
     assert "k3:515(12.71/13.41us)" in bench.compact_summary(out)
+    out["configs"]["c4"] = {"metric": "m", "error": "RuntimeError('x')"}   # a failed secondary leg
+    assert "c4 FAILED RuntimeError('x')" in bench.compact_summary(out)
 
 
 def test_gate_report_candidates_parsed(monkeypatch):
