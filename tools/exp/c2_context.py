@@ -52,13 +52,18 @@ def main():
     def run_groups(G, gk3, gste):
         """rounds x (G fwds, G bwds); returns (us per K3, us per STE): median over rounds."""
         evs = [[bench.timing_event() for _ in range(3)] for _ in range(rounds + 2)]
-        for r, ev in enumerate(evs):
+        one = os.environ.get("ONEGATE", "0") == "1"   # both kernels at gk3, no switch per phase
+        if one:
             H.set_tuning(H.TUNE_STORE_GATE, gk3)
+        for r, ev in enumerate(evs):
+            if not one:
+                H.set_tuning(H.TUNE_STORE_GATE, gk3)
             ev[0].record()
             for j in range(G):
                 f_fwd(*fwd[j % sl])
             ev[1].record()
-            H.set_tuning(H.TUNE_STORE_GATE, gste)
+            if not one:
+                H.set_tuning(H.TUNE_STORE_GATE, gste)
             for j in range(G):
                 f_bwd(*bwd[j % sl])
             ev[2].record()
@@ -68,6 +73,9 @@ def main():
         return a[len(a) // 2], b[len(b) // 2]
 
     gates = [0] + list(range(453, 623, 13))
+    if os.environ.get("NT", "1") == "0":
+        H.set_tuning(H.TUNE_NONTEMPORAL, 0)
+    glist = [int(v) for v in os.environ.get("CTX_GROUPS", "8,64").split(",")]
     if os.environ.get("K3ONLY", "0") == "1":   # K3 back to back, timed per 64 launches
         try:
             for gt in gates:
@@ -87,7 +95,7 @@ def main():
             H.set_tuning(H.TUNE_STORE_GATE, -1)
         return
     try:
-        for G in (8, 64):
+        for G in glist:
             run_groups(G, 500, 0)
             print(f"G={G}: K3 gate sweep (STE gate 0)        |  STE gate sweep (K3 gate 492)")
             print(" gate   K3 us  (STE us)  |  STE us  (K3 us)")
