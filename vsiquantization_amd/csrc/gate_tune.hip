@@ -16,8 +16,9 @@
 // tail.
 //
 // Bursts (round 5): where a site is launched back to back -- the next launch of the same
-// site is the next launch through the tuner, on the same stream, within kBurstGapUs of
-// host time -- a sample spans up to kBurst consecutive launches with the same gate (its
+// site is the next launch of this library (g_lib_launches: an untuned kernel in between,
+// e.g. a larger layer's, ends the burst), on the same stream, within kBurstGapUs of host
+// time -- a sample spans up to kBurst consecutive launches with the same gate (its
 // end event re-recorded after each), and counts their mean.  A lone launch's timing
 // includes how the GPU comes out of the previous, different kernel; launches that stream
 // back to back (a bench's group of one kernel, several layers of one shape in a row)
@@ -89,6 +90,7 @@ struct Site {
   uint64_t last_sel = 0;            // g_sel when this site was last launched
   struct Sample *open = nullptr;    // burst in progress (not in g_pending yet)
   uint64_t open_sel = 0;            // g_sel at the burst's last launch
+  uint64_t open_lib = 0;            // g_lib_launches at the burst's last launch
   std::chrono::steady_clock::time_point open_t;   // host time of the burst's last launch
 };
 
@@ -234,6 +236,8 @@ void harvest_locked() {
 
 }  // namespace
 
+std::atomic<uint64_t> g_lib_launches{0};
+
 GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, int occ, int64_t read_bytes,
                           hipStream_t st) {
   GateSel sel;
@@ -257,7 +261,10 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   }
   std::lock_guard<std::mutex> lk(g_mu);
   Site &s = g_sites[Key{kernel, grid, read_bytes, dev}];
-  const bool adjacent = s.open && s.open_sel == g_sel;   // no other tuned launch since the burst's last
+  // no other tuned launch since the burst's last, and no other library call that launched
+  // (the burst's own launch_rc() counts once)
+  const bool adjacent = s.open && s.open_sel == g_sel &&
+                        g_lib_launches.load(std::memory_order_relaxed) <= s.open_lib + 1;
   s.last_sel = ++g_sel;
   if (s.grid == 0) {
     s.label = label;
@@ -374,6 +381,7 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
   ++p->n;
   s.open = p;   // open until kBurst launches, another tuned launch, a gap or a read-out
   s.open_sel = g_sel;
+  s.open_lib = g_lib_launches.load(std::memory_order_relaxed);
   s.open_t = std::chrono::steady_clock::now();
   if (p->n >= kBurst) close_burst_locked(s);
 }

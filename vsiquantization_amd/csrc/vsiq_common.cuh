@@ -1365,7 +1365,13 @@ inline int64_t lsq_grid(int64_t groups) { return lsq_grid(groups, lsq_groups_per
 inline int64_t fold_records(int64_t grid) { return grid + (grid > kArriveFlat ? kArriveGroups : 0); }
 
 
+// every exported entry point ends with launch_rc(): the count of library calls that
+// launched (gate_tune.hip), so a store-gate burst sample never spans another kernel of
+// this library between two launches of its site
+extern std::atomic<uint64_t> g_lib_launches;
+
 inline int launch_rc() {
+  g_lib_launches.fetch_add(1, std::memory_order_relaxed);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
