@@ -183,3 +183,24 @@ def test_gate_drift_under_concurrent_load_retunes():
     assert _retunes(line) >= 1, (line0, line)
     for y in ys:
         G.assert_bitwise_f32(y.cpu().numpy(), want, "y")
+
+
+def test_burst_sample_never_spans_another_library_launch():
+    """A site's burst sample ends at any other launch of the library (g_lib_launches): a
+    1.6M-element K2o (a one-round gated site) alternating with a 52M-element K2o (an
+    untuned multi-round grid, ~70 us) -- were a sample to span the large launch, every
+    candidate's median would carry it.  The outputs stay the oracle's ReLU bits."""
+    _reset()
+    small = torch.randn(1_638_400, device=DEV)
+    big = torch.randn(52_428_800, device=DEV)
+    for i in range(400):
+        y, _ = FQ.observe_parts_out(small, "relu")
+        FQ.observe_parts_out(big, "relu")
+        if i % 16 == 15:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    G.assert_bitwise_f32(y.cpu().numpy(), O.act_forward(small.cpu().numpy(), "relu"), "relu")
+    line = _site_line("k2o_observe_out")
+    assert " done=1 " in line, H.gate_report()
+    meds = [float(t.split(":")[1]) for t in line.split() if ":" in t and t.split(":")[0].isdigit()]
+    assert len(meds) >= 12 and max(meds) < 30.0, line
