@@ -1,5 +1,9 @@
 """K6 / per-channel fake quant (LSQFakeQuantize per-channel, axis 1) at YOLOv8n activation
-shapes, batch 256, and axis-0 weights. Experiment only: prints us and GB/s per launch."""
+shapes, batch 256, and axis-0 weights. Experiment only: prints us and GB/s per launch.
+Event-timed through the Python API: the first round of a shape includes the GPU's ramp
+(round 5: K6 at 256x16x160x160 read 246-269 us in round 1, 206-208 from round 2; ROUNDS
+defaults to 2), and small shapes are host-bound here (use rocprofv3 --kernel-trace for
+their kernel time).  FLAT=1 adds K4 (per-tensor LSQ) on the same tensors."""
 import os, sys, torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
@@ -46,7 +50,7 @@ for shape, axis in (((256, 16, 160, 160), 1), ((256, 64, 40, 40), 1), ((256, 256
     def nxt():
         it[0] += 1
         return it[0] % nsets
-    for rnd in range(int(os.environ.get("ROUNDS", "1"))):
+    for rnd in range(int(os.environ.get("ROUNDS", "2"))):
         for alt in (os.environ.get("ALT", "").split(";") if os.environ.get("ALT") else [""]):
             for kv in alt.split():   # ALT="13=1;13=0": alternate knob settings, same process
                 k, v = kv.split("=")
@@ -54,5 +58,11 @@ for shape, axis in (((256, 16, 160, 160), 1), ((256, 64, 40, 40), 1), ((256, 256
             fwd = t(lambda: FQ.per_channel_fake_quant(xs[nxt()], s, z, -128, 127, axis=axis), reps)
             bwd = t(lambda: (lambda i: FQ.pc_lsq_backward(gs[i], xs[i], s, z, -128, 127, 1e-4, True, axis))(nxt()),
                     reps)
+            flat = ""
+            if os.environ.get("FLAT", "0") == "1":   # K4 (per-tensor LSQ) on the same tensors: the floor
+                s0 = torch.tensor(0.03, dtype=torch.float64, device=dev)
+                fl = t(lambda: (lambda i: FQ.lsq_backward(gs[i], xs[i], s0, 0.0, -128, 127, 1e-4, False))(nxt()),
+                       reps)
+                flat = f"   K4 flat {fl:8.2f} us ({12 * n / fl / 1e3:5.0f} GB/s)"
             print(f"{str(shape):22s} axis {axis} {alt:8s} fwd {fwd:8.2f} us ({8 * n / fwd / 1e3:5.0f} GB/s)   "
-                  f"bwd(K6) {bwd:8.2f} us ({12 * n / bwd / 1e3:5.0f} GB/s)", flush=True)
+                  f"bwd(K6) {bwd:8.2f} us ({12 * n / bwd / 1e3:5.0f} GB/s){flat}", flush=True)
