@@ -147,3 +147,28 @@ def test_gate_report_candidates_parsed(monkeypatch):
     n, sites = bench.settle_gates(W())
     assert n == 8 and sites[0]["gate_ticks"] == 528 and sites[0]["retunes"] == 1
     assert sites[0]["candidates"] == [[0, 13.41], [453, 12.95], [528, 12.70]]
+
+
+def test_chained_group_events_durations():
+    """Consecutive launch groups share their boundary event (bench._Chained): per-phase
+    durations read from the chained rows equal those of separate events per group."""
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def record(self, *_):
+            pass
+
+        def elapsed_time(self, end):
+            return end.t - self.t
+    # 3 groups x 2 phases: boundaries at 0, 5, 9 | 9, 14, 20 | 20, 26, 30 (ms)
+    marks = [[0, 5, 9], [9, 14, 20], [20, 26, 30]]
+    rows = []
+    for m in marks:
+        row = [Ev(t) for t in m]
+        if rows:
+            row[0] = bench._Chained(rows[-1][-1])
+        rows.append(row)
+    assert rows[1][0].record() is None   # recording the shared event again is a no-op
+    d = bench._durations(rows, ["fwd", "bwd"], steps=1000)
+    assert d == {"fwd": (5 + 5 + 6) / 1000 * 1e-3, "bwd": (4 + 6 + 4) / 1000 * 1e-3}
