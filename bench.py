@@ -1118,8 +1118,10 @@ def capture_groups(W, groups, nphase):
     """Every launch group of the timed region, phase by phase, as HIP graphs (the same
     launches, replayed without host work between the kernels).  None when a workload's
     launches cannot be captured (then the timed region launches directly)."""
+    from vsiquantization_amd.utils.graph import quiesce_collectives
     stream = torch.cuda.current_stream()
     out = []
+    quiesce_collectives()   # RCCL's watchdog must hold no collective to poll during the captures
     try:
         for g0, cnt in groups:
             cap = _GroupCapture(stream)

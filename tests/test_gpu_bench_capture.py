@@ -27,7 +27,8 @@ def test_act_leg_graph_capture_with_rccl_exchange():
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "bench_capture_worker.py")]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    why = [l for l in r.stderr.splitlines() if "terminated with exception" in l or "Error" in l][:6]
+    assert r.returncode == 0, "\n".join(why) + r.stdout[-2000:] + r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     got = json.loads(line)
     assert got["graph_equals_direct"] and got["self_check"], got

@@ -18,9 +18,26 @@ capture, steps until the store-gate tuner has settled every launch site the step
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 from .. import _hip as H
+
+
+def quiesce_collectives(settle_s: float = 0.3) -> None:
+    """Call right before a HIP-graph capture.  Finishes the device's work and, under an
+    NCCL (RCCL) process group, gives ProcessGroupNCCL's watchdog thread time to drop the
+    completed collectives from its list: it polls each listed collective's event every
+    ~100 ms and aborts the process if a poll fails, and a poll that lands inside a
+    capture can fail on HIP even in thread_local capture mode (seen as a rare SIGABRT,
+    "watchdog thread terminated with exception", in a 1-rank RCCL capture test).
+    Collectives issued under capture are never listed, so an empty list stays empty
+    for the capture."""
+    torch.cuda.synchronize()
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(settle_s)
 
 
 def _detached(v):
@@ -68,6 +85,7 @@ class GraphedStep:
                     break
         torch.cuda.current_stream().wait_stream(side)
         self._clear()
+        quiesce_collectives()
         self.graph = torch.cuda.CUDAGraph()
         before = set(H._WS)
         # thread_local: other threads of the process (torch's NCCL watchdog polling the events
