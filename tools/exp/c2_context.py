@@ -48,6 +48,21 @@ def main():
     bwd = [(P(gs[j].data_ptr()), P(masks[j].data_ptr()), P(gxs[j].data_ptr()), H.c_i64(rows * rowlen),
             P(qp[j][0].data_ptr()), H.c_i64(rowlen), 0.0, st) for j in range(sl)]
     f_fwd, f_bwd = lib.vsiq_pc_observe_fq_f32, lib.vsiq_ste_bwd_f32
+    partner = os.environ.get("PARTNER", "ste")   # what runs between the K3 phases
+    if partner == "copy":   # a plain ungated copy of the STE's bytes (c2_floor.hip)
+        import subprocess
+        so = os.path.join("/tmp", "c2_floor.so")
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", so,
+                        os.path.join(HERE, "c2_floor.hip")], check=True)
+        ex = ctypes.CDLL(so)
+        ex.exp_copy_gated.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, P]
+        f_bwd = lambda a, b, c, *_: ex.exp_copy_gated(a, c, rows, rowlen, 0, st)   # noqa: E731
+    elif partner == "tiny":   # a one-workgroup kernel: no traffic
+        tiny = torch.empty(64, device=dev)
+        f_bwd = lambda *_: (tiny.fill_(0.0), 0)[1]   # noqa: E731
+    elif partner == "ste_ownmask":   # the STE on masks K3 never writes (same bytes)
+        own = [m.clone() for m in masks]
+        bwd = [(b[0], P(own[j].data_ptr()), *b[2:]) for j, b in enumerate(bwd)]
 
     def run_groups(G, gk3, gste):
         """rounds x (G fwds, G bwds); returns (us per K3, us per STE): median over rounds."""
