@@ -1148,8 +1148,8 @@ def measure(W, steps, warmup, world, graphs=None):
     hipLaunchKernel, 5-10 us on a slow host, comparable to a C2 kernel) from between the
     kernels, but a graph's kernel nodes dispatch a little slower than direct launches on a
     fast host (measured: C2 29.7 vs 28.2 us/step).  So an untimed trial (up to 4 groups,
-    5 rounds each way, median wall time; graph only if >1 % faster) picks the mode for the
-    timed region, and the same
+    5 rounds each way, median wall time; one rank: graph unless direct is >1 % faster,
+    several: graph only if >1 % faster) picks the mode for the timed region, and the same
     `steps` are then timed the other way too and reported as "alt_launch"."""
     for i in range(warmup):
         assert W.launch(i) == 0
@@ -1210,9 +1210,10 @@ def _pick_launch(W, groups, graphs, reps=5, margin=0.01, min_ms=20.0, max_reps=5
     """Untimed trial: up to 4 launch groups each way, `reps` rounds -- more (up to
     `max_reps`) while the trial has run less than `min_ms` per mode, so that a short
     workload's (C1: ~0.25 ms per round) choice is not decided by host noise -- median
-    wall time per mode; graph replay is chosen only when it is faster by more than
-    `margin` (direct launches are the default).  Several ranks: exactly `reps` rounds
-    (every rank runs the same collectives; the caller agrees on the choice).  Returns
+    wall time per mode; one rank: graph replay unless direct launches are faster by more
+    than `margin`.  Several ranks: graph replay only when it is faster by more than
+    `margin`, and exactly `reps` rounds (every rank runs the same collectives; the caller
+    agrees on the choice).  Returns
     (use graph?, {mode: median ms})."""
     sel = list(range(min(4, len(groups))))
     t = {"direct": [], "graph": []}
@@ -1232,6 +1233,12 @@ def _pick_launch(W, groups, graphs, reps=5, margin=0.01, min_ms=20.0, max_reps=5
             torch.cuda.synchronize()
             t[mode].append((time.perf_counter() - t0) * 1e3)
     med = {k: sorted(v)[len(v) // 2] for k, v in t.items()}
+    if world == 1:
+        # one rank: graph replay unless direct launches are clearly faster -- within the
+        # margin the replay wins, since it does not depend on the host keeping up (round 5:
+        # C5 on a box whose host ran 2x slow: 417.9 us/step direct, 378.3 replayed, after a
+        # trial that had them tied)
+        return med["graph"] <= (1.0 + margin) * med["direct"], med
     return med["graph"] < (1.0 - margin) * med["direct"], med
 
 
