@@ -75,6 +75,15 @@ def parse(argv=None):
     p.add_argument("--master-port", type=int, default=0)
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal without a GPU: ranks join a gloo group and report")
+    p.add_argument("--gate-table", default=None, metavar="PATH",
+                   help="start from a store-gate table saved by --save-gate-table and freeze the tuner "
+                        "(no candidate or drift launches: reproducible kernel timing)")
+    p.add_argument("--save-gate-table", default=None, metavar="PATH",
+                   help="after the headline workload's gates have settled, save the table to PATH")
+    p.add_argument("--markers", action="store_true",
+                   help="launch vsiq_trace_marker right before / after each timed region (outside the "
+                        "wall-clock window), so tools/timed_region_stats.py can cut a rocprofv3 kernel trace "
+                        "to the timed launches")
     p.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                    help="experiments: vsiq_set_tuning(KEY, VALUE) before the workload is built "
                         "(keys: include/vsiq.h VSIQ_TUNE_*)")
@@ -1257,6 +1266,15 @@ class _Chained:
         return self.ev.elapsed_time(other)
 
 
+MARKERS = []   # [stream handle getter] when --markers: trace markers around each timed region
+
+
+def _marker(end):
+    if MARKERS:
+        from vsiquantization_amd import _hip as H
+        assert H.lib().vsiq_trace_marker(int(end), H.stream_of(torch.cuda.current_device())) == 0
+
+
 def _timed(W, groups, names, steps, world, captured):
     chain = os.environ.get("VSIQ_BENCH_CHAIN", "1") == "1"
     evs = []
@@ -1265,6 +1283,7 @@ def _timed(W, groups, names, steps, world, captured):
         if chain and evs:
             row[0] = _Chained(evs[-1][-1])
         evs.append(row)
+    _marker(0)   # queued before the synchronize: outside the wall-clock window
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1283,6 +1302,7 @@ def _timed(W, groups, names, steps, world, captured):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    _marker(1)
     assert rc == 0, f"kernel launch failed rc={rc}"
     return dt, evs
 
@@ -1531,6 +1551,10 @@ def main(argv=None):
     for kv in a.tune:
         k, v = kv.split("=")
         H.set_tuning(int(k), int(v))
+    if a.gate_table:
+        progress(f"gate table {a.gate_table}: {H.gate_load(a.gate_table)} sites, tuner frozen")
+    if a.markers:
+        MARKERS.append(True)
     cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
     bits = (a.bits_w, a.bits_a)
 
@@ -1566,6 +1590,8 @@ def main(argv=None):
         out["alt_launch"] = r["alt_launch"]
     if a.tune:
         out["config"]["tuning"] = a.tune
+    if a.gate_table:
+        out["store_gate"]["table"] = {"loaded": a.gate_table, "frozen": True}
     if a.workload == "c2":
         progress("c2: forward with uint8 codes")
         out["kernels"]["pc_observe_fq_fwd_with_codes"] = W.codes_variant()
@@ -1610,6 +1636,8 @@ def main(argv=None):
             extras[key]["alt_launch"] = rx["alt_launch"]
         del Wx
         torch.cuda.empty_cache()
+    if a.save_gate_table and rank == 0:
+        progress(f"gate table saved: {H.gate_save(a.save_gate_table)} sites -> {a.save_gate_table}")
     if cpu:
         # CPU legs after every GPU measurement (host threads do not disturb the timed regions)
         cpu_key = lambda k: "c3asym" if k == "c3" and a.asym else k   # noqa: E731

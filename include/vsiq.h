@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define VSIQ_ABI_VERSION 10
+#define VSIQ_ABI_VERSION 11
 
 /* uint32 words of a reducing kernel's arrival `counter` (all 0 before the first call) */
 #define VSIQ_COUNTER_WORDS 64
@@ -130,6 +130,46 @@ int vsiq_gate_reset(void);
  * re-tunes by itself when the median time of its chosen gate drifts by more than 15 %
  * (one launch in 128 is timed).  Results never depend on the gate. */
 int vsiq_gate_retune(void);
+/* Gate table (ABI 11).  A site's key is "<kernel symbol> <grid> <read bytes>" (stable
+ * for one build of the library); a table line is the key and the gate in ticks.
+ *   vsiq_gate_export: every tuned site's line (and every loaded line) into buf
+ *     (NUL-terminated, truncated to len); returns the full length;
+ *   vsiq_gate_import: load lines (e.g. a saved export); a listed site, existing or
+ *     first launched later, takes that gate and is never timed; returns the number of
+ *     lines, -1 on a malformed line (nothing loaded then);
+ *   vsiq_gate_freeze(1): from now on no launch is timed -- sites still tuning, and sites
+ *     first launched later without a loaded line, run the fixed default (1.05 x the read
+ *     time at 7.5 TB/s); vsiq_gate_retune does nothing while frozen.  Returns the
+ *     previous setting.  With a loaded table and freeze, a process's kernel timing no
+ *     longer depends on tuner state (no candidate or drift launches). */
+int64_t vsiq_gate_export(char *buf, int64_t len);
+/* Trace marker (ABI 11): one empty kernel, `vsiq_timed_region_marker`, grid 1 (end 0) or
+ * grid 2 (end 1), so a kernel trace can be cut to the region between the two
+ * (tools/timed_region_stats.py; bench.py --markers). */
+int vsiq_trace_marker(int end, hipStream_t stream);
+
+/*
+ * K11 (ABI 11): the reference's per-call mean|x| and mean x BIT FOR BIT as torch's CPU
+ * kernel computes them on the reference host -- quantization_manager.py:66-67 records
+ * torch.mean(torch.abs(x)).cpu().item() and torch.mean(x); qm.py:112 builds the
+ * learnable scale from that list.  torch's CPU sum is a cascade whose order depends on
+ * the host's thread count (chunks of at::parallel_for) and its vector width (`vec` = 8,
+ * the AVX2 Vectorized<float> this torch build dispatches on AVX2 and AVX-512 hosts
+ * alike; 16 supported); the activation (VSIQ_ACT_*, SiLU with its own reference layout)
+ * is applied first, as the fused layers record act(x).  One extra read of x (opt-in in
+ * the Python layer).  out4 (device, nullable): {sum |act(x)|, sum act(x), mean |act(x)|,
+ * mean act(x)} as fp32; stats (device, nullable): its VSIQ_ST_MEANABS / VSIQ_ST_MEAN
+ * entries overwritten with the two means.  ws: vsiq_torch_mean_ws_bytes(n, vec,
+ * threads) bytes (-1: unsupported arguments -- vec not 8 / 16, threads outside 1..4096,
+ * a chunk of 2^30 elements or more).  n = 0 gives NaN means, as torch.mean.
+ */
+int64_t vsiq_torch_mean_ws_bytes(int64_t n, int vec, int threads);
+int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4, double *stats,
+                        void *ws, int64_t ws_bytes, hipStream_t stream);
+/* The same on a host (CPU) tensor, out4 in host memory; chunks on the host pool. */
+int vsiq_host_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4);
+int vsiq_gate_import(const char *text);
+int vsiq_gate_freeze(int on);
 
 /*
  * Self-test of the kernels' correctly rounded division x / s (reciprocal +

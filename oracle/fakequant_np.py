@@ -219,6 +219,41 @@ def _silu_lib():
     return _SILU[0]
 
 
+# --------------------------------------------------------------------------- mean|x| / mean x
+# quantization_manager.py:66-67 records torch.mean(torch.abs(x)).cpu().item() and
+# torch.mean(x): fp32 sums in torch's CPU cascade order, which depends on the host's
+# thread count (oracle/mean_ref.c, pinned against torch.mean by tests/test_mean_oracle.py).
+MEAN_REF_VEC = 8   # Vectorized<float> of the sum kernel this torch build dispatches (AVX2 and AVX-512)
+_MEAN = []
+
+
+def _mean_lib():
+    if not _MEAN:
+        import ctypes
+
+        from oracle import build_oracle
+        lib = ctypes.CDLL(build_oracle.build_mean(verbose=False))
+        P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        for f in (lib.oracle_torch_sum_f32, lib.oracle_torch_mean_f32):
+            f.argtypes = [P, I64, I, I, I]
+            f.restype = ctypes.c_float
+        _MEAN.append(lib)
+    return _MEAN[0]
+
+
+def torch_mean(x, absf, threads, vec=MEAN_REF_VEC):
+    """torch.mean(torch.abs(x)) (absf) or torch.mean(x) of a float32 array as torch's CPU
+    kernel computes it on a host with `threads` threads: an np.float32."""
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32).reshape(-1))
+    return np.float32(_mean_lib().oracle_torch_mean_f32(_p(a), a.size, int(bool(absf)), int(vec), int(threads)))
+
+
+def torch_sum(x, absf, threads, vec=MEAN_REF_VEC):
+    """The fp32 sum torch_mean divides (torch.sum on that host)."""
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32).reshape(-1))
+    return np.float32(_mean_lib().oracle_torch_sum_f32(_p(a), a.size, int(bool(absf)), int(vec), int(threads)))
+
+
 def _p(a):
     import ctypes
     return ctypes.c_void_p(a.ctypes.data)

@@ -128,3 +128,36 @@ def test_copies_fold_their_own_records(fake_fold):
         assert (cp.observer.min_val, cp.observer.max_val) == (-3.0, 2.0)
         assert len(qm._pending_records) == 2
     assert (qm.observer.min_val, qm.observer.max_val) == (-3.0, 2.0)
+
+
+def test_hasattr_under_a_process_group_is_false(fake_fold):
+    """hasattr(qm, "scale") during a deferred multi-GPU calibration answers False (the read
+    raises DeferredSyncError, a RuntimeError that is also an AttributeError) and folds
+    nothing."""
+    from vsiquantization_amd.quantizers.quantization_manager import DeferredSyncError
+    qm = _manager()
+    qm.dist_group = object()
+    _call(qm, _record(-1.0, 2.0))
+    assert not hasattr(qm, "scale") and not hasattr(qm, "zero_point")
+    with pytest.raises(DeferredSyncError, match="sync_calibration"):
+        qm.scale
+    assert fake_fold == [] and len(qm._pending_records) == 1
+
+
+def test_failing_replay_keeps_the_calls(monkeypatch, fake_fold):
+    """A fold whose replay raises leaves the manager as it was: the calls stay pending and a
+    later read (once the replay works) gives the reference's state."""
+    qm = _manager()
+    for c in CALLS:
+        _call(qm, _record(*c))
+
+    def boom(*a, **k):
+        raise RuntimeError("replay failed")
+    monkeypatch.setattr(D, "replay_minmax", boom)
+    with pytest.raises(RuntimeError, match="replay failed"):
+        qm.scale
+    assert len(qm._pending_records) == len(CALLS) and qm._calib_init == (0, 0)
+    monkeypatch.undo()
+    monkeypatch.setattr(D, "fold_slots", lambda slots: torch.stack(slots))
+    assert (qm.observer.min_val, qm.observer.max_val) == _replayed(len(CALLS))[0]
+    assert qm._pending_records == []

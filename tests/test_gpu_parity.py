@@ -174,8 +174,25 @@ def test_asym_learnable_int_zero_point_raises_like_reference():
         q.quantize(torch.randn(10, device=DEV), s, 0, True)
 
 
+@pytest.mark.parametrize("mode", ["reference", "default"])
 @pytest.mark.parametrize("case", G.cases("manager_sequence"), ids=lambda c: c["key"])
-def test_golden_manager_sequence(case):
+def test_golden_manager_sequence(case, mode):
+    """calibrate (observe only) -> observe+quantize -> init_scaling_factor_for_learning ->
+    make_learn_qparameter -> one learnable step, nothing injected.  "reference": mean|x| /
+    mean x as torch's CPU kernel sums them on the golden host (H.set_mean_reference, K11),
+    so the learnable scale and the step are the reference's bit for bit.  "default" (no
+    extra pass): the means are the correctly rounded fp32 ones, within 1e-6; the scale's
+    fp32 value may then differ by an ulp, so y equals the reference's in its integer
+    codes, not in every bit."""
+    if mode == "reference":
+        H.set_mean_reference(G.GOLDEN_SILU_REF[1])
+    try:
+        _manager_sequence(case, exact=mode == "reference")
+    finally:
+        H.clear_mean_reference()
+
+
+def _manager_sequence(case, exact):
     qm = V.QuantizationManager("UniformQuantizer", "MinMaxObserver", case["bits"], case["sym"], True)
     qm.is_observer_qparam, qm.is_learning_scale, qm.is_quantize = True, False, False
     outs = [(qm.quantize(cu(G.arr(k))), k) for k in case["xs"]]
@@ -183,30 +200,41 @@ def test_golden_manager_sequence(case):
     cal = case["calib"]
     assert (qm.observer.min_val, qm.observer.max_val) == (cal["min_val"], cal["max_val"])
     assert float(qm.scale) == cal["scale"] and float(qm.zero_point) == cal["zero_point"]
-    np.testing.assert_allclose(qm.mean_abs_x, cal["mean_abs_x"], rtol=1e-6)
-    np.testing.assert_allclose(qm.mean_x, cal["mean_x"], rtol=1e-5, atol=1e-7)
+    if exact:
+        assert [float(v) for v in qm.mean_abs_x] == cal["mean_abs_x"]
+        assert [float(v) for v in qm.mean_x] == cal["mean_x"]
+    else:
+        np.testing.assert_allclose(qm.mean_abs_x, cal["mean_abs_x"], rtol=1e-6)
+        np.testing.assert_allclose(qm.mean_x, cal["mean_x"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(qm.std, cal["std"], rtol=1e-6)
     qm.is_quantize = True
     y = qm.quantize(cu(G.arr(case["x_oq"])))
     G.assert_bitwise_f32(npy(y), G.arr(case["y_oq"]), "observe+quantize")
     qm.is_learning_scale = True
     qm.init_scaling_factor_for_learning()
-    assert qm.scale == pytest.approx(case["init_scale"], rel=1e-6)
+    if exact:
+        assert qm.scale == case["init_scale"]
+    else:
+        assert qm.scale == pytest.approx(case["init_scale"], rel=1e-6)
     qm.make_learn_qparameter()
     assert isinstance(qm.scale, torch.nn.Parameter) and qm.scale.dtype == torch.float64
     if "learn_raises" in case:
         with pytest.raises(TypeError):
             qm.quantize(cu(G.arr(case["xs"][0])))
         return
-    # use the reference's exact init value so the learnable step is bit-comparable
-    with torch.no_grad():
-        qm.scale.copy_(torch.tensor(case["init_scale"], dtype=torch.float64))
     qm.cuda()
     xg = cu(G.arr(case["x4"]), grad=True)
     y4 = qm.quantize(xg)
-    G.assert_bitwise_f32(npy(y4), G.arr(case["y4"]), "y4")
+    if exact:
+        G.assert_bitwise_f32(npy(y4), G.arr(case["y4"]), "y4")
+    else:   # the same integer codes under each side's own fp32 scale
+        s_ours, s_ref = np.float32(float(qm.scale)), np.float32(case["init_scale"])
+        np.testing.assert_array_equal(np.rint(npy(y4) / s_ours), np.rint(G.arr(case["y4"]) / s_ref))
     y4.backward(cu(G.arr(case["g4"])))
-    G.assert_bitwise_f32(npy(xg.grad), G.arr(case["gx4"]), "gx4")
+    if exact:
+        G.assert_bitwise_f32(npy(xg.grad), G.arr(case["gx4"]), "gx4")
+    else:
+        np.testing.assert_array_equal(npy(xg.grad) != 0, G.arr(case["gx4"]) != 0)
     assert float(qm.scale.grad) == pytest.approx(case["scale_grad"], rel=1e-4)
 
 

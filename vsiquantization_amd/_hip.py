@@ -25,7 +25,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_d = ctypes.c_double
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 COUNTER_WORDS = 64   # VSIQ_COUNTER_WORDS
 COUNTER_GRID_ERRORS = 35   # VSIQ_COUNTER_GRID_ERRORS (K10's barrier-timeout count)
 
@@ -69,6 +69,51 @@ def silu_reference():
     if _SILU_PIN:
         return _SILU_PIN[0]
     return _SILU_W.get(torch.backends.cpu.get_cpu_capability(), 16), torch.get_num_threads()
+
+
+# mean|x| / mean x of an observer call as torch's CPU kernel sums them (K11,
+# csrc/k_mean.hip): off by default (the stats are the correctly rounded fp32 means of
+# an f64 sum, within one fp32 ulp of torch's; K11 costs one extra read per call).  On:
+# (vec, threads) of the reference host -- vec 8 is the Vectorized<float> this torch
+# build's sum kernel uses on AVX2 and AVX-512 hosts alike (tests/test_mean_oracle.py).
+_MEAN_REF = []
+
+
+def set_mean_reference(threads=None, vec: int = 8):
+    """Record mean|x| / mean x bit for bit as torch's CPU torch.mean on a host with
+    ``threads`` CPU threads (None: this process's torch.get_num_threads()); the reference
+    records those values (quantization_manager.py:66-67) and builds the learnable scale
+    from them (qm.py:112).  Costs one extra read of each observed tensor."""
+    t = torch.get_num_threads() if threads is None else int(threads)
+    if vec not in (8, 16) or not 1 <= t <= 4096:
+        raise ValueError(f"mean reference vec {vec} / threads {t}")
+    _MEAN_REF[:] = [(int(vec), t)]
+
+
+def clear_mean_reference():
+    """Back to the default statistics (no extra pass)."""
+    _MEAN_REF.clear()
+
+
+def mean_reference():
+    """(vec, threads) of the reference layout mean|x| / mean x follow, or None (off)."""
+    return _MEAN_REF[0] if _MEAN_REF else None
+
+
+def _mean_reference_from_env():
+    v = os.environ.get("VSIQ_MEAN_REFERENCE", "").strip()
+    if not v or v == "0":
+        return
+    if v == "host":
+        set_mean_reference()
+    elif "," in v:
+        a, b = v.split(",", 1)
+        set_mean_reference(int(b), int(a))
+    else:
+        set_mean_reference(int(v))
+
+
+_mean_reference_from_env()
 
 
 class SiluAct(str):
@@ -119,6 +164,13 @@ _SIGS = {
     "vsiq_gate_report": ([ctypes.c_char_p, c_i64], c_i64),
     "vsiq_gate_reset": ([], c_int),
     "vsiq_gate_retune": ([], c_int),
+    "vsiq_gate_export": ([ctypes.c_char_p, c_i64], c_i64),
+    "vsiq_gate_import": ([ctypes.c_char_p], c_int),
+    "vsiq_gate_freeze": ([c_int], c_int),
+    "vsiq_trace_marker": ([c_int, c_p], c_int),
+    "vsiq_torch_mean_ws_bytes": ([c_i64, c_int, c_int], c_i64),
+    "vsiq_torch_mean_f32": ([c_p, c_i64, c_int, c_int, c_int, c_p, c_p, c_p, c_i64, c_p], c_int),
+    "vsiq_host_torch_mean_f32": ([c_p, c_i64, c_int, c_int, c_int, c_p], c_int),
     "vsiq_selftest_div": ([c_p, c_int, c_p, c_p], c_int),
     "vsiq_selftest_fq": ([c_int, c_p, c_p, c_int, ctypes.c_float, ctypes.c_float, c_p, c_p], c_int),
     "vsiq_fq_fwd_f32": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_d, c_p, c_d, c_int, c_int, c_int, c_int, c_p],
@@ -243,6 +295,15 @@ def lib():
         v = handle.vsiq_abi_version()
         if v != ABI_VERSION:
             raise VsiqError(f"vsiq ABI version {v} != expected {ABI_VERSION}; rebuild the library")
+        # VSIQ_GATE_TABLE=<file of gate_save>: start from a saved store-gate table, frozen
+        # unless VSIQ_GATE_FREEZE=0 (reproducible kernel timing, no tuner launches)
+        table = os.environ.get("VSIQ_GATE_TABLE")
+        if table:
+            with open(table) as f:
+                if handle.vsiq_gate_import(f.read().encode()) < 0:
+                    raise VsiqError(f"VSIQ_GATE_TABLE={table}: malformed gate table")
+            if os.environ.get("VSIQ_GATE_FREEZE", "1") != "0":
+                handle.vsiq_gate_freeze(1)
         _LIB = handle
     return _LIB
 
@@ -325,6 +386,46 @@ def gate_report() -> str:
     buf = ctypes.create_string_buffer(n + 1)
     lib().vsiq_gate_report(buf, n + 1)
     return buf.value.decode()
+
+
+def gate_export() -> str:
+    """The tuned store-gate table, one "<kernel symbol> <grid> <bytes> <ticks>" line per
+    site (vsiq_gate_export)."""
+    n = int(lib().vsiq_gate_export(None, 0))
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().vsiq_gate_export(buf, n + 1)
+    return buf.value.decode()
+
+
+def gate_import(text: str) -> int:
+    """Load gate_export's lines: a listed site takes that gate and is never timed."""
+    n = int(lib().vsiq_gate_import(text.encode()))
+    if n < 0:
+        raise ValueError("vsiq_gate_import: malformed gate table")
+    return n
+
+
+def gate_freeze(on: bool = True) -> bool:
+    """Stop (or resume) all store-gate timing; returns the previous setting."""
+    return bool(lib().vsiq_gate_freeze(int(bool(on))))
+
+
+def gate_save(path: str) -> int:
+    """Write the tuned gate table to `path`; returns the number of sites."""
+    text = gate_export()
+    with open(path, "w") as f:
+        f.write(text)
+    return text.count("\n")
+
+
+def gate_load(path: str, freeze: bool = True) -> int:
+    """Load a table written by gate_save and (default) freeze the tuner: reproducible
+    timing, no candidate launches.  Returns the number of loaded sites."""
+    with open(path) as f:
+        n = gate_import(f.read())
+    if freeze:
+        gate_freeze(True)
+    return n
 
 
 def ptr(t):

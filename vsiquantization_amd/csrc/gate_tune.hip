@@ -39,9 +39,12 @@
 // and re-tuning.  The gate is a delay only: results are bit-identical whatever it is.
 #include "vsiq_common.cuh"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -66,6 +69,8 @@ constexpr double kBurstGapUs = 25.0;   // host time between the launches of a bu
 
 struct Site {
   std::string label;
+  std::string table_key;            // "<kernel symbol> <grid> <bytes>": the saved-table key
+  bool preset = false;              // gate taken from a loaded table (never timed)
   int64_t grid = 0, bytes = 0;
   int dev = 0;
   double est = 0.0;                 // ticks of read bytes at 7.5 TB/s
@@ -116,7 +121,6 @@ std::vector<Sample *> g_pending;
 std::map<int, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_pool;
 uint64_t g_sel = 0;    // launches through the tuner (a clock for "launched since")
 uint64_t g_mark = 0;   // g_sel at the previous vsiq_gate_tuning_pending()
-
 uint32_t clamp_ticks(double t, int khz) {
   const double cap = kCapUs * khz / 1e3;
   return (uint32_t)std::max(0.0, std::min(cap, t));
@@ -126,6 +130,41 @@ float median(std::vector<float> v) {
   std::sort(v.begin(), v.end());
   const size_t n = v.size();
   return n % 2 ? v[n / 2] : 0.5f * (v[n / 2 - 1] + v[n / 2]);
+}
+
+// Gate table (round 6): gates loaded with vsiq_gate_import, by table key; frozen: no
+// launch is ever timed (a loaded site keeps its gate, a site missing from the table runs
+// the fixed default), so a process's timing does not depend on tuner state.
+std::map<std::string, uint32_t> g_preset;
+bool g_frozen = false;
+
+// "<kernel host-stub symbol> <grid> <read bytes>": stable across processes of the same
+// build (the stubs are exported; dladdr names them), unlike the stub's address
+std::string table_key(const char *label, const void *kernel, int64_t grid, int64_t bytes) {
+  Dl_info info;
+  const char *name = (dladdr(kernel, &info) != 0 && info.dli_sname) ? info.dli_sname : label;
+  char tail[64];
+  std::snprintf(tail, sizeof tail, " %lld %lld", (long long)grid, (long long)bytes);
+  return std::string(name) + tail;
+}
+
+// caller holds g_mu: a site with a loaded gate is tuned; in a frozen table a site
+// without one keeps the default and is never timed
+void apply_preset(Site &s, int khz) {
+  auto it = g_preset.find(s.table_key);
+  if (it != g_preset.end()) {
+    s.best = it->second;
+    s.preset = true;
+  } else if (g_frozen) {
+    s.best = clamp_ticks(kDefault * s.est, khz);
+  } else {
+    return;
+  }
+  s.done = true;
+  s.best_ms = 0.0f;
+  s.watch.clear();
+  s.since_watch = 0;
+  s.drifting = 0;
 }
 
 void start_round(Site &s) {
@@ -275,6 +314,8 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     for (int c = 0; c < kCand; ++c) s.ticks[c] = clamp_ticks(kFactors[c] * est, khz);
     s.rng = 0x9e3779b97f4a7c15ull ^ (uint64_t)(uintptr_t)kernel ^ ((uint64_t)grid << 20) ^ (uint64_t)read_bytes;
     start_round(s);
+    s.table_key = table_key(label, kernel, grid, read_bytes);
+    apply_preset(s, khz);
   }
   if (s.open) {
     Sample *o = s.open;
@@ -285,6 +326,10 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
         us_since(s.open_t) < kBurstGapUs) {   // the burst goes on, same gate
       sel.gate = o->cand >= 0 ? s.ticks[o->cand] : s.best;
       sel.timing = o;
+      // the caller owns the sample until store_gate_launched re-opens it: a select of
+      // this site from another thread meanwhile finds no open burst, so the sample can
+      // never be published to g_pending while the caller still records into it
+      s.open = nullptr;
       return sel;
     }
     close_burst_locked(s);
@@ -292,6 +337,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   int cand = -2;
   if (s.done) {
     sel.gate = s.best;
+    if (s.preset || g_frozen) return sel;   // a loaded / frozen gate is never timed
     if (++s.since_watch < s.watch_every) return sel;
     s.since_watch = 0;
     cand = -1;   // time this launch: a drift sample
@@ -304,6 +350,7 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     (void)hipGetLastError();
     return sel;
   }
+  close_bursts_locked(false);   // other sites' bursts whose last launch is past the gap
   if (!g_pending.empty()) harvest_locked();
   int c = cand;
   if (c == -2) {
@@ -379,6 +426,9 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
     return;
   }
   ++p->n;
+  // another thread may have opened a burst of this site while p was out: that one is
+  // complete as far as it goes, so it is published before p takes its place
+  if (s.open && s.open != p) close_burst_locked(s);
   s.open = p;   // open until kBurst launches, another tuned launch, a gap or a read-out
   s.open_sel = g_sel;
   s.open_lib = g_lib_launches.load(std::memory_order_relaxed);
@@ -406,9 +456,9 @@ int64_t gate_report(char *buf, int64_t len) {
   for (auto &kv : g_sites) {
     const Site &s = kv.second;
     std::snprintf(line, sizeof line,
-                  "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u retunes=%d watch=%d",
+                  "%s dev=%d grid=%lld bytes=%lld est=%.0f done=%d best=%u retunes=%d watch=%d preset=%d",
                   s.label.c_str(), s.dev, (long long)s.grid, (long long)s.bytes, s.est, s.done ? 1 : 0,
-                  s.best, s.retunes, s.watch_every);
+                  s.best, s.retunes, s.watch_every, s.preset ? 1 : 0);
     out += line;
     for (int c = 0; c < kCand; ++c) {
       if (s.ms[c].empty()) continue;
@@ -427,14 +477,95 @@ int64_t gate_report(char *buf, int64_t len) {
 
 int gate_retune() {
   std::lock_guard<std::mutex> lk(g_mu);
+  if (g_frozen) return 0;   // a frozen table stays as loaded
   close_bursts_locked(true);
   harvest_locked();
   int n = 0;
   for (auto &kv : g_sites) {
+    kv.second.preset = false;
     retune(kv.second);
     ++n;
   }
   return n;
+}
+
+// "<symbol> <grid> <bytes> <ticks>" per tuned site (loaded ones included)
+int64_t gate_export(char *buf, int64_t len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
+  harvest_locked();
+  std::map<std::string, uint32_t> table = g_preset;   // loaded entries this process never launched stay
+  for (auto &kv : g_sites)
+    if (kv.second.done && (kv.second.preset || !g_frozen || g_preset.count(kv.second.table_key)))
+      table[kv.second.table_key] = kv.second.best;
+  std::string out;
+  for (auto &kv : table) out += kv.first + " " + std::to_string(kv.second) + "\n";
+  if (buf && len > 0) {
+    const int64_t n = std::min<int64_t>(len - 1, (int64_t)out.size());
+    std::copy(out.begin(), out.begin() + n, buf);
+    buf[n] = '\0';
+  }
+  return (int64_t)out.size();
+}
+
+// parse gate_export's text; every existing site whose key is listed takes its gate
+int gate_import(const char *text) {
+  if (!text) return -1;
+  std::map<std::string, uint32_t> add;
+  const char *p = text;
+  while (*p) {
+    const char *e = p;
+    while (*e && *e != '\n') ++e;
+    std::string line(p, e);
+    p = *e ? e + 1 : e;
+    if (line.empty() || line[0] == '#') continue;
+    const size_t k = line.find_last_of(' ');
+    if (k == std::string::npos || k == 0) return -1;
+    char *end = nullptr;
+    const unsigned long v = std::strtoul(line.c_str() + k + 1, &end, 10);
+    if (end == line.c_str() + k + 1 || *end != '\0' || v > 0xffffffffull) return -1;
+    // the key is "<symbol> <grid> <bytes>": two numeric fields before the gate
+    const size_t k2 = line.find_last_of(' ', k - 1);
+    const size_t k1 = k2 == std::string::npos || k2 == 0 ? std::string::npos : line.find_last_of(' ', k2 - 1);
+    if (k1 == std::string::npos) return -1;
+    add[line.substr(0, k)] = (uint32_t)v;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  close_bursts_locked(true);
+  harvest_locked();
+  for (auto &kv : add) g_preset[kv.first] = kv.second;
+  for (auto &kv : g_sites) {
+    Site &s = kv.second;
+    if (s.grid == 0) continue;
+    auto it = add.find(s.table_key);
+    if (it == add.end()) continue;
+    s.preset = true;
+    s.best = it->second;
+    s.done = true;
+    s.best_ms = 0.0f;
+    ++s.gen;   // timings in flight belong to the tuning this replaces
+  }
+  return (int)add.size();
+}
+
+// on: no launch is timed from now on; sites still tuning take the default gate
+int gate_freeze(int on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int was = g_frozen ? 1 : 0;
+  g_frozen = on != 0;
+  if (g_frozen) {
+    close_bursts_locked(true);
+    for (auto &kv : g_sites) {
+      Site &s = kv.second;
+      if (s.grid == 0 || s.done) continue;
+      const int khz = device_wall_clock_khz(s.dev);
+      s.best = clamp_ticks(kDefault * s.est, khz);
+      s.done = true;
+      s.best_ms = 0.0f;
+      ++s.gen;
+    }
+  }
+  return was;
 }
 
 int gate_reset() {
@@ -459,5 +590,11 @@ int64_t vsiq_gate_report(char *buf, int64_t len) { return gate_report(buf, len);
 int vsiq_gate_reset(void) { return gate_reset(); }
 
 int vsiq_gate_retune(void) { return gate_retune(); }
+
+int64_t vsiq_gate_export(char *buf, int64_t len) { return gate_export(buf, len); }
+
+int vsiq_gate_import(const char *text) { return gate_import(text); }
+
+int vsiq_gate_freeze(int on) { return gate_freeze(on); }
 
 }  // extern "C"

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "host_simd.h"
+#include "mean_cascade.cuh"
 #include "vsiq_common.cuh"
 
 namespace vsiq {
@@ -518,6 +519,37 @@ int vsiq_host_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t
     if (grad_zp_out) grad_zp_out[c] = z * gscale;
   }
   return rc.load();
+}
+
+// K11 on the host: torch CPU's mean|act(x)| / mean act(x) bits (mean_cascade.cuh), the
+// chunks of torch's layout on the pool, the second pass in slot order
+int vsiq_host_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4) {
+  if (n < 0 || (n > 0 && !x) || !out4 || (vec != 8 && vec != 16) || threads < 1 || threads > 4096 ||
+      !act_ok(act))
+    return VSIQ_E_ARG;
+  const MeanLay m = mean_lay(n, threads);
+  const SiluLay L = act_lay(act, n);
+  std::vector<MAcc> cs((size_t)(m.nchunks > 0 ? m.nchunks : 1));
+  auto chunk = [&](int64_t c) {
+    const int64_t o = c * m.cs, len = std::min(m.cs, n - o);
+    switch (act_kind(act)) {
+      case kActRelu:
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActRelu>(x[o + i], o + i, L); }, len, vec);
+        break;
+      case kActSilu:
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActSilu>(x[o + i], o + i, L); }, len, vec);
+        break;
+      default:
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActNone>(x[o + i], o + i, L); }, len, vec);
+    }
+  };
+  Pool::get().run(m.nchunks, chunk);
+  const MAcc t = mean_final_seq([&](int64_t i) { return cs[(size_t)i]; }, m, vec, threads);
+  out4[0] = t.a;
+  out4[1] = t.s;
+  out4[2] = t.a / (float)n;
+  out4[3] = t.s / (float)n;
+  return 0;
 }
 
 int vsiq_host_threads(void) { return usable_cpus(); }

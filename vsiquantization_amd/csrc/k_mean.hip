@@ -1,0 +1,226 @@
+// k_mean.hip — K11: the reference's mean|x| and mean x of an observer call, bit for bit
+// as torch's CPU kernel sums them on the reference host (mean_cascade.cuh; reference
+// quantization_manager.py:66-67).  Opt-in (the manager's mean reference, _hip.py
+// set_mean_reference): one extra read of the tensor per call (4 B / element), because
+// torch's order cuts the tensor by its CPU threads, which no observer grid follows.
+//
+//   tiles  (grid: super-tiles x chunks, 256 lanes) every complete level-1 node of every
+//          chunk: B x B rows of 4V streams (V = 8: 8192 elements at B = 16).  A lane holds
+//          one stream of B / slots level-0 blocks, each a sequential fp32 sum of B rows
+//          (loads issued 16 at a time, adds in row order); the B level-0 sums of a stream
+//          meet in LDS and one lane sums them in block order -> ws.
+//   chunks (one 64-lane workgroup per chunk) per stream: the level-2 nodes and level 3
+//          from the level-1 nodes, the partial levels of the chunk's last rows straight
+//          from x, ((tail + l1) + l2) + l3; lane 0 then folds the tail vectors, the 4
+//          k-streams, the scalar tail and the V lanes -> the chunk's sum.
+//   final  (one lane) the `threads`-slot second pass, then sum / float(n).
+// Both sums (|act(x)| and act(x)) ride the same pass.  HBM: 4 B / element read; the
+// level-1 nodes (8 B per 256 elements at V = 8) are written once and read once.
+#include "mean_cascade.cuh"
+
+namespace vsiq {
+namespace {
+
+struct MeanArgs {
+  const float *x;
+  int64_t n, cs, nchunks, tiles_max;
+  MAcc *l1;     // [nchunks][tiles_max][4V]
+  MAcc *csum;   // [nchunks]
+  SiluLay L;
+};
+
+// rows / level power / B / tiles of the chunk starting at o
+struct ChunkGeo {
+  int64_t o, len, nv, rows, B, B2, tiles;
+  int lp;
+};
+
+__host__ __device__ inline ChunkGeo chunk_geo(int64_t n, int64_t cs, int64_t c, int V) {
+  ChunkGeo g;
+  g.o = c * cs;
+  g.len = n - g.o < cs ? n - g.o : cs;
+  g.nv = g.len / V;
+  g.rows = g.nv / 4;
+  g.lp = mean_level_power(g.rows);
+  g.B = (int64_t)1 << g.lp;
+  g.B2 = g.B << g.lp;
+  g.tiles = g.len < V ? 0 : g.rows / g.B2;
+  return g;
+}
+
+template <int V, int ACT>
+__global__ __launch_bounds__(256) void k_mean_tiles(MeanArgs a) {
+  constexpr int S = 4 * V, SLOTS = 256 / S;
+  extern __shared__ MAcc l0[];   // [B][S]
+  const int64_t c = blockIdx.y, tile = blockIdx.x;
+  const ChunkGeo g = chunk_geo(a.n, a.cs, c, V);
+  if (tile >= g.tiles) return;   // workgroup-uniform
+  const int s = threadIdx.x % S, q = threadIdx.x / S;
+  const int64_t e0 = g.o + tile * g.B2 * S + s;   // stream s of the tile's first row
+  for (int64_t b = q; b < g.B; b += SLOTS) {
+    MAcc acc{0.0f, 0.0f};
+    const int64_t eb = e0 + b * g.B * S;
+    for (int64_t r = 0; r < g.B; r += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = a.x[eb + (r + j) * S];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc_add(acc, mean_elem<ACT>(v[j], eb + (r + j) * S, a.L));
+    }
+    l0[b * S + s] = acc;
+  }
+  __syncthreads();
+  if (q == 0) {
+    MAcc l1{0.0f, 0.0f};
+    for (int64_t b = 0; b < g.B; ++b) acc_add(l1, l0[b * S + s]);
+    a.l1[(c * a.tiles_max + tile) * S + s] = l1;
+  }
+}
+
+template <int V, int ACT>
+__global__ __launch_bounds__(64) void k_mean_chunks(MeanArgs a) {
+  constexpr int S = 4 * V;
+  __shared__ MAcc p[S];
+  const int64_t c = blockIdx.x;
+  const ChunkGeo g = chunk_geo(a.n, a.cs, c, V);
+  const int s = threadIdx.x;
+  auto ld = [&](int64_t i) { return mean_elem<ACT>(a.x[g.o + i], g.o + i, a.L); };
+  if (g.len < V) {   // a chunk shorter than a vector: row_sum on scalars
+    if (s == 0) a.csum[c] = mean_chunk_seq(ld, g.len, V);
+    return;
+  }
+  if (s < S) {
+    const MAcc *l1 = a.l1 + c * a.tiles_max * S + s;
+    MAcc acc0{0.0f, 0.0f}, acc1{0.0f, 0.0f}, acc2{0.0f, 0.0f}, acc3{0.0f, 0.0f};
+    const int64_t n1 = g.tiles, n2 = n1 / g.B;
+    for (int64_t d = 0; d < n2; ++d) {   // complete level-2 nodes -> level 3
+      MAcc l2{0.0f, 0.0f};
+      for (int64_t k = 0; k < g.B; ++k) acc_add(l2, l1[(d * g.B + k) * S]);
+      acc_add(acc3, l2);
+    }
+    for (int64_t t = n2 * g.B; t < n1; ++t) acc_add(acc2, l1[t * S]);   // open level 2
+    int64_t r = n1 * g.B2;
+    for (; r + g.B <= g.rows; r += g.B) {   // complete level-0 blocks after the tiles -> open level 1
+      MAcc l0{0.0f, 0.0f};
+      for (int64_t j = 0; j < g.B; ++j) acc_add(l0, ld((r + j) * S + s));
+      acc_add(acc1, l0);
+    }
+    for (; r < g.rows; ++r) acc_add(acc0, ld(r * S + s));   // open level 0
+    acc_add(acc0, acc1);
+    acc_add(acc0, acc2);
+    acc_add(acc0, acc3);
+    p[s] = acc0;
+  }
+  __syncthreads();
+  if (s == 0) {
+    for (int64_t vi = g.rows * 4; vi < g.nv; ++vi)   // tail vectors -> stream k = 0
+      for (int l = 0; l < V; ++l) acc_add(p[l], ld(vi * V + l));
+    for (int k = 1; k < 4; ++k)
+      for (int l = 0; l < V; ++l) acc_add(p[l], p[k * V + l]);
+    MAcc fin{0.0f, 0.0f};
+    for (int64_t e = g.nv * V; e < g.len; ++e) acc_add(fin, ld(e));
+    for (int l = 0; l < V; ++l) acc_add(fin, p[l]);
+    a.csum[c] = fin;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_mean_final(const MAcc *csum, MeanLay m, int V, int threads, int64_t n,
+                                                   float *out4, double *stats) {
+  if (threadIdx.x != 0) return;
+  const MAcc t = mean_final_seq([&](int64_t i) { return csum[i]; }, m, V, threads);
+  const float fn = (float)n;
+  const float ma = t.a / fn, ms = t.s / fn;
+  if (out4) {
+    out4[0] = t.a;
+    out4[1] = t.s;
+    out4[2] = ma;
+    out4[3] = ms;
+  }
+  if (stats) {
+    stats[VSIQ_ST_MEANABS] = (double)ma;
+    stats[VSIQ_ST_MEAN] = (double)ms;
+  }
+}
+
+int64_t tiles_max_of(const MeanLay &m, int64_t n, int V) {
+  int64_t t = 0;
+  if (m.nchunks > 0) {
+    t = chunk_geo(n, m.cs, 0, V).tiles;
+    const int64_t tl = chunk_geo(n, m.cs, m.nchunks - 1, V).tiles;
+    if (tl > t) t = tl;
+  }
+  return t;
+}
+
+bool mean_args_ok(int64_t n, int vec, int threads) {
+  if (n < 0 || (vec != 8 && vec != 16) || threads < 1 || threads > 4096) return false;
+  const MeanLay m = mean_lay(n, threads);
+  return m.nchunks == 0 || chunk_geo(n, m.cs, 0, vec).lp <= kMeanMaxLevelPow;
+}
+
+template <int V, int ACT>
+void launch_mean(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
+  constexpr int S = 4 * V;
+  if (a.tiles_max > 0) {
+    const int64_t B = chunk_geo(a.n, a.cs, 0, V).B;
+    const int64_t Bl = chunk_geo(a.n, a.cs, a.nchunks - 1, V).B;
+    const size_t lds = (size_t)(B > Bl ? B : Bl) * S * sizeof(MAcc);
+    hipLaunchKernelGGL((k_mean_tiles<V, ACT>), dim3((unsigned)a.tiles_max, (unsigned)m.nchunks), dim3(256), lds, st,
+                       a);
+  }
+  hipLaunchKernelGGL((k_mean_chunks<V, ACT>), dim3((unsigned)m.nchunks), dim3(64), 0, st, a);
+}
+
+template <int ACT>
+void launch_mean8(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
+  launch_mean<8, ACT>(a, m, st);
+}
+
+template <int ACT>
+void launch_mean16(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
+  launch_mean<16, ACT>(a, m, st);
+}
+
+}  // namespace
+
+int64_t mean_ws_bytes(int64_t n, int vec, int threads) {
+  const MeanLay m = mean_lay(n, threads);
+  const int64_t tm = tiles_max_of(m, n, vec);
+  return (int64_t)sizeof(MAcc) * (m.nchunks * tm * 4 * vec + (m.nchunks > 0 ? m.nchunks : 1));
+}
+
+}  // namespace vsiq
+
+using namespace vsiq;
+
+extern "C" {
+
+int64_t vsiq_torch_mean_ws_bytes(int64_t n, int vec, int threads) {
+  if (!mean_args_ok(n, vec, threads)) return -1;
+  return mean_ws_bytes(n, vec, threads);
+}
+
+int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4, double *stats,
+                        void *ws, int64_t ws_bytes, hipStream_t st) {
+  if (!mean_args_ok(n, vec, threads) || !act_ok(act) || (n > 0 && !x) || !ws || (!out4 && !stats))
+    return VSIQ_E_ARG;
+  if (ws_bytes < mean_ws_bytes(n, vec, threads)) return VSIQ_E_WS;
+  const MeanLay m = mean_lay(n, threads);
+  MeanArgs a;
+  a.x = x;
+  a.n = n;
+  a.cs = m.cs;
+  a.nchunks = m.nchunks;
+  a.tiles_max = tiles_max_of(m, n, vec);
+  a.l1 = static_cast<MAcc *>(ws);
+  a.csum = a.l1 + m.nchunks * a.tiles_max * 4 * vec;
+  a.L = act_lay(act, n);
+  if (m.nchunks > 0) {
+    if (vec == 8) VSIQ_ACT(act, launch_mean8, a, m, st);
+    else VSIQ_ACT(act, launch_mean16, a, m, st);
+  }
+  hipLaunchKernelGGL(k_mean_final, dim3(1), dim3(64), 0, st, a.csum, m, vec, threads, n, out4, stats);
+  return launch_rc();
+}
+
+}  // extern "C"

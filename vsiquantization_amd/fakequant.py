@@ -658,6 +658,33 @@ def per_channel_observe_fq(x: torch.Tensor, *, symmetric: bool, qmin: int, qmax:
                 row_stats=rstats)
 
 
+def torch_mean(x: torch.Tensor, act=None, ref=None) -> torch.Tensor:
+    """K11: fp32[4] {sum|act(x)|, sum act(x), mean|act(x)|, mean act(x)} bit for bit as
+    torch's CPU kernel sums them on a host of layout ``ref`` = (vec, threads) (default
+    H.mean_reference(), else this process's threads) -- quantization_manager.py:66-67's
+    torch.mean(torch.abs(x)) / torch.mean(x).  On x's device (CPU tensors: the host loop)."""
+    if ref is None:
+        ref = H.mean_reference() or (8, torch.get_num_threads())
+    vec, threads = int(ref[0]), int(ref[1])
+    from . import host
+    if host.is_host(x):
+        x = x.contiguous()
+        out = torch.empty(4, dtype=torch.float32)
+        rc = H.lib().vsiq_host_torch_mean_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), vec, threads, H.ptr(out))
+        H.check(rc, "vsiq_host_torch_mean_f32")
+        return out
+    x = H.require_device_f32(x)
+    nb = int(H.lib().vsiq_torch_mean_ws_bytes(_i64(x.numel()), vec, threads))
+    if nb < 0:
+        raise ValueError(f"torch_mean: unsupported layout {ref} for {x.numel()} elements")
+    ws = torch.empty(max(nb, 8), dtype=torch.uint8, device=x.device)
+    out = torch.empty(4, dtype=torch.float32, device=x.device)
+    rc = H.lib().vsiq_torch_mean_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), vec, threads, H.ptr(out), None,
+                                     H.ptr(ws), _i64(ws.numel()), H.stream_of(x.device))
+    H.check(rc, "vsiq_torch_mean_f32")
+    return out
+
+
 def stats_from_row_sums(row_stats: torch.Tensor, numel: int) -> torch.Tensor:
     """[C,3] per-row (sum|x|, sum x, sum x^2) -> f64[3] fp32-rounded (mean|x|, mean, std)
     (quantization_manager.py:66-68), on the device, no sync."""

@@ -55,6 +55,18 @@ _OBS_STREAMS = {}
 _MGR_IDS = itertools.count()
 
 
+class DeferredSyncError(RuntimeError, AttributeError):
+    """A read of scale / zero_point that needs every rank's deferred records (call
+    sync_calibration first).  Also an AttributeError, so hasattr(manager, "scale") answers
+    False instead of raising; the other reads (stat lists, observer state) raise the plain
+    RuntimeError, since an AttributeError from a property would be replaced by a bare
+    "no attribute" one."""
+
+
+class _NeedsAllRanks(RuntimeError):
+    pass
+
+
 def _observer_stream(device, idx):
     pool = _OBS_STREAMS.get(device)
     if pool is None:
@@ -162,7 +174,10 @@ class QuantizationManager(nn.Module):
     # minmax.py:42-47).  The stat lists and the observer's min/max fold the same way.
     def __getattr__(self, name):
         if name in _QP_ATTRS and self.__dict__.get("_pending_records"):
-            self._fold_pending()
+            try:
+                self._fold_pending()
+            except _NeedsAllRanks as e:   # also an AttributeError here (hasattr)
+                raise DeferredSyncError(str(e)) from None
             return getattr(self, name)
         return nn.Module.__getattr__(self, name)
 
@@ -197,7 +212,7 @@ class QuantizationManager(nn.Module):
         if not pend:
             return
         if self.dist_group is not None:
-            raise RuntimeError("QuantizationManager: scale / zero_point / mean_abs_x / observer state read during "
+            raise _NeedsAllRanks("QuantizationManager: scale / zero_point / mean_abs_x / observer state read during "
                                "a deferred multi-GPU calibration; these need every rank's records -- call "
                                "vsiquantization_amd.distributed.sync_calibration(model) on every rank first")
         from ..distributed import fold_slots
@@ -228,8 +243,20 @@ class QuantizationManager(nn.Module):
                 for i in range(3):
                     self._host_stats[i].append(r[i])
 
-    def _record_stats(self, st3: torch.Tensor):
+    def _record_stats(self, st3: torch.Tensor, x=None, act=None):
+        """st3: (mean|x|, mean, std) of this call.  With a mean reference set
+        (H.set_mean_reference) and the call's tensor given, mean|x| / mean are replaced by
+        torch CPU's exact bits for that host layout (K11, fakequant.torch_mean)."""
+        if x is not None and H.mean_reference() is not None and self.dist_group is None:
+            m4 = self._exact_means(x, act)
+            st3 = st3.clone()
+            st3[:2] = m4[2:].to(torch.float64)
         self._dev_stats.append(st3)
+
+    @staticmethod
+    def _exact_means(x, act):
+        from ..fakequant import torch_mean
+        return torch_mean(x.detach(), act=act)
 
     # ------------------------------------------------------------------ observe
     def _device_observer(self, x) -> bool:
@@ -265,13 +292,13 @@ class QuantizationManager(nn.Module):
     def _observe_device(self, x, act):
         if isinstance(self.observer, PerChannelMinMaxObserver):
             rs = self.observer.observe(x, want_row_stats=True)
-            self._record_stats(stats_from_row_sums(rs, x.numel()))
+            self._record_stats(stats_from_row_sums(rs, x.numel()), x)
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
         elif self.dist_group is not None or self.dist_defer:
             self._collect_distributed(x, act)
         else:
             qp, st = self.observer.observe_device(x, act=act)
-            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1], x, act)
             self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
 
     def _observe_host(self, x):
@@ -282,7 +309,7 @@ class QuantizationManager(nn.Module):
             # running state and the mean|x| / mean / std record; qparams as the
             # reference's host numbers (minmax.py:49-74)
             _, st = obs.observe_device(x.detach(), want_qp=False)
-            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+            self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1], x)
             self.scale, self.zero_point = obs.get_scale_zero_point()
             return
         # third-party observer: the reference's host path
@@ -311,6 +338,7 @@ class QuantizationManager(nn.Module):
                 self._pending_records.append(slot)
             else:
                 self._pending_records.append(observe_parts(x, out=slot, act=act))
+            self._defer_exact(x, act)
             return
         _, st = observe_tensor(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
                                run_minmax=None, want_qp=False, want_stats=True, act=act)
@@ -321,20 +349,43 @@ class QuantizationManager(nn.Module):
         self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
         self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
 
+    def _defer_exact(self, x, act):
+        """A deferred call under a mean reference: its exact means (K11) now, while x is
+        alive; _apply_synced_records puts them in place of the records' means."""
+        ex = self.__dict__.setdefault("_exact_pending", [])
+        while len(ex) < len(self._pending_records) - 1:
+            ex.append(None)
+        ex.append(self._exact_means(x, act) if (H.mean_reference() is not None and self.dist_group is None)
+                  else None)
+
     def _apply_synced_records(self, recs):
-        """recs: CPU f64 [k, ST_LEN], already all-reduced; replay the running state."""
+        """recs: CPU f64 [k, ST_LEN], already all-reduced; replay the running state.  Every
+        value is computed first; the pending records are dropped only when that worked
+        (a failing replay leaves the manager as it was, its calls still pending)."""
         from ..distributed import replay_minmax
         mn, mx = self._calib_init
-        self._pending_records = []
-        self._calib_init = None
+        exact = self.__dict__.get("_exact_pending") or []
+        if any(e is not None for e in exact):
+            recs = recs.clone()
+            for i, e in enumerate(exact[:recs.shape[0]]):
+                if e is not None:
+                    m = e.cpu()
+                    recs[i, H.ST_MEANABS] = float(m[2])
+                    recs[i, H.ST_MEAN] = float(m[3])
+        mn, mx = replay_minmax(mn, mx, recs[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
+        cols = [recs[:, col].tolist() for col in (H.ST_MEANABS, H.ST_MEAN, H.ST_STD)]
+        # commit: no pending records from here on, so the writes below do not fold again
+        d = self.__dict__
+        d["_pending_records"] = []
+        d.pop("_exact_pending", None)
+        d["_calib_init"] = None
         obs = self.observer
         if isinstance(obs, MinMaxObserver):
             obs._defer_owner = None
-        mn, mx = replay_minmax(mn, mx, recs[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
         obs.min_val, obs.max_val = mn, mx
         self._materialize_stats()
-        for i, col in enumerate((H.ST_MEANABS, H.ST_MEAN, H.ST_STD)):
-            self._host_stats[i].extend(recs[:, col].tolist())
+        for i, col in enumerate(cols):
+            self._host_stats[i].extend(col)
         self.scale, self.zero_point = obs.get_scale_zero_point()
 
     def _act_fusable(self, x) -> bool:
@@ -387,7 +438,7 @@ class QuantizationManager(nn.Module):
                 and isinstance(self.quantizer, PerChannelUniformQuantizer) and self._device_observer(x)):
             # fused per-channel observe + quantize: one read, one write of x
             y, rs = self.observer.observe_quantize(x, self.quantizer, want_row_stats=True)
-            self._record_stats(stats_from_row_sums(rs, x.numel()))
+            self._record_stats(stats_from_row_sums(rs, x.numel()), x)
             self.scale, self.zero_point = self.observer.get_scale_zero_point()
             return y
         if act is None or self._act_fusable(x):
@@ -417,6 +468,7 @@ class QuantizationManager(nn.Module):
         slot = torch.empty(part_out_slot_doubles(x.numel()), dtype=torch.float64, device=x.device)
         y, _ = observe_parts_out(x, act, out=slot)
         self._pending_records.append(slot)
+        self._defer_exact(x, act)
         return y
 
     def _observe_quantize_ranks(self, x, act):
@@ -477,7 +529,7 @@ class QuantizationManager(nn.Module):
             y, qp, st, _, _ = observe_fake_quant(x, symmetric=obs.symmetric, num_bits=obs.num_bits, eps=obs.eps,
                                                  qmin=q.qmin, qmax=q.qmax, run_minmax=state, act=act)
         obs._dirty = True
-        self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1])
+        self._record_stats(st[H.ST_MEANABS:H.ST_STD + 1], x, act)
         self.scale, self.zero_point = qp[H.QP_SCALE], qp[H.QP_ZP]
         return y
 
