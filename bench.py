@@ -804,9 +804,11 @@ class ActQuant:
                 rc |= self.f_obs(*t["obs"])
                 rc |= self.f_fq(*t["fq"])
             return rc
+        from vsiquantization_amd.distributed import collective_group
+        grp = collective_group(None)   # under a HIP-graph capture: the world's capture-only twin
         for t in self.L:   # local K2 pass, ONE all_gather of the 10-double records, ONE fold + fq launch
             rc |= self.f_obs(*t["obs"])
-            dist.all_gather_into_tensor(t["gat"], t["st"])
+            dist.all_gather_into_tensor(t["gat"], t["st"], group=grp)
             rc |= self.f_rfq(*t["rfq"])
         return rc
 
@@ -1130,7 +1132,9 @@ def capture_groups(W, groups, nphase):
     from vsiquantization_amd.utils.graph import quiesce_collectives
     stream = torch.cuda.current_stream()
     out = []
-    quiesce_collectives()   # RCCL's watchdog must hold no collective to poll during the captures
+    # every collective captured below runs on its group's capture-only twin (RCCL), which
+    # never runs an eager collective (vsiquantization_amd.distributed.prepare_capture)
+    quiesce_collectives()
     try:
         for g0, cnt in groups:
             cap = _GroupCapture(stream)
@@ -1329,7 +1333,10 @@ def _report(W, steps, world, dt, dur, names, settle, gate_sites):
     return {"value": total / dt / 1e6, "ms_per_step": dt / steps * 1e3, "self_check": ok,
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc_traffic(W.key, dom)},
+                         "traffic": load_pmc_traffic(W.key, dom),
+                         # the whole timed step: every phase's algorithmic bytes over the
+                         # wall time per step (launch gaps and host time included)
+                         "step_frac": sum(W.kernels.values()) / (dt / steps) / 1e9 / HBM_PEAK_GBS},
             "kernels": per_kernel,
             "store_gate": {"settle_steps": settle, "sites": gate_sites}}
 
@@ -1667,8 +1674,9 @@ def compact_summary(out) -> str:
         ks = ",".join(f"{k}={v['frac']:.3f}" for k, v in d.get("kernels", {}).items()
                       if isinstance(v, dict) and v.get("frac") and v.get("in_step", True))
         cb = (d.get("cpu_baseline") or {}).get("value")
+        sf = (d.get("roofline") or {}).get("step_frac")
         return (f"{name} {d['value']:.1f}Melem/s {1e3 * d['ms_per_step']:.2f}us {d.get('launch', '')[:6]} [{ks}]"
-                + (f" cpu={cb:.1f}" if cb else ""))
+                + (f" step={sf:.3f}" if sf else "") + (f" cpu={cb:.1f}" if cb else ""))
     parts = [leg(out["config"].get("workload", "")[:2], out)]
     parts += [leg(k, v) for k, v in (out.get("configs") or {}).items()]
     if "batched_act_quant" in out:

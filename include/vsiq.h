@@ -146,7 +146,7 @@ int64_t vsiq_gate_export(char *buf, int64_t len);
 /* Trace marker (ABI 11): one empty kernel, `vsiq_timed_region_marker`, grid 1 (end 0) or
  * grid 2 (end 1), so a kernel trace can be cut to the region between the two
  * (tools/timed_region_stats.py; bench.py --markers). */
-int vsiq_trace_marker(int end, hipStream_t stream);
+int vsiq_trace_marker(int end, void *stream);
 
 /*
  * K11 (ABI 11): the reference's per-call mean|x| and mean x BIT FOR BIT as torch's CPU
@@ -165,7 +165,7 @@ int vsiq_trace_marker(int end, hipStream_t stream);
  */
 int64_t vsiq_torch_mean_ws_bytes(int64_t n, int vec, int threads);
 int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4, double *stats,
-                        void *ws, int64_t ws_bytes, hipStream_t stream);
+                        void *ws, int64_t ws_bytes, void *stream);
 /* The same on a host (CPU) tensor, out4 in host memory; chunks on the host pool. */
 int vsiq_host_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4);
 int vsiq_gate_import(const char *text);

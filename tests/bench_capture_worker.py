@@ -37,8 +37,15 @@ def main():
     same = all(torch.equal(t["y"].view(torch.int32), y.view(torch.int32)) and torch.equal(t["qp"], qp)
                and torch.equal(t["rmm"], rmm) for t, (y, qp, rmm) in zip(W.L, ref))
     r = bench.measure(W, 4, 2, 1)
+    from vsiquantization_amd import distributed as D
+    twin = D.capture_group()
+    # the world still runs eager collectives after the captures (its stream never joined one)
+    t = torch.ones(1, device=dev)
+    dist.all_reduce(t)
     print(json.dumps({"graph_equals_direct": bool(same), "launch": r["launch"], "self_check": r["self_check"],
-                      "alt": r.get("alt_launch", {}).get("launch"), "frac": r["roofline"]["frac"]}), flush=True)
+                      "alt": r.get("alt_launch", {}).get("launch"), "frac": r["roofline"]["frac"],
+                      "capture_twin": twin is not None and twin is not dist.group.WORLD,
+                      "world_after": float(t)}), flush=True)
     dist.destroy_process_group()
 
 

@@ -60,6 +60,8 @@ def graph_replay(cfg, acts, shard):
         torch.cuda.synchronize()
         ok &= all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(ys, eager))
         ok &= all(torch.equal(x.grad.view(torch.int32), b.view(torch.int32)) for x, b in zip(xs, eager_g))
+    from vsiquantization_amd import distributed as D
+    ok &= D.capture_group() is not None   # the captured all_gathers ran on the capture-only twin
     return {"replays_equal_eager": bool(ok), "layers": len(xs),
             "y_sum": float(np.sum([float(y.double().sum()) for y in eager]))}
 

@@ -32,4 +32,6 @@ def test_act_leg_graph_capture_with_rccl_exchange():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     got = json.loads(line)
     assert got["graph_equals_direct"] and got["self_check"], got
+    # the captured all_gathers ran on the world's capture-only twin
+    assert got["capture_twin"] and got["world_after"] == 1.0, got
     assert got["launch"] in ("direct", "hip graph per phase and group") and got["alt"] is not None, got

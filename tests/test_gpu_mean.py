@@ -68,15 +68,16 @@ def test_k11_stats_record_and_errors():
     st = torch.zeros(H.ST_LEN, dtype=torch.float64, device=DEV)
     nb = int(H.lib().vsiq_torch_mean_ws_bytes(5000, 8, 8))
     ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
-    rc = H.lib().vsiq_torch_mean_f32(H.ptr(x), 5000, 0, 8, 8, None, H.ptr(st), H.ptr(ws), nb, H.stream_of(DEV))
+    rc = H.lib().vsiq_torch_mean_f32(H.ptr(x), 5000, 0, 8, 8, None, H.ptr(st), H.ptr(ws), nb, H.stream_of(x.device))
     assert rc == 0
     xs = x.cpu().numpy()
     assert float(st[H.ST_MEANABS]) == float(O.torch_mean(xs, 1, 8))
     assert float(st[H.ST_MEAN]) == float(O.torch_mean(xs, 0, 8))
+    torch.cuda.synchronize()
     assert float(st[H.ST_MIN]) == 0.0   # nothing else written
     assert H.lib().vsiq_torch_mean_ws_bytes(5000, 4, 8) == -1
     assert H.lib().vsiq_torch_mean_f32(H.ptr(x), 5000, 0, 8, 8, None, H.ptr(st), H.ptr(ws), nb - 1,
-                                       H.stream_of(DEV)) != 0
+                                       H.stream_of(x.device)) != 0
 
 
 @pytest.mark.parametrize("path", ["per_call", "deferred_relu", "observe_quantize"])

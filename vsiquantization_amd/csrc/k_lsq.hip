@@ -384,8 +384,12 @@ __global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict_
 // total -- grad_scale[c] / grad_zp[c] are written directly (no records, no fold
 // launch), and one-round grids store behind the store gate.  Same per-element code
 // (lsq_group_out) as the two-stage form; the f64 sums differ only in order.
+// At least 4 waves per SIMD (<= 128 VGPRs): 4 workgroups per CU, so the 1024 rows of a
+// C2-shaped weight are ONE round on 256 CUs.  Without it the learnable zero point's
+// variant (ZPL, 9 groups per lane) took 134 VGPRs = 3 workgroups per CU = a second,
+// quarter-occupied round (round 5: 24.2 us for 113 MB, 0.585 of 8 TB/s).
 template <bool VEC, bool NT, bool ZPL, int NV>
-__global__ __launch_bounds__(kBlock) void k_pcr_lsq_bwd(const float *__restrict__ g,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_pcr_lsq_bwd(const float *__restrict__ g,
                                                         const float *__restrict__ x,
                                                         float *__restrict__ gx, int64_t rowlen,
                                                         const double *__restrict__ scale,

@@ -14,7 +14,7 @@ __global__ __launch_bounds__(64) void vsiq_timed_region_marker(int tag) {
 
 }  // namespace vsiq
 
-extern "C" int vsiq_trace_marker(int end, hipStream_t st) {
-  hipLaunchKernelGGL(vsiq::vsiq_timed_region_marker, dim3(end ? 2u : 1u), dim3(64), 0, st, end);
+extern "C" int vsiq_trace_marker(int end, void *stream) {
+  hipLaunchKernelGGL(vsiq::vsiq_timed_region_marker, dim3(end ? 2u : 1u), dim3(64), 0, (hipStream_t)stream, end);
   return vsiq::launch_rc();
 }

@@ -201,7 +201,8 @@ int64_t vsiq_torch_mean_ws_bytes(int64_t n, int vec, int threads) {
 }
 
 int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads, float *out4, double *stats,
-                        void *ws, int64_t ws_bytes, hipStream_t st) {
+                        void *ws, int64_t ws_bytes, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
   if (!mean_args_ok(n, vec, threads) || !act_ok(act) || (n > 0 && !x) || !ws || (!out4 && !stats))
     return VSIQ_E_ARG;
   if (ws_bytes < mean_ws_bytes(n, vec, threads)) return VSIQ_E_WS;

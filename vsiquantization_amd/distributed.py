@@ -37,6 +37,85 @@ from . import _hip as H
 
 _SUM_SLICE = slice(H.ST_NAN, H.ST_N + 1)
 
+# ---------------------------------------------------------------- HIP-graph capture groups
+# A collective of this package issued inside a HIP-graph capture on RCCL runs on a
+# capture-only TWIN of its process group (prepare_capture): a communicator that never
+# runs an eager collective.  So, by construction, (1) no eager and captured RCCL
+# operations are ever mixed on one communicator, (2) the eager group's NCCL stream never
+# joins a capture, and (3) the twin's ProcessGroupNCCL watchdog never holds a work to
+# poll (captured collectives are never listed and graph replays list nothing) -- the
+# three ways a capture could meet the watchdog or RCCL's eager state (round 5 saw one
+# watchdog SIGABRT inside such a capture; tools/exp/rccl_capture_probe.py shows polling a
+# listed work's event during a capture does not fail by itself on this ROCm).
+_TWINS = {}   # id(group) -> (group, its capture-only twin)
+_USED = {}    # id(group) -> group: groups this package's collectives ran on, first-use order
+
+
+def _world(group):
+    return group if group is not None else dist.group.WORLD
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _resolve(group):
+    """The process group a collective of this package runs on: `group`, or under a
+    HIP-graph capture on RCCL its capture-only twin (prepare_capture must have created it:
+    groups cannot be created inside a capture)."""
+    g = _world(group)
+    _USED.setdefault(id(g), g)
+    if _capturing() and dist.get_backend(g) == "nccl":
+        tw = _TWINS.get(id(g))
+        if tw is None:
+            raise RuntimeError("an RCCL collective of vsiquantization_amd inside a HIP-graph capture needs the "
+                               "group's capture-only twin: call vsiquantization_amd.distributed.prepare_capture() "
+                               "on every rank before capturing (GraphedStep and bench.capture_groups do)")
+        return tw[1]
+    return group
+
+
+collective_group = _resolve   # public name: the group to pass to a collective issued by hand
+
+
+def capture_group(group=None):
+    """The capture-only twin of `group` (None: the world) after prepare_capture, else None."""
+    tw = _TWINS.get(id(_world(group)))
+    return tw[1] if tw else None
+
+
+def prepare_capture(groups=None) -> int:
+    """Create (collectively: every rank calls it, with the same groups) the capture-only
+    RCCL twin of every group this package's collectives have used so far -- or of
+    `groups` -- plus the world, eagerly initialised on the current device.  Idempotent;
+    nothing to do without an NCCL process group.  Returns the number of twins."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    gs = [_world(g) for g in groups] if groups is not None else list(_USED.values())
+    gs.append(dist.group.WORLD)
+    uniq = {}
+    for g in gs:
+        uniq.setdefault(id(g), g)
+    # the same creation order on every rank: by member ranks (first use breaks ties)
+    order = [g for g in sorted(uniq.values(), key=lambda g: tuple(dist.get_process_group_ranks(g)))
+             if id(g) not in _TWINS and dist.get_backend(g) == "nccl"]
+    if order:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    for g in order:
+        twin = dist.new_group(dist.get_process_group_ranks(g), backend="nccl", device_id=dev)
+        _TWINS[id(g)] = (g, twin)
+    return len(_TWINS)
+
+
+def release_capture_groups():
+    """Destroy the capture-only twins (e.g. before destroy_process_group of their groups)."""
+    for g, twin in list(_TWINS.values()):
+        try:
+            dist.destroy_process_group(twin)
+        except Exception:  # noqa: BLE001  (already torn down with the world)
+            pass
+    _TWINS.clear()
+
 
 def finish_stats(stats: torch.Tensor) -> torch.Tensor:
     """Recompute the fp32-rounded mean|x|, mean, std entries from the sums (in place)."""
@@ -56,6 +135,7 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     """All-reduce observer stats records ``[..., ST_LEN]`` across ranks, in place."""
     mm = torch.stack([-stats[..., H.ST_MIN], stats[..., H.ST_MAX]], dim=-1).contiguous()
     sums = stats[..., _SUM_SLICE].contiguous()
+    group = _resolve(group)
     dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     stats[..., H.ST_MIN] = -mm[..., 0]
@@ -71,7 +151,7 @@ def gather_stats(stats: torch.Tensor, group=None, out: torch.Tensor | None = Non
     world = dist.get_world_size(group)
     if out is None:
         out = torch.empty(world * H.ST_LEN, dtype=stats.dtype, device=stats.device)
-    dist.all_gather_into_tensor(out, stats.contiguous(), group=group)
+    dist.all_gather_into_tensor(out, stats.contiguous(), group=_resolve(group))
     return out
 
 
@@ -198,7 +278,7 @@ def check_call_counts(counts, device, group=None):
         h = (h * 1000003 + int(c) + 1) % 2147483647
     head = torch.tensor([len(counts), sum(counts), h], dtype=torch.float64)
     both = torch.cat([head, -head]).to(device)
-    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=_resolve(group))
     hi, lo = both[:3].cpu(), -both[3:].cpu()
     if not torch.equal(hi, lo):
         raise RuntimeError(f"sync_calibration: ranks hold different deferred observer calls "

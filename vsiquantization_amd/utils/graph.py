@@ -18,26 +18,21 @@ capture, steps until the store-gate tuner has settled every launch site the step
 """
 from __future__ import annotations
 
-import time
-
 import torch
 
 from .. import _hip as H
 
 
-def quiesce_collectives(settle_s: float = 0.3) -> None:
-    """Call right before a HIP-graph capture.  Finishes the device's work and, under an
-    NCCL (RCCL) process group, gives ProcessGroupNCCL's watchdog thread time to drop the
-    completed collectives from its list: it polls each listed collective's event every
-    ~100 ms and aborts the process if a poll fails, and a poll that lands inside a
-    capture can fail on HIP even in thread_local capture mode (seen as a rare SIGABRT,
-    "watchdog thread terminated with exception", in a 1-rank RCCL capture test).
-    Collectives issued under capture are never listed, so an empty list stays empty
-    for the capture."""
+def quiesce_collectives(groups=None) -> None:
+    """Call right before a HIP-graph capture: finishes the device's work and, under RCCL,
+    makes sure every group this package's collectives use has its capture-only twin
+    (vsiquantization_amd.distributed.prepare_capture; collective: every rank calls it).
+    The collectives captured next run on the twins, which never run an eager collective,
+    so no eager and captured RCCL work meet on one communicator (no timed wait: round 5's
+    0.3 s settle for ProcessGroupNCCL's watchdog is gone)."""
     torch.cuda.synchronize()
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        time.sleep(settle_s)
+    from .. import distributed as D
+    D.prepare_capture(groups)
 
 
 def _detached(v):
