@@ -265,6 +265,52 @@ class C2PerChannel:
         return {"avg_us": us, "alg_bytes": alg, "GBps": alg / us / 1e3, "frac": alg / us / 1e3 / 8000.0,
                 "codes_match_y": ok}
 
+    def alt_kernels(self, groups=25):
+        """SURVEY §8f2 at the north-star shape (not in the headline step): the LEARNABLE
+        per-channel quantizer on this weight (LSQFakeQuantize / a learnable
+        PerChannelUniformQuantizer on axis 0, lsq_module.py:96-175, 317-340) -- the forward
+        with the rounded learned zero point (vsiq_pcm_fq_fwd_f32, 8 B/elem) and the K6
+        backward with scale and zero point learned (vsiq_pcm_lsq_bwd_f32, reads x and g,
+        writes dx: 12 B/elem), each timed like the headline: groups of one launch per slot
+        between HIP events, after the store-gate tuner has settled the site."""
+        if self.key != "c2":
+            return {}
+        H, C, n = self.H, self.shape[0], self.n
+        lib = H.lib()
+        dev = self.slots[0]["x"].device
+        st = H.stream_of(dev)
+        wsn = int(lib.vsiq_pcm_workspace_doubles(C, self.rowlen))
+        ws = torch.empty(max(wsn, 2), dtype=torch.float64, device=dev)
+        gsc = torch.empty(C, dtype=torch.float64, device=dev)
+        gzp = torch.empty(C, dtype=torch.float64, device=dev)
+        fwd, bwd = [], []
+        for s in self.slots:
+            P = {k: H.ptr(s[k]) for k in ("x", "y", "g", "gx", "scale", "zp")}
+            fwd.append((P["x"], P["y"], None, None, H.c_i64(C), H.c_i64(self.rowlen), H.c_i64(C), P["scale"], P["zp"],
+                        1, self.qmin, self.qmax, st))
+            bwd.append((P["g"], P["x"], P["gx"], H.c_i64(C), H.c_i64(self.rowlen), H.c_i64(C), P["scale"], P["zp"], 1,
+                        self.qmin, self.qmax, 1e-4, H.ptr(gsc), H.ptr(gzp), H.ptr(ws), H.c_i64(ws.numel()), st))
+        out = {}
+        for name, f, args, alg in (("pc_learn_fwd", lib.vsiq_pcm_fq_fwd_f32, fwd, 8 * n),
+                                   ("pc_learn_bwd_k6", lib.vsiq_pcm_lsq_bwd_f32, bwd, 12 * n)):
+            for k in range(4000):
+                assert f(*args[k % len(args)]) == 0
+                if k % 8 == 7:
+                    torch.cuda.synchronize()
+                    if H.gate_tuning_pending() == 0:
+                        break
+            evs = [(timing_event(), timing_event()) for _ in range(groups)]
+            for e0, e1 in evs:
+                e0.record()
+                for a in args:
+                    assert f(*a) == 0
+                e1.record()
+            torch.cuda.synchronize()
+            us = sum(e0.elapsed_time(e1) for e0, e1 in evs) / (groups * len(args)) * 1e3
+            out[name] = {"avg_us": us, "alg_bytes": alg, "GBps": alg / us / 1e3, "frac": alg / us / 1e3 / 8000.0,
+                         "in_step": False}
+        return out
+
     def check(self):
         """Slot 0, 64 rows spread over the tensor, against the reference's formulas restated
         in torch on the host (minmax.py:49-74 in float64, uniform.py:55,95 with IEEE fp32
@@ -1671,8 +1717,8 @@ def compact_summary(out) -> str:
     def leg(name, d):
         if "error" in d:
             return f"{name} FAILED {d['error'][:120]}"
-        ks = ",".join(f"{k}={v['frac']:.3f}" for k, v in d.get("kernels", {}).items()
-                      if isinstance(v, dict) and v.get("frac") and v.get("in_step", True))
+        ks = ",".join(f"{k}={v['frac']:.3f}" + ("" if v.get("in_step", True) else "*")
+                      for k, v in d.get("kernels", {}).items() if isinstance(v, dict) and v.get("frac"))
         cb = (d.get("cpu_baseline") or {}).get("value")
         sf = (d.get("roofline") or {}).get("step_frac")
         return (f"{name} {d['value']:.1f}Melem/s {1e3 * d['ms_per_step']:.2f}us {d.get('launch', '')[:6]} [{ks}]"

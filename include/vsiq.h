@@ -119,8 +119,8 @@ int vsiq_set_tuning(int key, int value);
  *   vsiq_gate_report: one text line per site (label, grid, bytes, chosen ticks, median
  *     launch time per candidate in us) into buf (NUL-terminated, truncated to len);
  *     returns the full length;
- *   vsiq_gate_reset: forget every site (returns 1 and keeps them while timings are
- *     still in flight).
+ *   vsiq_gate_reset: forget every site and every gate loaded by vsiq_gate_import
+ *     (returns 1 and keeps them while timings are still in flight).
  */
 int vsiq_gate_tuning_pending(void);
 int64_t vsiq_gate_report(char *buf, int64_t len);

@@ -204,3 +204,50 @@ def test_burst_sample_never_spans_another_library_launch():
     assert " done=1 " in line, H.gate_report()
     meds = [float(t.split(":")[1]) for t in line.split() if ":" in t and t.split(":")[0].isdigit()]
     assert len(meds) >= 12 and max(meds) < 30.0, line
+
+
+def test_gate_table_save_load_freeze(tmp_path):
+    """A tuned table saved (vsiq_gate_export), reset, loaded and frozen: every site launched
+    again takes its saved gate and is never timed (no candidate medians in the report, no
+    drift samples), results stay bitwise, and a site missing from the table runs the fixed
+    default without tuning.  Unfreezing restores online tuning."""
+    shape = (1024, 1024, 3, 3)
+    rng = np.random.default_rng(9)
+    w = (rng.standard_normal(shape) * 0.05).astype(np.float32)
+    ref = O.per_channel_observe_fq(w, False, 8)
+    x = torch.from_numpy(w).to(DEV)
+    _reset()
+    for i in range(600):
+        FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)
+        if i % 16 == 15:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    assert H.gate_tuning_pending() == 0
+    path = str(tmp_path / "gates.txt")
+    nsaved = H.gate_save(path)
+    saved = {l.rsplit(" ", 1)[0]: int(l.rsplit(" ", 1)[1]) for l in open(path).read().splitlines()}
+    assert nsaved >= 1 and any("k_pc_observe_fq" in k for k in saved)
+    _reset()
+    try:
+        assert H.gate_load(path) == nsaved
+        for i in range(200):
+            y = FQ.per_channel_observe_fq(x, symmetric=False, qmin=0, qmax=255)["y"]
+        # a different grid (768 rows): not in the table -> the fixed default, untimed
+        x2 = torch.from_numpy((rng.standard_normal((768, 512, 3, 3)) * 0.05).astype(np.float32)).to(DEV)
+        for i in range(50):
+            FQ.per_channel_observe_fq(x2, symmetric=False, qmin=0, qmax=255)
+        torch.cuda.synchronize()
+        G.assert_bitwise_f32(y.cpu().numpy(), ref["y"], "y (frozen table)")
+        assert H.gate_tuning_pending() == 0
+        for line in H.gate_report().splitlines():
+            f = line.split()
+            assert " done=1 " in line and not any(":" in t for t in f[1:]), line   # nothing timed
+            if "grid=1024 " in line and f[0] == "k3_pc_observe_fq":
+                assert " preset=1 " in line + " ", line
+        exported = {l.rsplit(" ", 1)[0]: int(l.rsplit(" ", 1)[1]) for l in H.gate_export().splitlines()}
+        for k, v in saved.items():
+            assert exported.get(k) == v, (k, v, exported.get(k))
+        assert H.gate_retune() == 0   # frozen: nothing re-tunes
+    finally:
+        H.gate_freeze(False)
+        _reset()

@@ -574,6 +574,7 @@ int gate_reset() {
   harvest_locked();
   if (!g_pending.empty()) return 1;   // samples in flight keep their sites alive
   g_sites.clear();
+  g_preset.clear();   // and every loaded gate (the frozen flag stays as set)
   return 0;
 }
 

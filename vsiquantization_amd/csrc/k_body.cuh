@@ -104,7 +104,10 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
     const float t1 = g * (e.q - p.z);         // MulBackward0 (other)
     const float t2 = (-gm) * fdiv_fast_nz(u, p.d);   // DivBackward0 (other): -(gm) * ((x/s)/s)
     acc.t += (double)t1 + (double)t2;
-    if (ZPL) acc.z += (double)gm + (double)(-gq);   // AddBackward0 + SubBackward0 (other)
+    // AddBackward0 + SubBackward0 (other): gm + (-gq) is +0 when in range (acc starts at
+    // +0 and never becomes -0, so adding +0 is a no-op) and -gq when clamped -- the same
+    // bits with one conversion and one f64 add fewer
+    if (ZPL) acc.z += e.m ? 0.0 : -(double)gq;
     // DivBackward0 (self): ste_quot_d from the product already formed; 0/s signed like IEEE
     const float qd = __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-g, p.d.b, gq), p.d.r, g), gq);
     return e.m ? qd : 0.0f * p.d.r;
@@ -121,7 +124,7 @@ __device__ __forceinline__ float lsq_elem(float x, float g, const QP &p, LsqAcc 
   // lanes past the tensor's end (valid false) add +0 terms: selects, not exec branches
   // (acc starts at +0.0, so adding +0.0 never changes its bits)
   acc.t += valid ? (double)t1 + (double)t2 : 0.0;
-  if (ZPL) acc.z += valid ? (double)gm + (double)(-gq) : 0.0;   // AddBackward0 + SubBackward0 (other)
+  if (ZPL) acc.z += (valid && !m) ? -(double)gq : 0.0;   // AddBackward0 + SubBackward0 (other), as above
   return fdiv_t<IEEE>(gm, p.d);             // DivBackward0 (self)
 }
 

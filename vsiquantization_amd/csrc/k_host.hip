@@ -225,6 +225,78 @@ inline float fq(float x, const HQP &p, int discrete, bool *m, uint8_t *code) {
   return discrete ? q : (q - p.z) * p.s;
 }
 
+// One segment of at most kChunk elements, no activation: exactly what the per-tensor
+// entry points below do on one chunk (the AVX-512 loop where the CPU has it, else the
+// scalar loop in its 16-lane order), so a short row processed here gives the bits of a
+// per-tensor call on that row -- without that call's allocation and per-call setup.
+// (segments shorter than kSegSimd run the scalar loop: the same bits, without the AVX-512
+// call's setup -- an [N, C] activation's rows are one element each)
+constexpr int64_t kSegSimd = 64;
+
+inline void fq_seg(const float *x, float *y, uint8_t *mask, int64_t len, const HQP &p) {
+  if (len >= kSegSimd && use_simd(kActNone)) {
+    simd::fq(x, y, nullptr, mask, len, 0, p.s, p.z, p.lo, p.hi, 0);
+    return;
+  }
+  for (int64_t i = 0; i < len; ++i) {
+    bool m;
+    uint8_t c;
+    y[i] = fq(x[i], p, 0, &m, &c);
+    if (mask) mask[i] = m;
+  }
+}
+
+inline void ste_seg(const float *g, const uint8_t *mask, float *gx, int64_t len, float s) {
+  if (len >= kSegSimd && use_simd(kActNone)) {
+    simd::ste(g, mask, nullptr, gx, len, 0, s);
+    return;
+  }
+  for (int64_t i = 0; i < len; ++i) gx[i] = (mask[i] ? g[i] * s : 0.0f) / s;
+}
+
+// autograd of uniform.py:47-56 term by term (k_body.cuh lsq_elem): gx and {sum t, sum z}
+inline void lsq_seg(const float *g, const float *x, float *gx, int64_t len, const HQP &p, int zp_learn,
+                    double out[2]) {
+  if (len >= kSegSimd && use_simd(kActNone)) {
+    simd::lsq(g, x, gx, len, 0, p.s, p.z, p.lo, p.hi, zp_learn, out);
+    return;
+  }
+  double lt[kLanes] = {}, lz[kLanes] = {};
+  auto elem = [&](int64_t i, double *st, double *sz) {
+    const float u = x[i] / p.s;
+    const float r = __builtin_rintf(u + p.z);
+    const float q = r < p.lo ? p.lo : (r > p.hi ? p.hi : r);
+    const bool m = r >= p.lo && r <= p.hi;
+    const float gq = g[i] * p.s;
+    const float gm = m ? gq : 0.0f;
+    const float t1 = g[i] * (q - p.z);
+    const float xs = u / p.s;
+    const float t2 = (-gm) * xs;
+    *st += (double)t1 + (double)t2;
+    if (zp_learn) *sz += (double)gm + (double)(-gq);
+    gx[i] = gm / p.s;
+  };
+  int64_t i = 0;
+  for (; i + kLanes <= len; i += kLanes)
+    for (int k = 0; k < kLanes; ++k) elem(i + k, &lt[k], &lz[k]);
+  double st = 0.0, sz = 0.0;
+  for (int k = 0; k < kLanes; ++k) st += lt[k], sz += lz[k];
+  for (; i < len; ++i) elem(i, &st, &sz);
+  out[0] = st;
+  out[1] = sz;
+}
+
+// rows of at most kChunk elements: blocks of whole rows (~kChunk elements each) on the
+// pool, each row one segment call with its channel's qparams
+template <class F>
+void short_rows(int64_t rows, int64_t rowlen, F &&row) {
+  const int64_t per = std::max<int64_t>(1, kChunk / std::max<int64_t>(1, rowlen));
+  Pool::get().run(cdiv(rows, per), [&](int64_t b) {
+    const int64_t r1 = std::min(rows, (b + 1) * per);
+    for (int64_t r = b * per; r < r1; ++r) row(r);
+  });
+}
+
 }  // namespace host
 }  // namespace vsiq
 
@@ -471,6 +543,15 @@ int vsiq_host_pcm_fq_fwd_f32(const float *x, float *y, uint8_t *mask, int64_t ro
   if (rows < 0 || rowlen < 0 || channels <= 0 || rows % channels || (rows > 0 && (!x || !y || !scale)) ||
       qmin > qmax)
     return VSIQ_E_ARG;
+  if (rowlen <= kChunk) {   // short rows (an [N, C] activation: one element each): no per-row call
+    std::vector<HQP> hq((size_t)channels);
+    for (int64_t c = 0; c < channels; ++c) hq[(size_t)c] = make_hqp(scale[c], zp ? zp[c] : 0.0, zp_round, qmin, qmax);
+    short_rows(rows, rowlen, [&](int64_t r) {
+      const int64_t o = r * rowlen;
+      fq_seg(x + o, y + o, mask ? mask + o : nullptr, rowlen, hq[(size_t)(r % channels)]);
+    });
+    return 0;
+  }
   std::atomic<int> rc{0};
   Pool::get().run(rows, [&](int64_t r) {
     const int64_t c = r % channels;
@@ -486,6 +567,13 @@ int vsiq_host_pcm_ste_bwd_f32(const float *g, const uint8_t *mask, float *gx, in
                               int64_t channels, const double *scale) {
   if (rows < 0 || rowlen < 0 || channels <= 0 || rows % channels || (rows > 0 && (!g || !mask || !gx || !scale)))
     return VSIQ_E_ARG;
+  if (rowlen <= kChunk) {
+    short_rows(rows, rowlen, [&](int64_t r) {
+      const int64_t o = r * rowlen;
+      ste_seg(g + o, mask + o, gx + o, rowlen, (float)scale[r % channels]);
+    });
+    return 0;
+  }
   std::atomic<int> rc{0};
   Pool::get().run(rows, [&](int64_t r) {
     const int64_t o = r * rowlen;
@@ -501,22 +589,61 @@ int vsiq_host_pcm_lsq_bwd_f32(const float *g, const float *x, float *gx, int64_t
   if (rows <= 0 || rowlen <= 0 || channels <= 0 || rows % channels || !g || !x || !gx || !scale || !grad_scale_out ||
       qmin > qmax || (zp_learn && !zp) || zp_learn < 0 || zp_learn > 1)
     return VSIQ_E_ARG;
-  std::vector<double> part((size_t)rows * 2);
   std::atomic<int> rc{0};
+  const int64_t per = std::max<int64_t>(1, kChunk / rowlen), nb = cdiv(rows, per);
+  if (rowlen < kSegSimd && nb * channels <= ((int64_t)1 << 24)) {
+    // short rows (an [N, C] activation: one element each): blocks of ~kChunk elements of
+    // whole rows on the pool; each block sums its rows per channel in row order, the
+    // blocks fold in block order (fixed blocks: independent of the thread count)
+    std::vector<HQP> hq((size_t)channels);
+    std::vector<char> zok((size_t)channels, 0);
+    for (int64_t c = 0; c < channels; ++c) {
+      hq[(size_t)c] = make_hqp(scale[c], zp ? zp[c] : 0.0, zp_learn, qmin, qmax);
+      if (zp_learn) {   // ClampBackward of the rounded zero point (lsq_module.py:339-343)
+        const double zr = __builtin_rint(zp[c]);
+        zok[(size_t)c] = zr >= (double)qmin && zr <= (double)qmax;
+      }
+    }
+    std::vector<double> blk((size_t)(nb * channels * 2), 0.0);
+    Pool::get().run(nb, [&](int64_t b) {
+      double *acc = &blk[(size_t)(b * channels * 2)];
+      const int64_t r1 = std::min(rows, (b + 1) * per);
+      for (int64_t r = b * per; r < r1; ++r) {
+        const int64_t o = r * rowlen, c = r % channels;
+        double t[2];
+        lsq_seg(g + o, x + o, gx + o, rowlen, hq[(size_t)c], zp_learn, t);
+        acc[c * 2] += t[0];
+        if (zok[(size_t)c]) acc[c * 2 + 1] += t[1];
+      }
+    });
+    for (int64_t c = 0; c < channels; ++c) {
+      double ts = 0.0, zs = 0.0;
+      for (int64_t b = 0; b < nb; ++b) {
+        ts += blk[(size_t)((b * channels + c) * 2)];
+        zs += blk[(size_t)((b * channels + c) * 2 + 1)];
+      }
+      grad_scale_out[c] = ts * gscale;
+      if (grad_zp_out) grad_zp_out[c] = zs * gscale;
+    }
+    return 0;
+  }
+  std::vector<double> part((size_t)rows * 2);
   Pool::get().run(rows, [&](int64_t r) {
     const int64_t o = r * rowlen, c = r % channels;
     const int e = vsiq_host_lsq_bwd_f32(g + o, x + o, gx + o, rowlen, kActNone, scale[c], zp ? zp[c] : 0.0,
                                         zp_learn, qmin, qmax, 1.0, &part[(size_t)r * 2]);
     if (e) rc.store(e);
   });
-  for (int64_t c = 0; c < channels; ++c) {   // row order: independent of the thread count
-    double t = 0.0, z = 0.0;
-    for (int64_t r = c; r < rows; r += channels) {
-      t += part[(size_t)r * 2];
-      z += part[(size_t)r * 2 + 1];
-    }
-    grad_scale_out[c] = t * gscale;
-    if (grad_zp_out) grad_zp_out[c] = z * gscale;
+  // row order per channel (independent of the thread count), one sequential pass
+  std::vector<double> acc((size_t)channels * 2, 0.0);
+  for (int64_t r = 0; r < rows; ++r) {
+    const size_t c = (size_t)(r % channels);
+    acc[c * 2] += part[(size_t)r * 2];
+    acc[c * 2 + 1] += part[(size_t)r * 2 + 1];
+  }
+  for (int64_t c = 0; c < channels; ++c) {
+    grad_scale_out[c] = acc[(size_t)c * 2] * gscale;
+    if (grad_zp_out) grad_zp_out[c] = acc[(size_t)c * 2 + 1] * gscale;
   }
   return rc.load();
 }

@@ -9,10 +9,14 @@
 //          one stream of B / slots level-0 blocks, each a sequential fp32 sum of B rows
 //          (loads issued 16 at a time, adds in row order); the B level-0 sums of a stream
 //          meet in LDS and one lane sums them in block order -> ws.
-//   chunks (one 64-lane workgroup per chunk) per stream: the level-2 nodes and level 3
-//          from the level-1 nodes, the partial levels of the chunk's last rows straight
-//          from x, ((tail + l1) + l2) + l3; lane 0 then folds the tail vectors, the 4
-//          k-streams, the scalar tail and the V lanes -> the chunk's sum.
+//   l2     (grid: level-2 nodes x chunks, 64 lanes) every complete level-2 node: a
+//          stream's B level-1 nodes in order.
+//   chunks (one 256-lane workgroup per chunk) per stream, in parallel: the trailing
+//          complete level-0 blocks, then the four open levels (level 3 = the level-2
+//          nodes), ((tail + l1) + l2) + l3; lane 0 then folds the tail vectors, the 4
+//          k-streams, the scalar tail and the V lanes -> the chunk's sum.  Every
+//          sequential chain loads 16 values at a time (round 6's first form chained up
+//          to 1600 dependent loads per lane at one thread: 290 us at 52M elements).
 //   final  (one lane) the `threads`-slot second pass, then sum / float(n).
 // Both sums (|act(x)| and act(x)) ride the same pass.  HBM: 4 B / element read; the
 // level-1 nodes (8 B per 256 elements at V = 8) are written once and read once.
@@ -23,15 +27,16 @@ namespace {
 
 struct MeanArgs {
   const float *x;
-  int64_t n, cs, nchunks, tiles_max;
-  MAcc *l1;     // [nchunks][tiles_max][4V]
+  int64_t n, cs, nchunks, tiles_max, l2_max;
+  MAcc *l1;     // [nchunks][tiles_max][4V]: level-1 nodes
+  MAcc *l2;     // [nchunks][l2_max][4V]: complete level-2 nodes
   MAcc *csum;   // [nchunks]
   SiluLay L;
 };
 
 // rows / level power / B / tiles of the chunk starting at o
 struct ChunkGeo {
-  int64_t o, len, nv, rows, B, B2, tiles;
+  int64_t o, len, nv, rows, B, B2, tiles, l2;   // l2: complete level-2 nodes (B tiles each)
   int lp;
 };
 
@@ -45,6 +50,7 @@ __host__ __device__ inline ChunkGeo chunk_geo(int64_t n, int64_t cs, int64_t c, 
   g.B = (int64_t)1 << g.lp;
   g.B2 = g.B << g.lp;
   g.tiles = g.len < V ? 0 : g.rows / g.B2;
+  g.l2 = g.tiles / g.B;
   return g;
 }
 
@@ -77,42 +83,92 @@ __global__ __launch_bounds__(256) void k_mean_tiles(MeanArgs a) {
   }
 }
 
-template <int V, int ACT>
-__global__ __launch_bounds__(64) void k_mean_chunks(MeanArgs a) {
+// level-2 nodes: workgroup (d, chunk), lane s: the sequential sum of level-1 nodes
+// d*B .. d*B + B - 1 of stream s (loads 16 at a time, adds in node order)
+template <int V>
+__global__ __launch_bounds__(64) void k_mean_l2(MeanArgs a) {
   constexpr int S = 4 * V;
-  __shared__ MAcc p[S];
-  const int64_t c = blockIdx.x;
+  const int64_t c = blockIdx.y, d = blockIdx.x;
   const ChunkGeo g = chunk_geo(a.n, a.cs, c, V);
   const int s = threadIdx.x;
+  if (d >= g.l2 || s >= S) return;
+  const MAcc *l1 = a.l1 + (c * a.tiles_max + d * g.B) * S + s;
+  MAcc acc{0.0f, 0.0f};
+  for (int64_t k = 0; k < g.B; k += 16) {
+    MAcc v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = l1[(k + j) * S];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc_add(acc, v[j]);
+  }
+  a.l2[(c * a.l2_max + d) * S + s] = acc;
+}
+
+// sequential sum (from +0) of m values v(i), loaded 16 at a time
+template <class LD>
+__device__ __forceinline__ MAcc seq_batched(const LD &v, int64_t m) {
+  MAcc acc{0.0f, 0.0f};
+  int64_t i = 0;
+  for (; i + 16 <= m; i += 16) {
+    MAcc t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t[j] = v(i + j);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc_add(acc, t[j]);
+  }
+  for (; i < m; ++i) acc_add(acc, v(i));
+  return acc;
+}
+
+// one workgroup per chunk: the open levels of every stream in parallel -- slots compute
+// the trailing complete level-0 blocks (LDS), then slot 0 / 1 / 2 / 3 of each stream the
+// open level 1 (those blocks), open level 2 (level-1 nodes after the last level-2 node),
+// level 3 (the level-2 nodes) and the open level 0 (tail rows); ((l0 + l1) + l2) + l3;
+// lane 0 then folds the tail vectors, the 4 k-streams, the scalar tail and the V lanes
+template <int V, int ACT>
+__global__ __launch_bounds__(256) void k_mean_chunks(MeanArgs a) {
+  constexpr int S = 4 * V, SLOTS = 256 / S;
+  __shared__ MAcc l0r[64 * S];   // trailing complete level-0 blocks (< B <= 64) x streams
+  __shared__ MAcc part[4][S];
+  const int64_t c = blockIdx.x;
+  const ChunkGeo g = chunk_geo(a.n, a.cs, c, V);
+  const int s = threadIdx.x % S, q = threadIdx.x / S;
   auto ld = [&](int64_t i) { return mean_elem<ACT>(a.x[g.o + i], g.o + i, a.L); };
   if (g.len < V) {   // a chunk shorter than a vector: row_sum on scalars
-    if (s == 0) a.csum[c] = mean_chunk_seq(ld, g.len, V);
+    if (threadIdx.x == 0) a.csum[c] = mean_chunk_seq(ld, g.len, V);
     return;
   }
-  if (s < S) {
-    const MAcc *l1 = a.l1 + c * a.tiles_max * S + s;
-    MAcc acc0{0.0f, 0.0f}, acc1{0.0f, 0.0f}, acc2{0.0f, 0.0f}, acc3{0.0f, 0.0f};
-    const int64_t n1 = g.tiles, n2 = n1 / g.B;
-    for (int64_t d = 0; d < n2; ++d) {   // complete level-2 nodes -> level 3
-      MAcc l2{0.0f, 0.0f};
-      for (int64_t k = 0; k < g.B; ++k) acc_add(l2, l1[(d * g.B + k) * S]);
-      acc_add(acc3, l2);
+  const int64_t r0 = g.tiles * g.B2;              // first row after the complete tiles
+  const int64_t rb = (g.rows - r0) / g.B;          // complete level-0 blocks after them
+  const int64_t rt = r0 + rb * g.B;                // first tail row
+  for (int64_t b = q; b < rb; b += SLOTS)
+    l0r[b * S + s] = seq_batched([&](int64_t j) { return ld((r0 + b * g.B + j) * S + s); }, g.B);
+  __syncthreads();
+  if (q < 4) {
+    MAcc v{0.0f, 0.0f};
+    if (q == 0) {
+      v = seq_batched([&](int64_t b) { return l0r[b * S + s]; }, rb);
+    } else if (q == 1) {
+      const MAcc *l1 = a.l1 + (c * a.tiles_max + g.l2 * g.B) * S + s;
+      v = seq_batched([&](int64_t t) { return l1[t * S]; }, g.tiles - g.l2 * g.B);
+    } else if (q == 2) {
+      const MAcc *l2 = a.l2 + c * a.l2_max * S + s;
+      v = seq_batched([&](int64_t d) { return l2[d * S]; }, g.l2);
+    } else {
+      v = seq_batched([&](int64_t r) { return ld((rt + r) * S + s); }, g.rows - rt);
     }
-    for (int64_t t = n2 * g.B; t < n1; ++t) acc_add(acc2, l1[t * S]);   // open level 2
-    int64_t r = n1 * g.B2;
-    for (; r + g.B <= g.rows; r += g.B) {   // complete level-0 blocks after the tiles -> open level 1
-      MAcc l0{0.0f, 0.0f};
-      for (int64_t j = 0; j < g.B; ++j) acc_add(l0, ld((r + j) * S + s));
-      acc_add(acc1, l0);
-    }
-    for (; r < g.rows; ++r) acc_add(acc0, ld(r * S + s));   // open level 0
-    acc_add(acc0, acc1);
-    acc_add(acc0, acc2);
-    acc_add(acc0, acc3);
-    p[s] = acc0;
+    part[q][s] = v;
   }
   __syncthreads();
-  if (s == 0) {
+  if (threadIdx.x == 0) {
+    MAcc p[S];
+    for (int k = 0; k < S; ++k) {   // ((tail + l1) + l2) + l3 per stream
+      MAcc t = part[3][k];
+      acc_add(t, part[0][k]);
+      acc_add(t, part[1][k]);
+      acc_add(t, part[2][k]);
+      p[k] = t;
+    }
     for (int64_t vi = g.rows * 4; vi < g.nv; ++vi)   // tail vectors -> stream k = 0
       for (int l = 0; l < V; ++l) acc_add(p[l], ld(vi * V + l));
     for (int k = 1; k < 4; ++k)
@@ -152,6 +208,16 @@ int64_t tiles_max_of(const MeanLay &m, int64_t n, int V) {
   return t;
 }
 
+int64_t l2_max_of(const MeanLay &m, int64_t n, int V) {
+  int64_t t = 0;
+  if (m.nchunks > 0) {
+    t = chunk_geo(n, m.cs, 0, V).l2;
+    const int64_t tl = chunk_geo(n, m.cs, m.nchunks - 1, V).l2;
+    if (tl > t) t = tl;
+  }
+  return t;
+}
+
 bool mean_args_ok(int64_t n, int vec, int threads) {
   if (n < 0 || (vec != 8 && vec != 16) || threads < 1 || threads > 4096) return false;
   const MeanLay m = mean_lay(n, threads);
@@ -168,7 +234,9 @@ void launch_mean(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
     hipLaunchKernelGGL((k_mean_tiles<V, ACT>), dim3((unsigned)a.tiles_max, (unsigned)m.nchunks), dim3(256), lds, st,
                        a);
   }
-  hipLaunchKernelGGL((k_mean_chunks<V, ACT>), dim3((unsigned)m.nchunks), dim3(64), 0, st, a);
+  if (a.l2_max > 0)
+    hipLaunchKernelGGL((k_mean_l2<V>), dim3((unsigned)a.l2_max, (unsigned)m.nchunks), dim3(64), 0, st, a);
+  hipLaunchKernelGGL((k_mean_chunks<V, ACT>), dim3((unsigned)m.nchunks), dim3(256), 0, st, a);
 }
 
 template <int ACT>
@@ -185,8 +253,8 @@ void launch_mean16(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
 
 int64_t mean_ws_bytes(int64_t n, int vec, int threads) {
   const MeanLay m = mean_lay(n, threads);
-  const int64_t tm = tiles_max_of(m, n, vec);
-  return (int64_t)sizeof(MAcc) * (m.nchunks * tm * 4 * vec + (m.nchunks > 0 ? m.nchunks : 1));
+  const int64_t tm = tiles_max_of(m, n, vec), l2 = l2_max_of(m, n, vec);
+  return (int64_t)sizeof(MAcc) * (m.nchunks * (tm + l2) * 4 * vec + (m.nchunks > 0 ? m.nchunks : 1));
 }
 
 }  // namespace vsiq
@@ -213,8 +281,10 @@ int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads
   a.cs = m.cs;
   a.nchunks = m.nchunks;
   a.tiles_max = tiles_max_of(m, n, vec);
+  a.l2_max = l2_max_of(m, n, vec);
   a.l1 = static_cast<MAcc *>(ws);
-  a.csum = a.l1 + m.nchunks * a.tiles_max * 4 * vec;
+  a.l2 = a.l1 + m.nchunks * a.tiles_max * 4 * vec;
+  a.csum = a.l2 + m.nchunks * a.l2_max * 4 * vec;
   a.L = act_lay(act, n);
   if (m.nchunks > 0) {
     if (vec == 8) VSIQ_ACT(act, launch_mean8, a, m, st);
