@@ -115,8 +115,8 @@ def test_launch_mode_agreed_across_ranks():
 
 
 def test_compact_summary_is_short_and_complete():
-    """The stderr summary after the JSON line carries every leg's value, in-step kernel
-    fractions, API timings and chosen gates in a few hundred characters."""
+    """The stderr summary after the JSON line carries every leg's value, kernel fractions
+    (off-step kernels marked *), API timings and chosen gates in a few hundred characters."""
     k = {"pc_observe_fq_fwd": {"frac": 0.74, "avg_us": 12.9}, "ste_bwd": {"frac": 0.76, "avg_us": 12.4},
          "alt": {"frac": 0.8, "avg_us": 1.0, "in_step": False}}
     leg = {"value": 1000.0, "ms_per_step": 0.2, "launch": "direct", "kernels": k}
@@ -125,7 +125,7 @@ def test_compact_summary_is_short_and_complete():
                store_gate={"sites": [{"site": "k3", "gate_ticks": 515}]}, cpu_baseline={"value": 100.0})
     s = bench.compact_summary(out)
     assert s.startswith("[bench summary]") and len(s) < 1500
-    assert "pc_observe_fq_fwd=0.740" in s and "alt=" not in s and "k3:515" in s and "api_us_per_step" in s
+    assert "pc_observe_fq_fwd=0.740" in s and "alt=0.800*" in s and "k3:515" in s and "api_us_per_step" in s
     assert "c5 " in s and "act " in s and "cpu=100.0" in s
     out["store_gate"]["sites"][0]["candidates"] = [[0, 13.41], [489, 12.93], [515, 12.71], [541, 12.80]]
     assert "k3:515(12.71/13.41us)" in bench.compact_summary(out)

@@ -13,7 +13,7 @@ def main():
     acc = defaultdict(list)
     for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
             if filt and not any(s in name for s in filt):
                 continue
             grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)

@@ -385,28 +385,28 @@ __global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict_
 // launch), and one-round grids store behind the store gate.  Same per-element code
 // (lsq_group_out) as the two-stage form; the f64 sums differ only in order.
 // At least 4 waves per SIMD (<= 128 VGPRs): 4 workgroups per CU, so the 1024 rows of a
-// C2-shaped weight are ONE round on 256 CUs (the learnable zero point's variant at 9
+// C2-shaped weight are ONE round on 256 CUs (round 5's learnable-zero-point variant at 9
 // groups per lane took 134 VGPRs = 3 workgroups per CU = a second, quarter-occupied
-// round: round 5's 24.2 us for 113 MB).  STAGE: where grad_x waits for the store gate --
-// 0 registers, 1 LDS (NV x 256 x 16 B, frees the registers the held outputs take),
-// 2 nowhere (stored as computed, no gate).
-template <bool VEC, bool NT, bool ZPL, int NV, int STAGE>
+// round: 24.2 us for 113 MB).  SPLIT (9 groups per lane): grad_x waits for the store gate
+// in LDS (NV x 256 x 16 B) instead of registers, and the second half of the x / g loads
+// is issued only once the first half is computed (a scheduling barrier keeps the compiler
+// from hoisting them) -- 95 VGPRs, no spills, where holding everything took 128 + 8-17
+// spilled (round 6, C2 bench leg pc_learn_bwd_k6: 0.67 against 0.56-0.66 for the other
+// forms on the same boxes, profiles/r06/r06f_k6_stages.txt).
+template <bool VEC, bool NT, bool ZPL, int NV, bool SPLIT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_pcr_lsq_bwd(
     const float *__restrict__ g, const float *__restrict__ x, float *__restrict__ gx, int64_t rowlen,
     const double *__restrict__ scale, const double *__restrict__ zp, float lo, float hi, double gscale,
     double *__restrict__ gs_out, double *__restrict__ gz_out, uint32_t gate) {
-  extern __shared__ f4 s_o[];   // STAGE 1: [NV][kBlock]
+  extern __shared__ f4 s_o[];   // SPLIT: [NV][kBlock]
   const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x;
   const QP p = load_qp(QPSrc{nullptr, scale + row, zp ? zp + row : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   const int64_t ng = cdiv(rowlen, 4);
   const float *xr = x + row * rowlen, *gr = g + row * rowlen;
   float *gxr = gx + row * rowlen;
-  f4 xv[NV], gv[NV], o[STAGE == 0 ? NV : 1];
-  // STAGE 3 (LDS staging, loads in two halves): the second half's loads are issued only
-  // once the first half is computed (a scheduling barrier keeps the compiler from hoisting
-  // them), so at most ~NV/2 groups of x and g are live -- fewer VGPRs than all NV at once
-  constexpr int H1 = STAGE == 3 ? (NV + 1) / 2 : NV;
+  f4 xv[NV], gv[NV], o[SPLIT ? 1 : NV];
+  constexpr int H1 = SPLIT ? (NV + 1) / 2 : NV;
   LsqAcc acc{0.0, 0.0};
 #pragma unroll
   for (int k = 0; k < H1; ++k) {
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    if (STAGE == 3 && k == H1) {
+    if (SPLIT && k == H1) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = H1; j < NV; ++j) {
@@ -423,11 +423,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         gv[j] = load_group_c<VEC, NT>(gr, threadIdx.x + j * kBlock, ng, rowlen);
       }
     }
-    const int64_t i = threadIdx.x + k * kBlock;
-    const f4 r = lsq_group_out<ZPL, kActNone>(i, ng, rowlen, xv[k], gv[k], p, acc);
-    if constexpr (STAGE == 0) o[k] = r;
-    else if constexpr (STAGE == 1 || STAGE == 3) s_o[k * kBlock + threadIdx.x] = r;
-    else if (i < ng) store_group<VEC, NT>(gxr, i, rowlen, r);
+    const f4 r = lsq_group_out<ZPL, kActNone>(threadIdx.x + k * kBlock, ng, rowlen, xv[k], gv[k], p, acc);
+    if constexpr (SPLIT) s_o[k * kBlock + threadIdx.x] = r;
+    else o[k] = r;
   }
   lsq_block_reduce(acc);
   if (threadIdx.x == 0) {
@@ -441,57 +439,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       gz_out[row] = gz;
     }
   }
-  if constexpr (STAGE != 2) {
-    gate_pass(gate, gc);
+  gate_pass(gate, gc);
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int64_t i = threadIdx.x + k * kBlock;
-      if (i < ng) store_group<VEC, NT>(gxr, i, rowlen, STAGE == 0 ? o[k] : s_o[k * kBlock + threadIdx.x]);
-    }
+  for (int k = 0; k < NV; ++k) {
+    const int64_t i = threadIdx.x + k * kBlock;
+    if (i < ng) store_group<VEC, NT>(gxr, i, rowlen, SPLIT ? s_o[k * kBlock + threadIdx.x] : o[k]);
   }
-}
-
-inline int pcr_stage_env() {
-  static const int v = [] {
-    const char *e = std::getenv("VSIQ_EXP_PCR_STAGE");
-    return e ? std::atoi(e) : -1;
-  }();
-  return v;
-}
-
-template <bool VEC, bool NT, bool ZPL, int NV, int STAGE>
-void launch_pcr_st(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
-                   const double *scale, const double *zp, float lo, float hi, double gscale,
-                   double *gs, double *gz, hipStream_t st) {
-  GateSel sel;
-  const void *kern = reinterpret_cast<const void *>(k_pcr_lsq_bwd<VEC, NT, ZPL, NV, STAGE>);
-  const size_t lds = (STAGE == 1 || STAGE == 3) ? (size_t)NV * kBlock * sizeof(f4) : 0;
-  if (STAGE != 2 && g_tune.store_gate != 0) {
-    static const int occ = occupancy_blocks(kern, kBlock);
-    sel = store_gate_select("k6_pcr_lsq_bwd", kern, rows, occ, 8 * rows * rowlen, st);
-  }
-  hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV, STAGE>), dim3((unsigned)rows), dim3(kBlock), lds, st, g, x,
-                     gx, rowlen, scale, zp, lo, hi, gscale, gs, gz, sel.gate);
-  store_gate_launched(sel, st);
 }
 
 template <bool VEC, bool NT, bool ZPL, int NV>
 void launch_pcr_nv(const float *g, const float *x, float *gx, int64_t rows, int64_t rowlen,
                    const double *scale, const double *zp, float lo, float hi, double gscale,
                    double *gs, double *gz, hipStream_t st) {
-  int stage = 0;
-  if constexpr (NV == 9) {
-    const int e = pcr_stage_env();
-    stage = e >= 0 ? e : 1;
+  constexpr bool SPLIT = NV == 9;
+  GateSel sel;
+  const void *kern = reinterpret_cast<const void *>(k_pcr_lsq_bwd<VEC, NT, ZPL, NV, SPLIT>);
+  if (g_tune.store_gate != 0) {
+    static const int occ = occupancy_blocks(kern, kBlock);
+    sel = store_gate_select("k6_pcr_lsq_bwd", kern, rows, occ, 8 * rows * rowlen, st);
   }
-  if (stage == 3)
-    launch_pcr_st<VEC, NT, ZPL, NV, 3>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st);
-  else if (stage == 1)
-    launch_pcr_st<VEC, NT, ZPL, NV, 1>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st);
-  else if (stage == 2)
-    launch_pcr_st<VEC, NT, ZPL, NV, 2>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st);
-  else
-    launch_pcr_st<VEC, NT, ZPL, NV, 0>(g, x, gx, rows, rowlen, scale, zp, lo, hi, gscale, gs, gz, st);
+  hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV, SPLIT>), dim3((unsigned)rows), dim3(kBlock),
+                     SPLIT ? (size_t)NV * kBlock * sizeof(f4) : 0, st, g, x, gx, rowlen, scale, zp, lo, hi, gscale,
+                     gs, gz, sel.gate);
+  store_gate_launched(sel, st);
 }
 
 // rows == channels and whole rows fit 9 groups per lane with >= 1 per lane
