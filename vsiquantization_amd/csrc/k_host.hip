@@ -658,20 +658,22 @@ int vsiq_host_torch_mean_f32(const float *x, int64_t n, int act, int vec, int th
   const SiluLay L = act_lay(act, n);
   std::vector<MAcc> cs((size_t)(m.nchunks > 0 ? m.nchunks : 1));
   auto chunk = [&](int64_t c) {
+    MAcc buf[kMeanScratch];
     const int64_t o = c * m.cs, len = std::min(m.cs, n - o);
     switch (act_kind(act)) {
       case kActRelu:
-        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActRelu>(x[o + i], o + i, L); }, len, vec);
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActRelu>(x[o + i], o + i, L); }, len, vec, buf);
         break;
       case kActSilu:
-        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActSilu>(x[o + i], o + i, L); }, len, vec);
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActSilu>(x[o + i], o + i, L); }, len, vec, buf);
         break;
       default:
-        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActNone>(x[o + i], o + i, L); }, len, vec);
+        cs[c] = mean_chunk_seq([&](int64_t i) { return mean_elem<kActNone>(x[o + i], o + i, L); }, len, vec, buf);
     }
   };
   Pool::get().run(m.nchunks, chunk);
-  const MAcc t = mean_final_seq([&](int64_t i) { return cs[(size_t)i]; }, m, vec, threads);
+  MAcc buf[kMeanScratch];
+  const MAcc t = mean_final_seq([&](int64_t i) { return cs[(size_t)i]; }, m, vec, threads, buf);
   out4[0] = t.a;
   out4[1] = t.s;
   out4[2] = t.a / (float)n;

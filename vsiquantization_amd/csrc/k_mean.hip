@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void k_mean_chunks(MeanArgs a) {
   const int s = threadIdx.x % S, q = threadIdx.x / S;
   auto ld = [&](int64_t i) { return mean_elem<ACT>(a.x[g.o + i], g.o + i, a.L); };
   if (g.len < V) {   // a chunk shorter than a vector: row_sum on scalars
-    if (threadIdx.x == 0) a.csum[c] = mean_chunk_seq(ld, g.len, V);
+    if (threadIdx.x == 0) a.csum[c] = mean_chunk_seq(ld, g.len, V, &l0r[0]);
     return;
   }
   const int64_t r0 = g.tiles * g.B2;              // first row after the complete tiles
@@ -160,15 +160,16 @@ __global__ __launch_bounds__(256) void k_mean_chunks(MeanArgs a) {
     part[q][s] = v;
   }
   __syncthreads();
+  if (threadIdx.x < S) {   // ((tail + l1) + l2) + l3 per stream, in LDS for lane 0
+    MAcc t = part[3][threadIdx.x];
+    acc_add(t, part[0][threadIdx.x]);
+    acc_add(t, part[1][threadIdx.x]);
+    acc_add(t, part[2][threadIdx.x]);
+    l0r[threadIdx.x] = t;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    MAcc p[S];
-    for (int k = 0; k < S; ++k) {   // ((tail + l1) + l2) + l3 per stream
-      MAcc t = part[3][k];
-      acc_add(t, part[0][k]);
-      acc_add(t, part[1][k]);
-      acc_add(t, part[2][k]);
-      p[k] = t;
-    }
+    MAcc *p = l0r;
     for (int64_t vi = g.rows * 4; vi < g.nv; ++vi)   // tail vectors -> stream k = 0
       for (int l = 0; l < V; ++l) acc_add(p[l], ld(vi * V + l));
     for (int k = 1; k < 4; ++k)
@@ -182,8 +183,9 @@ __global__ __launch_bounds__(256) void k_mean_chunks(MeanArgs a) {
 
 __global__ __launch_bounds__(64) void k_mean_final(const MAcc *csum, MeanLay m, int V, int threads, int64_t n,
                                                    float *out4, double *stats) {
+  __shared__ MAcc buf[kMeanScratch];   // the one lane's accumulators: LDS, not scratch
   if (threadIdx.x != 0) return;
-  const MAcc t = mean_final_seq([&](int64_t i) { return csum[i]; }, m, V, threads);
+  const MAcc t = mean_final_seq([&](int64_t i) { return csum[i]; }, m, V, threads, buf);
   const float fn = (float)n;
   const float ma = t.a / fn, ms = t.s / fn;
   if (out4) {

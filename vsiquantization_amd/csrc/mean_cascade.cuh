@@ -73,13 +73,18 @@ __host__ __device__ inline MeanLay mean_lay(int64_t n, int threads) {
   return m;
 }
 
+// Every sequential helper works in `buf`: kMeanScratch accumulators the caller provides
+// (a local array on the host, LDS in the GPU's one-lane stages, where a dynamically
+// indexed local array would live in scratch memory).
+constexpr int kMeanScratch = 16 * kMeanMaxLanes + 4 * kMeanMaxLanes + kMeanMaxLanes;
+
 // multi_row_sum<acc, 4> over `size` rows of 4 * lanes items; item c of row i = ld(i * 4 * lanes + c)
 template <class LD>
-__host__ __device__ void mean_multi_row_seq(const LD &ld, int64_t size, int lanes, MAcc *out) {
+__host__ __device__ void mean_multi_row_seq(const LD &ld, int64_t size, int lanes, MAcc *out, MAcc *buf) {
   const int w = 4 * lanes;
   const int lp = mean_level_power(size);
   const int64_t step = (int64_t)1 << lp, mask = step - 1;
-  MAcc acc[4][4 * kMeanMaxLanes];
+  MAcc *acc[4] = {buf, buf + 4 * kMeanMaxLanes, buf + 8 * kMeanMaxLanes, buf + 12 * kMeanMaxLanes};
   for (int j = 0; j < 4; ++j)
     for (int c = 0; c < w; ++c) acc[j][c] = MAcc{0.0f, 0.0f};
   int64_t i = 0;
@@ -103,10 +108,10 @@ __host__ __device__ void mean_multi_row_seq(const LD &ld, int64_t size, int lane
 
 // row_sum<acc, 4>: `size` items of `lanes` values; the lanes' sums in out[0..lanes)
 template <class LD>
-__host__ __device__ void mean_row_seq(const LD &ld, int64_t size, int lanes, MAcc *out) {
-  MAcc p[4 * kMeanMaxLanes];
+__host__ __device__ void mean_row_seq(const LD &ld, int64_t size, int lanes, MAcc *out, MAcc *buf) {
+  MAcc *p = buf + 16 * kMeanMaxLanes;
   const int64_t ilp = size / 4;
-  mean_multi_row_seq(ld, ilp, lanes, p);
+  mean_multi_row_seq(ld, ilp, lanes, p, buf);
   for (int64_t i = ilp * 4; i < size; ++i)
     for (int l = 0; l < lanes; ++l) acc_add(p[l], ld(i * lanes + l));
   for (int k = 1; k < 4; ++k)
@@ -116,14 +121,14 @@ __host__ __device__ void mean_row_seq(const LD &ld, int64_t size, int lanes, MAc
 
 // the reduce loop over one chunk of len items (vectorized_inner_sum / its scalar form)
 template <class LD>
-__host__ __device__ MAcc mean_chunk_seq(const LD &ld, int64_t len, int V) {
-  MAcc lanes[kMeanMaxLanes];
+__host__ __device__ MAcc mean_chunk_seq(const LD &ld, int64_t len, int V, MAcc *buf) {
+  MAcc *lanes = buf + 20 * kMeanMaxLanes;
   if (len < V) {
-    mean_row_seq(ld, len, 1, lanes);
+    mean_row_seq(ld, len, 1, lanes, buf);
     return lanes[0];
   }
   const int64_t nv = len / V;
-  mean_row_seq(ld, nv, V, lanes);
+  mean_row_seq(ld, nv, V, lanes, buf);
   MAcc acc{0.0f, 0.0f};
   for (int64_t k = nv * V; k < len; ++k) acc_add(acc, ld(k));
   for (int l = 0; l < V; ++l) acc_add(acc, lanes[l]);
@@ -132,7 +137,7 @@ __host__ __device__ MAcc mean_chunk_seq(const LD &ld, int64_t len, int V) {
 
 // the second pass: `threads` slots, chunk sums in the first nchunks (0 + sum), zeros after
 template <class CS>
-__host__ __device__ MAcc mean_final_seq(const CS &csum, const MeanLay &m, int V, int threads) {
+__host__ __device__ MAcc mean_final_seq(const CS &csum, const MeanLay &m, int V, int threads, MAcc *buf) {
   MAcc out{0.0f, 0.0f};
   if (!m.twopass) {
     if (m.nchunks > 0) acc_add(out, csum(0));
@@ -143,7 +148,7 @@ __host__ __device__ MAcc mean_final_seq(const CS &csum, const MeanLay &m, int V,
     if (t < m.nchunks) acc_add(v, csum(t));
     return v;
   };
-  acc_add(out, mean_chunk_seq(slot, threads, V));
+  acc_add(out, mean_chunk_seq(slot, threads, V, buf));
   return out;
 }
 
