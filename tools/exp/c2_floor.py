@@ -6,6 +6,10 @@ sweep (ticks of the 100 MHz wall clock; 0 = no gate), R launches back to back, e
   * K3 with the gate forced (VSIQ_TUNE_STORE_GATE),
   * the STE backward (vsiq_ste_bwd_f32: read g + the mask bits, write grad_x) with the
     same gate,
+  * the learnable per-channel forward (vsiq_pcm_fq_fwd_f32: given f64 scale / zp per row,
+    zp rounded, no observer; bench.py's pc_learn_fwd leg) with the same gate, without
+    and with the 1-bit mask, and its backward K6 (vsiq_pcm_lsq_bwd_f32, zp learned: read g, x,
+    write grad_x, 12 B/elem; bench.py's pc_learn_bwd_k6 leg),
   * a plain gated copy of the same grid shape (c2_floor.hip: 9 float4 loads per lane, the
     gate, 9 stores; no reduction, no mask).
 
@@ -61,6 +65,27 @@ def main():
         return lib.vsiq_ste_bwd_f32(P(gs[j].data_ptr()), P(mask.data_ptr()), P(gxs[j].data_ptr()),
                                     H.c_i64(rows * rowlen), P(qp[0].data_ptr()), H.c_i64(rowlen), 0.0, st)
 
+    sc = torch.rand(rows, dtype=torch.float64, device=dev, generator=g) * 0.002 + 0.0005
+    zp = torch.rand(rows, dtype=torch.float64, device=dev, generator=g) * 8 - 4
+
+    def pcm(with_mask):
+        mp = P(mask.data_ptr()) if with_mask else None
+        return lambda i: lib.vsiq_pcm_fq_fwd_f32(P(xs[i % sl].data_ptr()), P(ys[i % sl].data_ptr()), None, mp,
+                                                 H.c_i64(rows), H.c_i64(rowlen), H.c_i64(rows), P(sc.data_ptr()),
+                                                 P(zp.data_ptr()), 1, -128, 127, st)
+
+    nws = int(lib.vsiq_pcm_workspace_doubles(H.c_i64(rows), H.c_i64(rowlen)))
+    ws = torch.zeros(max(nws, 1), dtype=torch.float64, device=dev)
+    gsc = torch.empty(rows, dtype=torch.float64, device=dev)
+    gzp = torch.empty(rows, dtype=torch.float64, device=dev)
+
+    def k6(i):
+        j = i % sl
+        return lib.vsiq_pcm_lsq_bwd_f32(P(gs[j].data_ptr()), P(xs[j].data_ptr()), P(gxs[j].data_ptr()),
+                                        H.c_i64(rows), H.c_i64(rowlen), H.c_i64(rows), P(sc.data_ptr()),
+                                        P(zp.data_ptr()), 1, -128, 127, 1e-4, P(gsc.data_ptr()), P(gzp.data_ptr()),
+                                        P(ws.data_ptr()), H.c_i64(nws), st)
+
     def plain(gate):
         return lambda i: ex.exp_copy_gated(P(xs[i % sl].data_ptr()), P(ys[i % sl].data_ptr()), rows, rowlen, gate, st)
 
@@ -83,23 +108,27 @@ def main():
     gates = [0] + list(range(440, 701, 13))
     res = []
     print(f"C2 shape {rows}x{rowlen}, {sl} buffers, {reps} launches per timing (min of 3)")
-    print(" gate   K3 us  STE us  plain us")
+    print(" gate   K3 us  STE us  plain us  pcm us  pcm+mask us  K6 us")
     try:
         for gt in gates:
             H.set_tuning(H.TUNE_STORE_GATE, gt)
             a = t(k3)
             c = t(ste)
             b = t(plain(gt))
-            res.append((gt, a, b, c))
-            print(f"{gt:5d} {a:7.2f} {c:7.2f} {b:9.2f}", flush=True)
+            d = t(pcm(False))
+            e = t(pcm(True))
+            f = t(k6)
+            res.append((gt, a, b, c, d, e, f))
+            print(f"{gt:5d} {a:7.2f} {c:7.2f} {b:9.2f} {d:7.2f} {e:11.2f} {f:6.2f}", flush=True)
     finally:
         H.set_tuning(H.TUNE_STORE_GATE, -1)
     pa = min(res, key=lambda r: r[2])
     print(f"best plain copy {pa[2]:.2f} us at gate {pa[0]} = {alg / pa[2] / 1e3:.0f} GB/s ({alg / pa[2] / 8e6:.3f} of 8 TB/s)")
-    for name, col in (("K3", 1), ("STE", 3)):
+    for name, col in (("K3", 1), ("STE", 3), ("pcm fwd", 4), ("pcm fwd + mask", 5), ("K6", 6)):
         ka = min(res, key=lambda r: r[col])
-        print(f"best {name} {ka[col]:.2f} us at gate {ka[0]} = {alg / ka[col] / 1e3:.0f} GB/s "
-              f"({alg / ka[col] / 8e6:.3f} of 8 TB/s); {pa[2] / ka[col]:.3f} of the plain copy's rate")
+        nb = alg * 3 // 2 if col == 6 else alg
+        print(f"best {name} {ka[col]:.2f} us at gate {ka[0]} = {nb / ka[col] / 1e3:.0f} GB/s "
+              f"({nb / ka[col] / 8e6:.3f} of 8 TB/s); no gate {res[0][col]:.2f} us")
 
 
 if __name__ == "__main__":

@@ -389,11 +389,13 @@ __global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict_
 // groups per lane took 134 VGPRs = 3 workgroups per CU = a second, quarter-occupied
 // round: 24.2 us for 113 MB).  SPLIT (9 groups per lane): grad_x waits for the store gate
 // in LDS (NV x 256 x 16 B) instead of registers, and the second half of the x / g loads
-// is issued only once the first half is computed (a scheduling barrier keeps the compiler
-// from hoisting them) -- 95 VGPRs, no spills, where holding everything took 128 + 8-17
-// spilled (round 6, C2 bench leg pc_learn_bwd_k6: 0.67 against 0.56-0.66 for the other
-// forms on the same boxes, profiles/r06/r06f_k6_stages.txt).
-template <bool VEC, bool NT, bool ZPL, int NV, bool SPLIT>
+// is issued once ISSUE groups of the first half are computed (a scheduling barrier keeps
+// the compiler from hoisting them) -- 111 VGPRs at ISSUE 3 (95 at 5, 119 at 2), no spills,
+// where holding everything took 128 + 8-17 spilled (round 6, C2 bench leg
+// pc_learn_bwd_k6: 0.67 against 0.56-0.66 for the other forms on the same boxes,
+// profiles/r06/r06f_k6_stages.txt; issue point 5 / 3 / 2 twice each on one box: 0.683 /
+// 0.703 / 0.701, then 0.687 / 0.702 / 0.700, profiles/r06/r06i_k6_issue.txt).
+template <bool VEC, bool NT, bool ZPL, int NV, bool SPLIT, int ISSUE = 3>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_pcr_lsq_bwd(
     const float *__restrict__ g, const float *__restrict__ x, float *__restrict__ gx, int64_t rowlen,
     const double *__restrict__ scale, const double *__restrict__ zp, float lo, float hi, double gscale,
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    if (SPLIT && k == H1) {
+    if (SPLIT && k == ISSUE) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = H1; j < NV; ++j) {
@@ -458,9 +460,9 @@ void launch_pcr_nv(const float *g, const float *x, float *gx, int64_t rows, int6
     static const int occ = occupancy_blocks(kern, kBlock);
     sel = store_gate_select("k6_pcr_lsq_bwd", kern, rows, occ, 8 * rows * rowlen, st);
   }
-  hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV, SPLIT>), dim3((unsigned)rows), dim3(kBlock),
-                     SPLIT ? (size_t)NV * kBlock * sizeof(f4) : 0, st, g, x, gx, rowlen, scale, zp, lo, hi, gscale,
-                     gs, gz, sel.gate);
+  const size_t lds = SPLIT ? (size_t)NV * kBlock * sizeof(f4) : 0;
+  hipLaunchKernelGGL((k_pcr_lsq_bwd<VEC, NT, ZPL, NV, SPLIT>), dim3((unsigned)rows), dim3(kBlock), lds, st, g, x,
+                     gx, rowlen, scale, zp, lo, hi, gscale, gs, gz, sel.gate);
   store_gate_launched(sel, st);
 }
 
