@@ -206,6 +206,28 @@ def test_burst_sample_never_spans_another_library_launch():
     assert len(meds) >= 12 and max(meds) < 30.0, line
 
 
+def test_burst_sample_excludes_foreign_kernels():
+    """Kernels of another library (here torch's elementwise add over 52M floats, ~70 us)
+    queued between two launches of a burst are not counted: every launch of a burst has
+    its own event pair (round 6).  K3 at C2 through the C ABI (launches enqueue within the
+    burst gap) alternates with the torch op; every candidate's median stays a K3 time."""
+    x, want = _k3_inputs()
+    launch = _k3_direct(x)
+    big = torch.zeros(52_428_800, device=DEV)
+    _reset()
+    for i in range(800):
+        y = launch()
+        big.add_(1.0)
+        if i % 16 == 15:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    G.assert_bitwise_f32(y.cpu().numpy(), want, "y")
+    line = _site_line("k3_pc_observe_fq")
+    assert " done=1 " in line, H.gate_report()
+    meds = [float(t.split(":")[1]) for t in line.split() if ":" in t and t.split(":")[0].isdigit()]
+    assert len(meds) >= 12 and max(meds) < 40.0, line
+
+
 def test_gate_table_save_load_freeze(tmp_path):
     """A tuned table saved (vsiq_gate_export), reset, loaded and frozen: every site launched
     again takes its saved gate and is never timed (no candidate medians in the report, no

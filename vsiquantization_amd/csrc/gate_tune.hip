@@ -18,8 +18,10 @@
 // Bursts (round 5): where a site is launched back to back -- the next launch of the same
 // site is the next launch of this library (g_lib_launches: an untuned kernel in between,
 // e.g. a larger layer's, ends the burst), on the same stream, within kBurstGapUs of host
-// time -- a sample spans up to kBurst consecutive launches with the same gate (its
-// end event re-recorded after each), and counts their mean.  A lone launch's timing
+// time -- a sample spans up to kBurst consecutive launches with the same gate and counts
+// the mean of their durations.  Each launch of a burst has its own pair of events (round
+// 6): kernels of other libraries (torch, MIOpen) queued on the stream between two
+// launches of the burst are outside every pair, so they never enter a sample.  A lone launch's timing
 // includes how the GPU comes out of the previous, different kernel; launches that stream
 // back to back (a bench's group of one kernel, several layers of one shape in a row)
 // have a different, sharper optimum (tools/exp/c2_floor.py: K3 at C2 12.0 us at 518
@@ -100,12 +102,12 @@ struct Site {
 };
 
 struct Sample {
-  hipEvent_t a = nullptr, b = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;   // start / end per launch; ev[0..n) recorded
   Site *site = nullptr;
   int cand = 0;   // -1: a drift sample of the tuned gate
   int dev = 0;
   int gen = 0;    // the site's tuning round when issued: samples of an earlier round are dropped
-  int n = 0;      // launches the sample spans (end event recorded after each)
+  int n = 0;      // launches recorded (a select in flight has pushed ev[n] already)
   hipStream_t st = nullptr;
 };
 
@@ -228,6 +230,24 @@ void watch_sample(Site &s, float ms) {
   if (s.drifting >= 2) retune(s);
 }
 
+// caller holds g_mu: a start / end event pair for one timed launch (pooled per device)
+bool take_pair(int dev, std::pair<hipEvent_t, hipEvent_t> &ev) {
+  auto &pool = g_pool[dev];
+  if (!pool.empty()) {
+    ev = pool.back();
+    pool.pop_back();
+    return true;
+  }
+  ev = {nullptr, nullptr};
+  if (hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence) != hipSuccess) {
+    (void)hipGetLastError();
+    if (ev.first) (void)hipEventDestroy(ev.first);
+    return false;
+  }
+  return true;
+}
+
 // caller holds g_mu: an open burst becomes a sample to harvest
 void close_burst_locked(Site &s) {
   if (!s.open) return;
@@ -246,14 +266,20 @@ void harvest_locked() {
   size_t keep = 0;
   for (size_t i = 0; i < g_pending.size(); ++i) {
     Sample *p = g_pending[i];
-    const hipError_t q = hipEventQuery(p->b);
+    const hipError_t q = p->n > 0 ? hipEventQuery(p->ev[p->n - 1].second) : hipErrorInvalidValue;
     if (q == hipErrorNotReady) {
       g_pending[keep++] = p;
       continue;
     }
     float ms = 0.0f;
+    bool ok = q == hipSuccess;
+    for (int k = 0; ok && k < p->n; ++k) {   // one stream: the last end done -> every pair done
+      float d = 0.0f;
+      ok = hipEventElapsedTime(&d, p->ev[k].first, p->ev[k].second) == hipSuccess && d > 0.0f;
+      ms += d;
+    }
     const bool current = p->gen == p->site->gen;
-    if (q == hipSuccess && hipEventElapsedTime(&ms, p->a, p->b) == hipSuccess && ms > 0.0f && p->n > 0) {
+    if (ok) {
       ms /= (float)p->n;
       if (!current) {
         // a sample of the round before a re-tune: not counted in the new round's issued[]
@@ -263,7 +289,7 @@ void harvest_locked() {
         p->site->ms[p->cand].push_back(ms);
         finish_if_complete(*p->site);
       }
-      g_pool[p->dev].emplace_back(p->a, p->b);
+      for (auto &e : p->ev) g_pool[p->dev].push_back(e);
     } else {
       if (current && p->cand >= 0 && !p->site->done) p->site->issued[p->cand]--;   // lost sample: issue again
       (void)hipGetLastError();
@@ -322,15 +348,21 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
     hipStreamCaptureStatus ocs = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(st, &ocs) != hipSuccess || ocs != hipStreamCaptureStatusNone;
     if (capturing) (void)hipGetLastError();
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (adjacent && !capturing && o->st == st && o->n < kBurst && o->gen == s.gen &&
-        us_since(s.open_t) < kBurstGapUs) {   // the burst goes on, same gate
-      sel.gate = o->cand >= 0 ? s.ticks[o->cand] : s.best;
-      sel.timing = o;
-      // the caller owns the sample until store_gate_launched re-opens it: a select of
-      // this site from another thread meanwhile finds no open burst, so the sample can
-      // never be published to g_pending while the caller still records into it
-      s.open = nullptr;
-      return sel;
+        us_since(s.open_t) < kBurstGapUs && take_pair(dev, ev)) {   // the burst goes on, same gate
+      if (hipEventRecord(ev.first, st) == hipSuccess) {
+        o->ev.push_back(ev);
+        sel.gate = o->cand >= 0 ? s.ticks[o->cand] : s.best;
+        sel.timing = o;
+        // the caller owns the sample until store_gate_launched re-opens it: a select of
+        // this site from another thread meanwhile finds no open burst, so the sample can
+        // never be published to g_pending while the caller still records into it
+        s.open = nullptr;
+        return sel;
+      }
+      (void)hipGetLastError();
+      g_pool[dev].push_back(ev);
     }
     close_burst_locked(s);
   }
@@ -376,24 +408,15 @@ GateSel store_gate_select(const char *label, const void *kernel, int64_t grid, i
   } else if (!s.done) {
     return sel;   // the harvest above started a re-tune: plain launch this time
   }
-  auto &pool = g_pool[dev];
   std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-  if (!pool.empty()) {
-    ev = pool.back();
-    pool.pop_back();
-  } else if (hipEventCreateWithFlags(&ev.first, hipEventDisableSystemFence) != hipSuccess ||
-             hipEventCreateWithFlags(&ev.second, hipEventDisableSystemFence) != hipSuccess) {
-    (void)hipGetLastError();
-    return sel;
-  }
+  if (!take_pair(dev, ev)) return sel;
   if (hipEventRecord(ev.first, st) != hipSuccess) {
     (void)hipGetLastError();
-    pool.push_back(ev);
+    g_pool[dev].push_back(ev);
     return sel;
   }
   Sample *p = new Sample;
-  p->a = ev.first;
-  p->b = ev.second;
+  p->ev.push_back(ev);
   p->site = &s;
   p->cand = c;
   p->dev = dev;
@@ -413,15 +436,16 @@ void store_gate_launched(GateSel &sel, hipStream_t st) {
   sel.timing = nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
   Site &s = *p->site;
-  if (hipEventRecord(p->b, st) != hipSuccess) {
+  if (hipEventRecord(p->ev.back().second, st) != hipSuccess) {
     (void)hipGetLastError();
+    g_pool[p->dev].push_back(p->ev.back());   // this launch's pair: never completed
+    p->ev.pop_back();
     if (s.open == p) s.open = nullptr;
-    if (p->n > 0) {   // the burst's earlier launches: b holds the last of them
+    if (p->n > 0) {   // the burst's earlier launches stand on their own
       g_pending.push_back(p);
       return;
     }
     if (p->cand >= 0 && p->gen == s.gen) s.issued[p->cand]--;
-    g_pool[p->dev].emplace_back(p->a, p->b);
     delete p;
     return;
   }

@@ -7,21 +7,29 @@
 
 namespace vsiq {
 
+// A body's qparams: a QP computed by the caller, or a callable that loads them (round 6:
+// called once the body's first loads are issued, so a kernel's qparam reads -- scalar
+// loads, load_qp<true> -- overlap its streaming loads instead of preceding them)
+__device__ __forceinline__ const QP &qp_of(const QP &p) { return p; }
+template <class F>
+__device__ __forceinline__ QP qp_of(const F &f) { return f(); }
+
 // ----------------------------------------------------------------------------
 // K1: y = fq(act(x)), one-shot (kFlatU groups per lane, no loop: exact vmcnt)
 // ----------------------------------------------------------------------------
 // U groups per lane: kFlatU, or 9 for a one-round grid whose stores wait behind the
 // store gate (gc: gate_begin at the workgroup start; gate 0 = no gate).
-template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U = kFlatU>
+template <bool VEC, bool NT, bool CODES, bool MASK, int ACT, int U = kFlatU, class QF = QP>
 __device__ __forceinline__ void fq_fwd_block(const float *__restrict__ x, float *__restrict__ y,
                                              uint8_t *__restrict__ codes, uint64_t *__restrict__ mask,
-                                             int64_t n, const QP &p, int64_t blk, GateClk gc = GateClk{0},
+                                             int64_t n, const QF &qf, int64_t blk, GateClk gc = GateClk{0},
                                              uint32_t gate = 0, const SiluLay &L = SiluLay{}) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * U + threadIdx.x;   // lanes chunk-aligned
   f4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) v[u] = load_group_c<VEC, NT>(x, base + u * kBlock, ng, n);
+  const QP &p = qp_of(qf);
   GroupOut go[U];
   uint32_t mlo = 0, mhi = 0;
 #pragma unroll
@@ -228,10 +236,10 @@ __device__ __forceinline__ void lsq_group(float *gx, int64_t i, int64_t ng, int6
 // group k+kLsqPrefetch is loaded while group k computes, so x/g loads stay in flight
 // and s_waitcnt counts are exact.  Adds this thread's terms to c (not reduced) and
 // leaves grad_x in o[] (stored by lsq_store_block once the block has arrived).
-template <bool VEC, bool NT, bool ZPL, int ACT, int G>
-__device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const float *__restrict__ x,
-                                              int64_t n, const QP &p, int64_t blk, LsqAcc &c, f4 (&o)[G],
-                                              const SiluLay &L = SiluLay{}) {
+template <bool VEC, bool NT, bool ZPL, int ACT, int G, class QF = QP>
+__device__ __forceinline__ QP lsq_bwd_block(const float *__restrict__ g, const float *__restrict__ x,
+                                            int64_t n, const QF &qf, int64_t blk, LsqAcc &c, f4 (&o)[G],
+                                            const SiluLay &L = SiluLay{}) {
   const int64_t ng = cdiv(n, 4);
   const int64_t base = blk * kBlock * G + threadIdx.x;
   f4 xv[G], gv[G];
@@ -240,6 +248,7 @@ __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const
     xv[k] = load_group_c<VEC, NT>(x, base + k * kBlock, ng, n);
     gv[k] = load_group_c<VEC, NT>(g, base + k * kBlock, ng, n);
   }
+  const QP &p = qp_of(qf);
 #pragma unroll
   for (int k = 0; k < G; ++k) {
     if (k + kLsqPrefetch < G) {
@@ -248,6 +257,7 @@ __device__ __forceinline__ void lsq_bwd_block(const float *__restrict__ g, const
     }
     o[k] = lsq_group_out<ZPL, ACT>(base + k * kBlock, ng, n, xv[k], gv[k], p, c, L);
   }
+  return p;
 }
 
 template <bool VEC, bool NT, int G>

@@ -11,8 +11,9 @@ __global__ __launch_bounds__(kBlock) void k_fq_fwd(const float *__restrict__ x, 
                                                    uint64_t *__restrict__ mask, int64_t n,
                                                    QPSrc src, uint32_t gate, SiluLay L) {
   const GateClk gc = gate_begin(gate);
-  const QP p = load_qp(src);
-  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, p, blockIdx.x, gc, gate, L);
+  // the kernel-uniform qparams as scalar loads, after the x loads are issued
+  fq_fwd_block<VEC, NT, CODES, MASK, ACT, U>(x, y, codes, mask, n, [&] { return load_qp<true>(src); }, blockIdx.x,
+                                             gc, gate, L);
 }
 
 // One-round grids get the store gate (store_gate_select: >= 2 workgroups per CU, all

@@ -17,10 +17,18 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
                                                     double *__restrict__ ws,
                                                     uint32_t *__restrict__ counter, uint32_t gate) {
   const GateClk gc = gate_begin(gate);
-  const QP p = load_qp(src);
   LsqAcc c{0.0, 0.0};
   f4 o[G];
-  lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o, L);
+  // G <= 2 (C4's small one-round layers): the kernel-uniform qparams as scalar loads after
+  // the first x / g loads are issued (round 6).  Deeper grids keep them first: the late
+  // loads cost 2 VGPRs there, one wave per SIMD at G = 4 / 8 (C3's K4: 98 VGPRs, 4 waves).
+  QP p;
+  if constexpr (G <= 2) {
+    p = lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, [&] { return load_qp<true>(src); }, blockIdx.x, c, o, L);
+  } else {
+    p = load_qp(src);
+    (void)lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, p, blockIdx.x, c, o, L);
+  }
   if (PART) {
     // no arrival to order against: every wave issues its grad_x stores first, so the
     // block reduction runs while they drain (the one-round grids of small layers end
@@ -403,7 +411,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   extern __shared__ f4 s_o[];   // SPLIT: [NV][kBlock]
   const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x;
-  const QP p = load_qp(QPSrc{nullptr, scale + row, zp ? zp + row : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   const int64_t ng = cdiv(rowlen, 4);
   const float *xr = x + row * rowlen, *gr = g + row * rowlen;
   float *gxr = gx + row * rowlen;
@@ -415,6 +422,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     xv[k] = load_group_c<VEC, NT>(xr, threadIdx.x + k * kBlock, ng, rowlen);
     gv[k] = load_group_c<VEC, NT>(gr, threadIdx.x + k * kBlock, ng, rowlen);
   }
+  // the row's qparams after its loads are issued, as scalar loads (ld_uniform_f64)
+  const QP p = load_qp<true>(QPSrc{nullptr, scale + row, zp ? zp + row : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     if (SPLIT && k == ISSUE) {
@@ -520,6 +529,9 @@ inline int64_t pcc_images(int64_t rowlen) {
 // fixed order of k_pcm_lsq_fold (same bits), writes grad_scale[c] / grad_zp[c] and
 // resets counters[c].  grad_x is stored after the arrival, so the drain waits only for
 // the record.  No workgroup waits for another.
+// Round 6 at 256x256x10x10: the channel's qparams as scalar loads after the x / g loads
+// 22.2 -> 21.3 us; grad_x staged in LDS at 7 waves / SIMD (11 spilled VGPRs) 25.4 us, not
+// taken (profiles/r06/r06k_k6_column.txt).
 template <bool NT, bool ZPL, bool ARRIVE>
 __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict__ g,
                                                         const float *__restrict__ x,
@@ -537,19 +549,22 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   const uint32_t nr = (uint32_t)std::min<int64_t>(nb_img, images - n0);
   const uint32_t gpr = (uint32_t)(rowlen / 4);
   const uint32_t nj = nr * gpr;
-  const QP p = load_qp(QPSrc{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   const int64_t rstride = channels * rowlen;               // floats between (n, c) and (n+1, c)
   const int64_t base = (n0 * channels + c) * rowlen;
+  const float *xb = x + base, *gb = g + base;
+  float *gxb = gx + base;
   f4 xv[kColGroups], gv[kColGroups];
-  int64_t off[kColGroups];
+  uint32_t off[kColGroups];   // floats from base: < nb_img * channels * rowlen < 2^31 (host check)
 #pragma unroll
   for (int k = 0; k < kColGroups; ++k) {
     const uint32_t j = threadIdx.x + k * kBlock;
     const uint32_t jj = j < nj ? j : nj - 1;
-    off[k] = base + (int64_t)(jj / gpr) * rstride + 4 * (jj % gpr);
-    xv[k] = load_group<true, NT>(x + off[k], 0, 4);
-    gv[k] = load_group<true, NT>(g + off[k], 0, 4);
+    off[k] = (jj / gpr) * (uint32_t)rstride + 4 * (jj % gpr);
+    xv[k] = load_group<true, NT>(xb + off[k], 0, 4);
+    gv[k] = load_group<true, NT>(gb + off[k], 0, 4);
   }
+  // the channel's qparams after the loads are issued, as scalar loads (ld_uniform_f64)
+  const QP p = load_qp<true>(QPSrc{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   LsqAcc acc{0.0, 0.0};
   f4 o[kColGroups];
 #pragma unroll
@@ -560,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   if (!ARRIVE) {
 #pragma unroll
     for (int k = 0; k < kColGroups; ++k)
-      if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
+      if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gxb + off[k], 0, 4, o[k]);
     lsq_block_reduce(acc);
     if (threadIdx.x == 0) {
       ws[2 * (int64_t)b] = acc.t;
@@ -585,7 +600,7 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kColGroups; ++k)
-    if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gx + off[k], 0, 4, o[k]);
+    if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gxb + off[k], 0, 4, o[k]);
   if (!s_last) return;
   LsqAcc f{0.0, 0.0};   // k_pcm_lsq_fold's order: thread j sums records j, j + 256, ... then the tree
   for (uint32_t i = threadIdx.x; i < nib; i += kBlock) {
@@ -755,7 +770,8 @@ int vsiq_pcm_lsq_bwd_arrive_f32(const float *g, const float *x, float *gx, int64
   }
   int64_t frows = rows, fchunks = chunks;   // record layout the fold reads
   const int packed = g_tune.pc_packed;
-  if (vec && pc_packed(rowlen) && rows > channels && packed == 1) {   // axis 1, short rows: columns
+  if (vec && pc_packed(rowlen) && rows > channels && packed == 1 &&
+      pcc_images(rowlen) * channels * rowlen < ((int64_t)1 << 31)) {   // axis 1, short rows: columns
     frows = nt ? launch_pcc_lsq<true>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,
                                       (float)qmax, ws, counters, gscale, grad_scale_out, grad_zp_out, st)
                : launch_pcc_lsq<false>(g, x, gx, rows, rowlen, channels, scale, zp, zp_learn, (float)qmin,

@@ -53,10 +53,11 @@ template <bool NT>
 __global__ __launch_bounds__(kBlock) void k_lsq_fwd_multi(const MBatch b) {
   const int t = mtensor_of(b);
   const MTensor &T = b.t[t];
-  const QP p = load_qp(mtensor_qp(T));
   const int64_t blk = (int64_t)blockIdx.x - b.blk0[t];
-  if (T.vec) fq_fwd_block<true, NT, false, false, kActNone>(T.x, T.y, nullptr, nullptr, T.n, p, blk);
-  else fq_fwd_block<false, NT, false, false, kActNone>(T.x, T.y, nullptr, nullptr, T.n, p, blk);
+  // the tensor's qparams (workgroup-uniform) as scalar loads, after the x loads are issued
+  const auto qf = [&] { return load_qp<true>(mtensor_qp(T)); };
+  if (T.vec) fq_fwd_block<true, NT, false, false, kActNone>(T.x, T.y, nullptr, nullptr, T.n, qf, blk);
+  else fq_fwd_block<false, NT, false, false, kActNone>(T.x, T.y, nullptr, nullptr, T.n, qf, blk);
 }
 
 // Backward: block partial -> ws record (global block index), flat arrival on the
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd_multi(const MBatch b, double
   const int t = mtensor_of(b);
   const MTensor &T = b.t[t];
   const QPSrc src = mtensor_qp(T);
-  const QP p = load_qp(src);
+  const auto qf = [&] { return load_qp<true>(src); };   // scalar loads, after the first loads
   const uint32_t first = b.blk0[t], nb = b.blk0[t + 1] - first;
   const int64_t blk = (int64_t)blockIdx.x - first;
   LsqAcc c{0.0, 0.0};
@@ -76,11 +77,12 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd_multi(const MBatch b, double
   f4 o[kMultiG];
   double rec[2], f[2];
   bool w0;
+  QP p;
   if (T.vec) {
-    lsq_bwd_block<true, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, p, blk, c, o);
+    p = lsq_bwd_block<true, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, qf, blk, c, o);
     w0 = lsq_block_record<true, NT, kMultiG>(c, T.gx, T.n, blk, o, rec);
   } else {
-    lsq_bwd_block<false, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, p, blk, c, o);
+    p = lsq_bwd_block<false, NT, true, kActNone, kMultiG>(T.g, T.x, T.n, qf, blk, c, o);
     w0 = lsq_block_record<false, NT, kMultiG>(c, T.gx, T.n, blk, o, rec);
   }
   if (!w0) return;   // waves 1..3 have stored their grad_x

@@ -56,10 +56,12 @@ struct PCFixed {
   int64_t channels;
 };
 
+// UNI: `row` is wave-uniform (scalar qparam loads, ld_uniform_f64); rows < 2^31 (host check)
+template <bool UNI = false>
 __device__ __forceinline__ QP pc_fixed_qp(const PCFixed &a, int64_t row) {
-  const int64_t c = row % a.channels;
+  const int64_t c = (uint32_t)row % (uint32_t)a.channels;
   QPSrc s{nullptr, a.scale + c, a.zp ? a.zp + c : nullptr, 0.0, 0.0, a.lo, a.hi, a.zp_round, 0};
-  return load_qp(s);
+  return load_qp<UNI>(s);
 }
 
 // U groups per lane: kFlatU, or 9 for a one-round grid behind the store gate
@@ -72,7 +74,6 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
   const GateClk gc = gate_begin(gate);
   const int64_t row = blockIdx.x / chunks;
   const int64_t chunk = blockIdx.x % chunks;
-  const QP p = pc_fixed_qp(a, row);
   const int64_t ng = cdiv(a.rowlen, 4);
   const float *xr = x + row * a.rowlen;
   float *yr = y + row * a.rowlen;
@@ -80,6 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_pc_fq_fwd(const float *__restrict__ 
   f4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) v[u] = load_group_c<VEC, NT>(xr, base + u * kBlock, ng, a.rowlen);
+  const QP p = pc_fixed_qp<true>(a, row);   // after the x loads are issued, on lgkmcnt
   GroupOut go[U];
   uint32_t mlo = 0, mhi = 0;
 #pragma unroll

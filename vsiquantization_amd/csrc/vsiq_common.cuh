@@ -577,14 +577,37 @@ struct QPSrc {
   int discrete;         // write clamp(round(x/s+zp)) itself (discreate_tensor) instead of y
 };
 
+// A wave-uniform f64 read as a scalar load (s_load_dwordx2).  Scalar loads count on
+// lgkmcnt, so a kernel can issue its streaming loads first and then wait for its qparams
+// without waiting for those; the same read as a global_load is ordered with them on vmcnt.
+// (Round 6, the learnable per-channel forward at C2: the compiler put the scale / zp
+// global_loads and their vmcnt(0) waits ahead of the x loads -- the gate sweep's optimum
+// sat 0.65 us later than K3's and the kernel at 0.75 against K3's 0.79.)  `p` must be the
+// same in every lane; a read-only value of an earlier launch (the scalar cache is
+// invalidated at each dispatch).
+__device__ __forceinline__ double ld_uniform_f64(const double *p) {
+  const uint64_t u = (uint64_t)(uintptr_t)p;
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32));
+  return *(const __attribute__((address_space(4))) double *)((hi << 32) | lo);
+}
+
+// UNI: every pointer of `a` is wave-uniform -> scalar loads (ld_uniform_f64)
+template <bool UNI = false>
+__device__ __forceinline__ double ld_qp_f64(const double *p) {
+  if constexpr (UNI) return ld_uniform_f64(p);
+  else return *p;
+}
+
+template <bool UNI = false>
 __device__ __forceinline__ QP load_qp(const QPSrc &a) {
   double s, z;
   if (a.qp) {
-    s = a.qp[VSIQ_QP_SCALE];
-    z = a.qp[VSIQ_QP_ZP];
+    s = ld_qp_f64<UNI>(a.qp + VSIQ_QP_SCALE);
+    z = ld_qp_f64<UNI>(a.qp + VSIQ_QP_ZP);
   } else {
-    s = a.sdev ? *a.sdev : a.shost;
-    z = a.zdev ? *a.zdev : a.zhost;
+    s = a.sdev ? ld_qp_f64<UNI>(a.sdev) : a.shost;
+    z = a.zdev ? ld_qp_f64<UNI>(a.zdev) : a.zhost;
     if (a.zround) {
       // quantizers/uniform.py:98-102: clamp(round(zp), qmin, qmax) in f64, NaN propagates
       const double zr = __builtin_rint(z);
