@@ -203,10 +203,14 @@ def _manager_sequence(case, exact):
     if exact:
         assert [float(v) for v in qm.mean_abs_x] == cal["mean_abs_x"]
         assert [float(v) for v in qm.mean_x] == cal["mean_x"]
+        assert [float(v) for v in qm.std] == cal["std"]
     else:
         np.testing.assert_allclose(qm.mean_abs_x, cal["mean_abs_x"], rtol=1e-6)
         np.testing.assert_allclose(qm.mean_x, cal["mean_x"], rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(qm.std, cal["std"], rtol=1e-6)
+        np.testing.assert_allclose(qm.std, cal["std"], rtol=1e-6)
+    # every recorded value is an fp32 value, as the reference's .item() of an fp32 tensor
+    for v in list(qm.mean_abs_x) + list(qm.mean_x) + list(qm.std):
+        assert float(np.float32(v)) == v
     qm.is_quantize = True
     y = qm.quantize(cu(G.arr(case["x_oq"])))
     G.assert_bitwise_f32(npy(y), G.arr(case["y_oq"]), "observe+quantize")

@@ -133,8 +133,8 @@ def test_host_loop_equals_oracle(act, nthreads):
 
 def test_manager_chain_host_golden_init_scale():
     """calibrate (observe only) -> observe+quantize -> init_scaling_factor_for_learning on
-    CPU tensors under the golden host's mean reference: mean_abs_x and the init scale are
-    the reference's bits, with no value injected."""
+    CPU tensors under the golden host's mean reference: mean_abs_x, mean_x, std and the init
+    scale are the reference's bits, with no value injected."""
     import vsiquantization_amd as V
     import vsiquantization_amd._hip as H
     H.set_mean_reference(GOLDEN_THREADS)
@@ -147,6 +147,7 @@ def test_manager_chain_host_golden_init_scale():
                 qm.quantize(torch.from_numpy(G.arr(k).copy()))
             assert [float(v) for v in qm.mean_abs_x] == c["calib"]["mean_abs_x"]
             assert [float(v) for v in qm.mean_x] == c["calib"]["mean_x"]
+            assert [float(v) for v in qm.std] == c["calib"]["std"]   # the f64 std rounded to fp32
             qm.is_quantize = True
             qm.quantize(torch.from_numpy(G.arr(c["x_oq"]).copy()))
             qm.is_learning_scale = True

@@ -38,6 +38,14 @@ from ..utils.registry import CLASS_REGISTRY
 from .per_channel import PerChannelUniformQuantizer
 
 _STAT_NAMES = ("mean_abs_x", "mean_x", "std")
+
+
+def _as_f32(t: torch.Tensor) -> torch.Tensor:
+    """f64 stats -> the fp32 values the reference's lists hold (quantization_manager.py:66-68
+    append torch.mean / torch.std of an fp32 tensor, .item()-ed: fp32 values), kept as f64.
+    Under a mean reference mean|x| / mean are torch's bits already (K11) and the f64 std
+    rounds to torch's fp32 std (its two-pass f64 sum about the fp32 mean, rounded once)."""
+    return t.to(torch.float32).to(torch.float64)
 _QP_ATTRS = ("scale", "zero_point")
 
 # Calibration-time observer streams: an observe-only call (is_quantize False) has no
@@ -237,7 +245,7 @@ class QuantizationManager(nn.Module):
         self._join()
         pend = self.__dict__.get("_dev_stats")
         if pend:
-            rows = torch.stack(pend).cpu().tolist()
+            rows = _as_f32(torch.stack(pend).cpu()).tolist()
             self.__dict__["_dev_stats"] = []
             for r in rows:
                 for i in range(3):
@@ -373,7 +381,7 @@ class QuantizationManager(nn.Module):
                     recs[i, H.ST_MEANABS] = float(m[2])
                     recs[i, H.ST_MEAN] = float(m[3])
         mn, mx = replay_minmax(mn, mx, recs[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
-        cols = [recs[:, col].tolist() for col in (H.ST_MEANABS, H.ST_MEAN, H.ST_STD)]
+        cols = [_as_f32(recs[:, col]).tolist() for col in (H.ST_MEANABS, H.ST_MEAN, H.ST_STD)]
         # commit: no pending records from here on, so the writes below do not fold again
         d = self.__dict__
         d["_pending_records"] = []
