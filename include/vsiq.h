@@ -99,9 +99,11 @@ int64_t vsiq_mask_words(int64_t rows, int64_t rowlen);
                                           per launch site (kernel, grid, bytes, device) from
                                           event-timed launches; 0: fixed 1.05 x the read time
                                           at 7.5 TB/s */
-#define VSIQ_TUNE_XCD_ORDER 13         /* 1 (default): XCD-contiguous workgroup order where
-                                          neighbouring workgroups share cache lines (K6 on
-                                          channel columns); 0: hardware order */
+#define VSIQ_TUNE_XCD_ORDER 13         /* where neighbouring workgroups share cache lines (K6
+                                          on channel columns of short rows): 2 (default) each
+                                          XCD a range of channels, image blocks outermost
+                                          (channels % 8 == 0, else 1); 1: XCD-contiguous
+                                          block order; 0: hardware order */
 #define VSIQ_TUNE_K2O_FORM 14          /* K2o: 0 (default) one-shot, one record per workgroup;
                                           1: grid-stride, vsiq_act_observe_part_f32's records */
 #define VSIQ_TUNE_K2O_GROUPS 15        /* K2o one-shot groups per lane 1/2/4/8/16, 0 = default (2) */
@@ -159,7 +161,9 @@ int vsiq_trace_marker(int end, void *stream);
  * is applied first, as the fused layers record act(x).  One extra read of x (opt-in in
  * the Python layer).  out4 (device, nullable): {sum |act(x)|, sum act(x), mean |act(x)|,
  * mean act(x)} as fp32; stats (device, nullable): its VSIQ_ST_MEANABS / VSIQ_ST_MEAN
- * entries overwritten with the two means.  ws: vsiq_torch_mean_ws_bytes(n, vec,
+ * entries overwritten with the two means and VSIQ_ST_STD with torch.std(act(x)) as torch's
+ * CPU kernel computes it (qm.py:68: f64 sum of squared deviations from the fp32 mean,
+ * rounded to fp32 once; a second read of x).  ws: vsiq_torch_mean_ws_bytes(n, vec,
  * threads) bytes (-1: unsupported arguments -- vec not 8 / 16, threads outside 1..4096,
  * a chunk of 2^30 elements or more).  n = 0 gives NaN means, as torch.mean.
  */

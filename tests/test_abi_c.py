@@ -26,7 +26,7 @@ int main(void) {
     return 5;                                                           /* n < 0 */
   if (vsiq_fq_fwd_f32(NULL, NULL, NULL, NULL, 0, NULL, NULL, 1.0, NULL, 0.0, 0, 0, 0, 1, NULL) != 0)
     return 6;                                                           /* n == 0: no-op */
-  if (vsiq_set_tuning(VSIQ_TUNE_XCD_ORDER, 2) == 0) return 7;
+  if (vsiq_set_tuning(VSIQ_TUNE_XCD_ORDER, 3) == 0) return 7;
   if (vsiq_observe_part_records(1) != 4) return 8;                    /* one record per wave */
   if (vsiq_lsq_fold_multi(NULL, 0, NULL) != 0) return 9;
   printf("ok %d\n", vsiq_abi_version());

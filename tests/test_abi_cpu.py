@@ -164,9 +164,11 @@ def test_tuning_keys_match_header_and_bounds():
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 2) == 0
     assert lib.vsiq_set_tuning(H.TUNE_GATE_AUTOTUNE, 2) != 0
     assert lib.vsiq_set_tuning(H.TUNE_PC_PACKED, 1) == 0
-    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 2) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 3) != 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 2) == 0
     assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 0) == 0
     assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 1) == 0
+    assert lib.vsiq_set_tuning(H.TUNE_XCD_ORDER, 2) == 0   # back to the default
     assert lib.vsiq_set_tuning(99, 0) != 0
 
 

@@ -89,7 +89,8 @@ def test_pc_lsq_vs_oracle(shape, axis):
                                    (256, 37, 10, 10), (9, 300, 6, 6)])
 def test_packed_rows_equal_per_row_grid(shape):
     """Channel columns for K6 (VSIQ_TUNE_PC_PACKED 1, default; 10x10 rows in XCD-contiguous
-    block order, VSIQ_TUNE_XCD_ORDER 0 the hardware order) and packed short rows (2) vs
+    block order, VSIQ_TUNE_XCD_ORDER 0 the hardware order, 2 channel ranges per XCD) and
+    packed short rows (2) vs
     one workgroup per row (0): y / grad_x bit for bit, per-channel gradients to float64
     reordering."""
     from vsiquantization_amd import _hip as H
@@ -101,17 +102,18 @@ def test_packed_rows_equal_per_row_grid(shape):
     z = torch.tensor(np.rint(rng.uniform(0, 255, C)) + 0.2, dtype=torch.float64, device=DEV)
     out = {}
     try:
-        for packed, xo in ((1, 1), (1, 0), (2, 1), (0, 1)):
+        for packed, xo in ((1, 1), (1, 0), (1, 2), (2, 1), (0, 1)):
             H.set_tuning(H.TUNE_PC_PACKED, packed)
             H.set_tuning(H.TUNE_XCD_ORDER, xo)
             y = FQ.per_channel_fake_quant(cu(x), s, z, 0, 255, zp_round=True, axis=1)[0]
             gx, gs, gz = FQ.pc_lsq_backward(cu(g), cu(x), s, z, 0, 255, 1e-3, True, 1)
-            out[packed if xo else -1] = [npy(t) for t in (y, gx, gs, gz)]
+            out[packed if xo == 1 else -1 - xo] = [npy(t) for t in (y, gx, gs, gz)]
     finally:
         H.set_tuning(H.TUNE_PC_PACKED, 1)
-        H.set_tuning(H.TUNE_XCD_ORDER, 1)
+        H.set_tuning(H.TUNE_XCD_ORDER, 2)   # the default
     for k in range(4):   # block order moves no record: every output identical, f64 included
         np.testing.assert_array_equal(out[-1][k], out[1][k])
+        np.testing.assert_array_equal(out[-3][k], out[1][k])
     for mode in (1, 2):
         G.assert_bitwise_f32(out[mode][0], out[0][0], "y")
         G.assert_bitwise_f32(out[mode][1], out[0][1], "grad_x")

@@ -104,5 +104,34 @@ def test_manager_records_reference_means(path):
             want_s.append(float(O.torch_mean(a, 0, 8)))
         assert [float(v) for v in qm.mean_abs_x] == want_a
         assert [float(v) for v in qm.mean_x] == want_s
+        want_sd = [float(_std_ref(O.act_forward(x, "relu") if path == "deferred_relu" else x, 8)) for x in xs]
+        assert [float(v) for v in qm.std] == want_sd
     finally:
         H.clear_mean_reference()
+
+
+def _std_ref(a, threads):
+    """torch.std(a) on a reference host of `threads` threads (tests/test_mean_oracle.py
+    pins this restatement against torch.std): the fp32 mean of that layout as a double,
+    the f64 sum of squared deviations / (n - 1), sqrt, rounded to fp32."""
+    if a.size < 2:
+        return np.float32(np.nan)
+    m = float(O.torch_mean(a, 0, threads))
+    return np.float32(np.sqrt(np.sum((a.astype(np.float64) - m) ** 2) / (a.size - 1)))
+
+
+@pytest.mark.parametrize("act", [None, "relu", "silu"])
+def test_k11_std_pass(act):
+    """vsiq_torch_mean_f32 with a stats record: VSIQ_ST_STD is torch.std(act(x)) of the
+    reference host, bit for bit (fakequant.torch_stats)."""
+    from vsiquantization_amd.fakequant import torch_stats
+    for i, n in enumerate([1, 2, 9, 600, 32769, 1_000_003, 13_107_200]):
+        x = _x(n, 900 + i)
+        actv = H.SiluAct(32, 8) if act == "silu" else act
+        got = torch_stats(torch.from_numpy(x).to(DEV), act=actv, ref=(8, 8)).cpu().numpy()
+        a = O.act_forward(x, act, (32, 8)) if act else x
+        assert _same(got[0], O.torch_mean(a, 1, 8)) and _same(got[1], O.torch_mean(a, 0, 8)), (n, act)
+        assert _same(got[2], _std_ref(a, 8)), (n, act, got[2], _std_ref(a, 8))
+    x = _x(5000, 3)
+    x[17] = np.inf
+    assert np.isnan(torch_stats(torch.from_numpy(x).to(DEV), ref=(8, 8)).cpu().numpy()[2])

@@ -155,3 +155,22 @@ def test_manager_chain_host_golden_init_scale():
             assert qm.scale == c["init_scale"]
     finally:
         H.clear_mean_reference()
+
+
+def _std_restated(a):
+    """torch CPU std of an fp32 tensor (ATen std_var_all_cpu): the fp32 torch.mean as a
+    double, the f64 sum of squared deviations, / (n - 1), sqrt, rounded to fp32 once --
+    what K11's std pass computes (csrc/k_mean.hip)."""
+    a64 = a.astype(np.float64)
+    m = float(torch.mean(torch.from_numpy(a)))
+    return np.float32(np.sqrt(np.sum((a64 - m) ** 2) / (a.size - 1)))
+
+
+@pytest.mark.parametrize("n", [2, 7, 600, 8193, 40_000, 1_000_003])
+def test_std_restatement_equals_torch_std(n):
+    """The restated std equals torch.std on this host bit for bit (the order of the f64 sum
+    only moves it ~1e-16 relative, which the fp32 rounding absorbs)."""
+    rng = np.random.default_rng(n)
+    for scale, shift in ((1.0, 0.0), (0.05, 3.0), (10.0, -1.0)):
+        a = (rng.standard_normal(n) * scale + shift).astype(np.float32)
+        assert _std_restated(a).tobytes() == torch.std(torch.from_numpy(a)).numpy().tobytes(), (n, scale, shift)

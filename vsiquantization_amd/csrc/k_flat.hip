@@ -1336,7 +1336,7 @@ int vsiq_set_tuning(int key, int value) {
       g_tune.gate_autotune = value;
       return 0;
     case VSIQ_TUNE_XCD_ORDER:
-      if (value != 0 && value != 1) return VSIQ_E_ARG;
+      if (value < 0 || value > 2) return VSIQ_E_ARG;
       g_tune.xcd_order = value;
       return 0;
     case VSIQ_TUNE_K2O_FORM:

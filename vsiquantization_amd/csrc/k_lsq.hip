@@ -543,7 +543,16 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
                                                         uint32_t *__restrict__ counters, uint32_t nib,
                                                         double gscale, double *__restrict__ gs_out,
                                                         double *__restrict__ gz_out) {
-  const uint32_t b = xo ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;   // logical block i*C + c
+  // logical block i*C + c.  xo 1: XCD-contiguous (xcd_block); xo 2 (channels % 8 == 0): XCD x
+  // takes channels [x C/8, (x+1) C/8) of every image block, image blocks outermost, so the
+  // neighbours sharing lines stay on one XCD and the short last image block runs last
+  uint32_t b = blockIdx.x;
+  if (xo == 1) {
+    b = xcd_block(blockIdx.x, gridDim.x);
+  } else if (xo == 2) {
+    const uint32_t cpx = (uint32_t)channels / kXcds, k = blockIdx.x / kXcds;
+    b = (k / cpx) * (uint32_t)channels + (blockIdx.x % kXcds) * cpx + k % cpx;
+  }
   const int64_t c = b % channels;
   const int64_t n0 = (int64_t)(b / channels) * nb_img;
   const uint32_t nr = (uint32_t)std::min<int64_t>(nb_img, images - n0);
@@ -630,8 +639,12 @@ void launch_pcc_k(const float *g, const float *x, float *gx, int64_t images, int
                   double *ws, uint32_t *counters, double gscale, double *gs, double *gz, hipStream_t st) {
   // XCD-contiguous order where a row ends mid-line: at 10x10 rows ~half of the lines
   // are shared with the neighbouring channel's workgroup (PMC fetch 1.30x -> 1.04x the
-  // algorithmic bytes, 24.2 -> 21.7 us at 256x256x10x10); 20x20 and up measured slower
-  const uint32_t xo = g_tune.xcd_order != 0 && (rowlen * 4) % 128 != 0 && rowlen * 4 <= 512;
+  // algorithmic bytes, 24.2 -> 21.7 us at 256x256x10x10); 20x20 and up measured slower.
+  // Order 2 (round 6, the default where channels % 8 == 0) keeps that sharing and runs the
+  // short last image block last: 18.78 / 18.36 us against order 1's 18.84 / 18.96 and the
+  // hardware order's 21.60 / 20.74 on one box (profiles/r06/r06l_k6_xcd_order.txt)
+  uint32_t xo = g_tune.xcd_order != 0 && (rowlen * 4) % 128 != 0 && rowlen * 4 <= 512 ? 1u : 0u;
+  if (xo && g_tune.xcd_order == 2 && channels % kXcds == 0) xo = 2;
   hipLaunchKernelGGL((k_pcc_lsq_bwd<NT, ZPL, ARRIVE>), dim3((unsigned)grid), dim3(kBlock), 0, st, g, x, gx, images,
                      rowlen, (uint32_t)nb, channels, scale, zp, lo, hi, ws, xo, counters,
                      (uint32_t)cdiv(images, nb), gscale, gs, gz);

@@ -18,6 +18,12 @@
 //          sequential chain loads 16 values at a time (round 6's first form chained up
 //          to 1600 dependent loads per lane at one thread: 290 us at 52M elements).
 //   final  (one lane) the `threads`-slot second pass, then sum / float(n).
+//   std    (with a stats record) torch.std(act(x)) as torch's CPU kernel computes it
+//          (ATen std_var_all_cpu, quantization_manager.py:68): the fp32 mean above taken
+//          as a double, the sum of (double(v) - mean)^2 in f64, / (n - 1), sqrt, rounded
+//          to fp32 once.  The f64 sum's order differs from torch's parallel_reduce, which
+//          moves the result ~1e-16 relative: the fp32 rounding absorbs it except when the
+//          value straddles a rounding boundary.  kStdParts fixed-order partials, one fold.
 // Both sums (|act(x)| and act(x)) ride the same pass.  HBM: 4 B / element read; the
 // level-1 nodes (8 B per 256 elements at V = 8) are written once and read once.
 #include "mean_cascade.cuh"
@@ -200,6 +206,47 @@ __global__ __launch_bounds__(64) void k_mean_final(const MAcc *csum, MeanLay m, 
   }
 }
 
+constexpr int kStdParts = 512;
+
+template <int ACT>
+__global__ __launch_bounds__(256) void k_std_part(const float *__restrict__ x, int64_t n,
+                                                  const double *__restrict__ stats, SiluLay L,
+                                                  double *__restrict__ part) {
+  __shared__ double s_w[256 / kWave];
+  const double m = stats[VSIQ_ST_MEAN];   // torch: self.mean().item<double>()
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double d = (double)mean_elem<ACT>(x[i], i, L).s - m;
+    acc += d * d;
+  }
+  acc = wave_reduce(acc, AddD());
+  if (threadIdx.x % kWave == 0) s_w[threadIdx.x / kWave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 256 / kWave; ++w) t += s_w[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_std_final(const double *__restrict__ part, int parts, int64_t n,
+                                                  double *__restrict__ stats) {
+  double t = 0.0;
+  for (int i = threadIdx.x; i < parts; i += 64) t += part[i];
+  t = wave_reduce(t, AddD());
+  if (threadIdx.x == 0) {
+    const double dn = (double)n - 1.0;
+    const double var = t / (dn > 0.0 ? dn : 0.0);   // n <= 1: 0 / 0 = NaN, as torch
+    stats[VSIQ_ST_STD] = (double)(float)__builtin_sqrt(var);
+  }
+}
+
+template <int ACT>
+void launch_std(const float *x, int64_t n, double *stats, const SiluLay &L, double *part, hipStream_t st) {
+  hipLaunchKernelGGL((k_std_part<ACT>), dim3(kStdParts), dim3(256), 0, st, x, n, stats, L, part);
+}
+
 int64_t tiles_max_of(const MeanLay &m, int64_t n, int V) {
   int64_t t = 0;
   if (m.nchunks > 0) {
@@ -256,7 +303,8 @@ void launch_mean16(const MeanArgs &a, const MeanLay &m, hipStream_t st) {
 int64_t mean_ws_bytes(int64_t n, int vec, int threads) {
   const MeanLay m = mean_lay(n, threads);
   const int64_t tm = tiles_max_of(m, n, vec), l2 = l2_max_of(m, n, vec);
-  return (int64_t)sizeof(MAcc) * (m.nchunks * (tm + l2) * 4 * vec + (m.nchunks > 0 ? m.nchunks : 1));
+  return (int64_t)sizeof(MAcc) * (m.nchunks * (tm + l2) * 4 * vec + (m.nchunks > 0 ? m.nchunks : 1)) +
+         (int64_t)sizeof(double) * kStdParts;   // the std pass's partials (8-B aligned: MAcc is 8 B)
 }
 
 }  // namespace vsiq
@@ -293,6 +341,11 @@ int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads
     else VSIQ_ACT(act, launch_mean16, a, m, st);
   }
   hipLaunchKernelGGL(k_mean_final, dim3(1), dim3(64), 0, st, a.csum, m, vec, threads, n, out4, stats);
+  if (stats) {
+    double *part = reinterpret_cast<double *>(a.csum + (m.nchunks > 0 ? m.nchunks : 1));
+    VSIQ_ACT(act, launch_std, x, n, stats, a.L, part, st);
+    hipLaunchKernelGGL(k_std_final, dim3(1), dim3(64), 0, st, part, kStdParts, n, stats);
+  }
   return launch_rc();
 }
 

@@ -58,7 +58,7 @@ struct Tuning {
   std::atomic<int> lsq_groups{0};          // K4 groups per lane 2 / 4 / 8 / 16 (0 = by size)
   std::atomic<int> store_gate{-1};         // store gate ticks (10 ns) for one-round grids (-1 = auto, 0 = off)
   std::atomic<int> gate_autotune{1};       // store gate tuned online per launch site (0 = fixed estimate)
-  std::atomic<int> xcd_order{1};           // XCD-contiguous block order where neighbours share lines
+  std::atomic<int> xcd_order{2};           // XCD block order where neighbours share lines (k_lsq.hip K6 columns)
   std::atomic<int> k2o_form{0};            // K2o: 0 one-shot (one record per workgroup), 1 grid-stride (K2p's records)
   std::atomic<int> k2o_groups{0};          // K2o one-shot groups per lane 1 / 2 / 4 / 8 / 16 (0 = default 2)
   std::atomic<int> k2o_block{0};           // K2o one-shot lanes per workgroup 256 / 512 / 1024 (0 = default 256)

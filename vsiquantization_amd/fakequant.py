@@ -685,6 +685,31 @@ def torch_mean(x: torch.Tensor, act=None, ref=None) -> torch.Tensor:
     return out
 
 
+def torch_stats(x: torch.Tensor, act=None, ref=None) -> torch.Tensor:
+    """f64[3] {mean|act(x)|, mean act(x), std act(x)} as quantization_manager.py:66-68
+    records them on a host of layout ``ref`` (torch.mean / torch.std of the fp32 tensor,
+    .item()-ed): K11 and its std pass (vsiq_torch_mean_f32 with a stats record), on x's
+    device.  CPU tensors: torch_mean's two means and NaN for std (the host observer's
+    record holds the host std)."""
+    from . import host
+    if host.is_host(x):
+        m = torch_mean(x, act=act, ref=ref)
+        return torch.stack([m[2].double(), m[3].double(), torch.tensor(float("nan"), dtype=torch.float64)])
+    if ref is None:
+        ref = H.mean_reference() or (8, torch.get_num_threads())
+    vec, threads = int(ref[0]), int(ref[1])
+    x = H.require_device_f32(x)
+    nb = int(H.lib().vsiq_torch_mean_ws_bytes(_i64(x.numel()), vec, threads))
+    if nb < 0:
+        raise ValueError(f"torch_stats: unsupported layout {ref} for {x.numel()} elements")
+    ws = torch.empty(max(nb, 8), dtype=torch.uint8, device=x.device)
+    st = torch.zeros(H.ST_LEN, dtype=torch.float64, device=x.device)
+    rc = H.lib().vsiq_torch_mean_f32(H.ptr(x), _i64(x.numel()), H.act_code(act), vec, threads, None, H.ptr(st),
+                                     H.ptr(ws), _i64(ws.numel()), H.stream_of(x.device))
+    H.check(rc, "vsiq_torch_mean_f32")
+    return st[H.ST_MEANABS:H.ST_STD + 1]
+
+
 def stats_from_row_sums(row_stats: torch.Tensor, numel: int) -> torch.Tensor:
     """[C,3] per-row (sum|x|, sum x, sum x^2) -> f64[3] fp32-rounded (mean|x|, mean, std)
     (quantization_manager.py:66-68), on the device, no sync."""

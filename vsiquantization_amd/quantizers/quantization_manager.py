@@ -253,18 +253,24 @@ class QuantizationManager(nn.Module):
 
     def _record_stats(self, st3: torch.Tensor, x=None, act=None):
         """st3: (mean|x|, mean, std) of this call.  With a mean reference set
-        (H.set_mean_reference) and the call's tensor given, mean|x| / mean are replaced by
-        torch CPU's exact bits for that host layout (K11, fakequant.torch_mean)."""
+        (H.set_mean_reference) and the call's tensor given, mean|x| / mean / std are replaced
+        by torch CPU's bits for that host layout (K11 and its std pass,
+        fakequant.torch_stats; CPU tensors: the means, the host record's std)."""
         if x is not None and H.mean_reference() is not None and self.dist_group is None:
-            m4 = self._exact_means(x, act)
+            ex = self._exact_stats(x, act)
             st3 = st3.clone()
-            st3[:2] = m4[2:].to(torch.float64)
+            if ex.device.type == "cpu":   # CPU tensor: the means; the host record's std stays
+                st3[:2] = ex[:2].to(st3.device)
+            else:
+                st3.copy_(ex)
         self._dev_stats.append(st3)
 
     @staticmethod
-    def _exact_means(x, act):
-        from ..fakequant import torch_mean
-        return torch_mean(x.detach(), act=act)
+    def _exact_stats(x, act):
+        """f64[3] mean|x| / mean / std of act(x) as the reference host's torch records them
+        (fakequant.torch_stats: K11 and its std pass; CPU tensors: the means, std NaN)."""
+        from ..fakequant import torch_stats
+        return torch_stats(x.detach(), act=act)
 
     # ------------------------------------------------------------------ observe
     def _device_observer(self, x) -> bool:
@@ -363,7 +369,7 @@ class QuantizationManager(nn.Module):
         ex = self.__dict__.setdefault("_exact_pending", [])
         while len(ex) < len(self._pending_records) - 1:
             ex.append(None)
-        ex.append(self._exact_means(x, act) if (H.mean_reference() is not None and self.dist_group is None)
+        ex.append(self._exact_stats(x, act) if (H.mean_reference() is not None and self.dist_group is None)
                   else None)
 
     def _apply_synced_records(self, recs):
@@ -378,8 +384,10 @@ class QuantizationManager(nn.Module):
             for i, e in enumerate(exact[:recs.shape[0]]):
                 if e is not None:
                     m = e.cpu()
-                    recs[i, H.ST_MEANABS] = float(m[2])
-                    recs[i, H.ST_MEAN] = float(m[3])
+                    recs[i, H.ST_MEANABS] = float(m[0])
+                    recs[i, H.ST_MEAN] = float(m[1])
+                    if not torch.isnan(m[2]):
+                        recs[i, H.ST_STD] = float(m[2])
         mn, mx = replay_minmax(mn, mx, recs[:, [H.ST_MIN, H.ST_MAX, H.ST_NAN]].tolist())
         cols = [_as_f32(recs[:, col]).tolist() for col in (H.ST_MEANABS, H.ST_MEAN, H.ST_STD)]
         # commit: no pending records from here on, so the writes below do not fold again
