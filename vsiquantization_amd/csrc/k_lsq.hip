@@ -517,7 +517,14 @@ void launch_pcp_lsq(const float *g, const float *x, float *gx, int64_t rows, int
 // record i*C + c -- k_pcm_lsq_fold's layout for rows' = cdiv(N, NB) * C, one chunk.  No
 // per-group LDS arrays or per-row reductions (the packed-rows form's tail), one block
 // reduction; rows are rowlen floats contiguous (rowlen % 4 == 0, vector path only).
-constexpr int kColGroups = 4;   // groups per lane
+// 8 groups per lane (round 6; 4 before): 81 images of 10x10 per workgroup, 4 waves / SIMD,
+// ONE round at 256x256x10x10 (1024 workgroups) where 4 groups took 1.17 rounds at 6 / SIMD.
+// Kernel-trace medians, two passes on one box (profiles/r06/r06n_k6_column_groups.txt):
+// 10x10 19.08 / 19.00 us against 20.20 / 19.40; 40x40 57.3 / 57.4 against 59.4 / 60.5;
+// 20x20 32.4 / 32.6 against 32.1 / 32.0.  Channel tiles (a workgroup = adjacent channels'
+// contiguous rows of a few images, every load coalesced over the run) measured slower:
+// 24-26 us at 10x10, 38-39 at 20x20 (profiles/r06/r06o_k6_channel_tiles.txt).
+constexpr int kColGroups = 8;
 inline int64_t pcc_images(int64_t rowlen) {
   return std::max<int64_t>(1, (int64_t)kBlock * kColGroups * 4 / rowlen);
 }
@@ -532,8 +539,8 @@ inline int64_t pcc_images(int64_t rowlen) {
 // Round 6 at 256x256x10x10: the channel's qparams as scalar loads after the x / g loads
 // 22.2 -> 21.3 us; grad_x staged in LDS at 7 waves / SIMD (11 spilled VGPRs) 25.4 us, not
 // taken (profiles/r06/r06k_k6_column.txt).
-template <bool NT, bool ZPL, bool ARRIVE>
-__global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict__ g,
+template <bool NT, bool ZPL, bool ARRIVE, int CG = kColGroups>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_pcc_lsq_bwd(const float *__restrict__ g,
                                                         const float *__restrict__ x,
                                                         float *__restrict__ gx, int64_t images,
                                                         int64_t rowlen, uint32_t nb_img, int64_t channels,
@@ -562,10 +569,10 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   const int64_t base = (n0 * channels + c) * rowlen;
   const float *xb = x + base, *gb = g + base;
   float *gxb = gx + base;
-  f4 xv[kColGroups], gv[kColGroups];
-  uint32_t off[kColGroups];   // floats from base: < nb_img * channels * rowlen < 2^31 (host check)
+  f4 xv[CG], gv[CG];
+  uint32_t off[CG];   // floats from base: < nb_img * channels * rowlen < 2^31 (host check)
 #pragma unroll
-  for (int k = 0; k < kColGroups; ++k) {
+  for (int k = 0; k < CG; ++k) {
     const uint32_t j = threadIdx.x + k * kBlock;
     const uint32_t jj = j < nj ? j : nj - 1;
     off[k] = (jj / gpr) * (uint32_t)rstride + 4 * (jj % gpr);
@@ -575,15 +582,15 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   // the channel's qparams after the loads are issued, as scalar loads (ld_uniform_f64)
   const QP p = load_qp<true>(QPSrc{nullptr, scale + c, zp ? zp + c : nullptr, 0.0, 0.0, lo, hi, ZPL ? 1 : 0, 0});
   LsqAcc acc{0.0, 0.0};
-  f4 o[kColGroups];
+  f4 o[CG];
 #pragma unroll
-  for (int k = 0; k < kColGroups; ++k) {
+  for (int k = 0; k < CG; ++k) {
     const uint32_t j = threadIdx.x + k * kBlock;
     o[k] = lsq_group_out<ZPL, kActNone>(j < nj ? 0 : 1, 1, 4, xv[k], gv[k], p, acc);   // i=1: no terms
   }
   if (!ARRIVE) {
 #pragma unroll
-    for (int k = 0; k < kColGroups; ++k)
+    for (int k = 0; k < CG; ++k)
       if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gxb + off[k], 0, 4, o[k]);
     lsq_block_reduce(acc);
     if (threadIdx.x == 0) {
@@ -608,7 +615,7 @@ __global__ __launch_bounds__(kBlock) void k_pcc_lsq_bwd(const float *__restrict_
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kColGroups; ++k)
+  for (int k = 0; k < CG; ++k)
     if (threadIdx.x + k * kBlock < nj) store_group<true, NT>(gxb + off[k], 0, 4, o[k]);
   if (!s_last) return;
   LsqAcc f{0.0, 0.0};   // k_pcm_lsq_fold's order: thread j sums records j, j + 256, ... then the tree
