@@ -402,7 +402,8 @@ __global__ __launch_bounds__(kBlock) void k_pcp_lsq_bwd(const float *__restrict_
 // where holding everything took 128 + 8-17 spilled (round 6, C2 bench leg
 // pc_learn_bwd_k6: 0.67 against 0.56-0.66 for the other forms on the same boxes,
 // profiles/r06/r06f_k6_stages.txt; issue point 5 / 3 / 2 twice each on one box: 0.683 /
-// 0.703 / 0.701, then 0.687 / 0.702 / 0.700, profiles/r06/r06i_k6_issue.txt).
+// 0.703 / 0.701, then 0.687 / 0.702 / 0.700, profiles/r06/r06i_k6_issue.txt).  g by LDS-DMA
+// (global_load_lds, all 18 loads at once) measured no better (profiles/r06/r06q_k6_glds.txt).
 template <bool VEC, bool NT, bool ZPL, int NV, bool SPLIT, int ISSUE = 3>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_pcr_lsq_bwd(
     const float *__restrict__ g, const float *__restrict__ x, float *__restrict__ gx, int64_t rowlen,
