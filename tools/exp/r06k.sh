@@ -5,6 +5,8 @@
 # gate sweep (tools/exp/c2_floor.py), then the K6 column form (axis 1, 256x256x10x10)
 # with grad_x in registers against LDS staging at 7 waves (VSIQ_EXP_PCC_STAGE, a
 # temporary switch) under a kernel trace.
+# (Record of a session: its VSIQ_EXP_PCC_STAGE variant was removed after it; the script
+# no longer selects it.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out

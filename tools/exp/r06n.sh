@@ -3,6 +3,8 @@
 # a temporary switch: 8 = 81 images of 10x10 per workgroup, 4 waves / SIMD, one round at
 # 256x256x10x10) at the three YOLOv8n axis-1 shapes, kernel-trace medians by grid, twice;
 # then the K6 module tests under CG 8.
+# (Record of a session: VSIQ_EXP_PCC_CG was removed after it -- 8 groups per lane is now
+# the only form.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out

@@ -3,6 +3,8 @@
 # 8 or 4 images per workgroup, VSIQ_EXP_PCT_NB, a temporary switch) against the channel
 # columns (1, default) at 10x10 and 20x20, kernel-trace medians by grid, twice; the K6
 # module tests first (they cover the tile form).
+# (Record of a session: the tile form and VSIQ_TUNE_PC_PACKED 3 were removed after it; the
+# script fails on the knob now.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out

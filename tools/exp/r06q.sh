@@ -2,6 +2,7 @@
 # round 6 session q: K6 axis 0 with g by LDS-DMA (VSIQ_EXP_PCR_GLDS=1, a temporary switch)
 # against the split-load form: the K6 module tests under the LDS-DMA form, the C2 bench's
 # learnable legs twice each way, then the C2 gate sweep's K6 column each way.
+# (Record of a session: the LDS-DMA variant and VSIQ_EXP_PCR_GLDS were removed after it.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
