@@ -21,7 +21,8 @@ def main():
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             acc[(name.split("(")[0][:90], grid // max(wg, 1))].append(dur)
     for (name, wgs), v in sorted(acc.items(), key=lambda kv: (kv[0][0], kv[0][1])):
-        print(f"{name:90s} wgs={wgs:7d} n={len(v):6d} med={statistics.median(v):8.2f} min={min(v):8.2f}")
+        print(f"{name:90s} wgs={wgs:7d} n={len(v):6d} med={statistics.median(v):8.2f} min={min(v):8.2f} "
+              f"sum={sum(v):10.1f}")
 
 
 if __name__ == "__main__":

@@ -23,7 +23,8 @@
 //          as a double, the sum of (double(v) - mean)^2 in f64, / (n - 1), sqrt, rounded
 //          to fp32 once.  The f64 sum's order differs from torch's parallel_reduce, which
 //          moves the result ~1e-16 relative: the fp32 rounding absorbs it except when the
-//          value straddles a rounding boundary.  kStdParts fixed-order partials, one fold.
+//          value straddles a rounding boundary.  kStdParts fixed-order partials (16-B
+//          loads, kStdU groups in flight per lane), one fold.
 // Both sums (|act(x)| and act(x)) ride the same pass.  HBM: 4 B / element read; the
 // level-1 nodes (8 B per 256 elements at V = 8) are written once and read once.
 #include "mean_cascade.cuh"
@@ -206,19 +207,40 @@ __global__ __launch_bounds__(64) void k_mean_final(const MAcc *csum, MeanLay m, 
   }
 }
 
-constexpr int kStdParts = 512;
+constexpr int kStdParts = 1024;
+constexpr int kStdU = 4;   // groups of 4 elements in flight per lane per iteration
 
+// one element's squared deviation in f64 (0 for lanes past the end)
 template <int ACT>
+__device__ __forceinline__ double std_term(float v, int64_t e, bool valid, double m, const SiluLay &L) {
+  const double d = (double)mean_elem<ACT>(v, e, L).s - m;
+  return valid ? d * d : 0.0;
+}
+
+// kStdParts workgroups stride over the tensor's 4-element groups, kStdU groups per lane
+// per iteration (all loads issued before the arithmetic); VEC: 16-B aligned x
+template <int ACT, bool VEC>
 __global__ __launch_bounds__(256) void k_std_part(const float *__restrict__ x, int64_t n,
                                                   const double *__restrict__ stats, SiluLay L,
                                                   double *__restrict__ part) {
   __shared__ double s_w[256 / kWave];
   const double m = stats[VSIQ_ST_MEAN];   // torch: self.mean().item<double>()
-  double acc = 0.0;
+  const int64_t ng = cdiv(n, 4);
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const double d = (double)mean_elem<ACT>(x[i], i, L).s - m;
-    acc += d * d;
+  double acc = 0.0;
+  for (int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x; g0 < ng; g0 += kStdU * stride) {
+    f4 v[kStdU];
+#pragma unroll
+    for (int u = 0; u < kStdU; ++u) v[u] = load_group_c<VEC, true>(x, g0 + u * stride, ng, n);
+#pragma unroll
+    for (int u = 0; u < kStdU; ++u) {
+      const int64_t gi = g0 + u * stride;
+      const int nv = gi < ng ? valid_in_group(gi, n) : 0;
+      acc += std_term<ACT>(v[u].x, 4 * gi, nv > 0, m, L);
+      acc += std_term<ACT>(v[u].y, 4 * gi + 1, nv > 1, m, L);
+      acc += std_term<ACT>(v[u].z, 4 * gi + 2, nv > 2, m, L);
+      acc += std_term<ACT>(v[u].w, 4 * gi + 3, nv > 3, m, L);
+    }
   }
   acc = wave_reduce(acc, AddD());
   if (threadIdx.x % kWave == 0) s_w[threadIdx.x / kWave] = acc;
@@ -244,7 +266,10 @@ __global__ __launch_bounds__(64) void k_std_final(const double *__restrict__ par
 
 template <int ACT>
 void launch_std(const float *x, int64_t n, double *stats, const SiluLay &L, double *part, hipStream_t st) {
-  hipLaunchKernelGGL((k_std_part<ACT>), dim3(kStdParts), dim3(256), 0, st, x, n, stats, L, part);
+  if (n % 4 == 0 && aligned16(x))
+    hipLaunchKernelGGL((k_std_part<ACT, true>), dim3(kStdParts), dim3(256), 0, st, x, n, stats, L, part);
+  else
+    hipLaunchKernelGGL((k_std_part<ACT, false>), dim3(kStdParts), dim3(256), 0, st, x, n, stats, L, part);
 }
 
 int64_t tiles_max_of(const MeanLay &m, int64_t n, int V) {
