@@ -82,6 +82,11 @@ constexpr int kMeanScratch = 16 * kMeanMaxLanes + 4 * kMeanMaxLanes + kMeanMaxLa
 template <class LD>
 __host__ __device__ void mean_multi_row_seq(const LD &ld, int64_t size, int lanes, MAcc *out, MAcc *buf) {
   const int w = 4 * lanes;
+  if (size <= 0) {   // no rows: every accumulator stays +0 (the same bits, ~300 LDS ops fewer
+                     // for the one-lane final stage, where rows = threads / (4 V) is 0)
+    for (int c = 0; c < w; ++c) out[c] = MAcc{0.0f, 0.0f};
+    return;
+  }
   const int lp = mean_level_power(size);
   const int64_t step = (int64_t)1 << lp, mask = step - 1;
   MAcc *acc[4] = {buf, buf + 4 * kMeanMaxLanes, buf + 8 * kMeanMaxLanes, buf + 12 * kMeanMaxLanes};
