@@ -252,12 +252,22 @@ __global__ __launch_bounds__(256) void k_std_part(const float *__restrict__ x, i
   }
 }
 
-__global__ __launch_bounds__(64) void k_std_final(const double *__restrict__ part, int parts, int64_t n,
-                                                  double *__restrict__ stats) {
+// kStdParts / 256 independent loads per lane (issued together), then the block's tree
+__global__ __launch_bounds__(256) void k_std_final(const double *__restrict__ part, int64_t n,
+                                                   double *__restrict__ stats) {
+  static_assert(kStdParts % 256 == 0, "k_std_final: whole rows of partials");
+  __shared__ double s_w[256 / kWave];
+  double v[kStdParts / 256];
+#pragma unroll
+  for (int k = 0; k < kStdParts / 256; ++k) v[k] = part[threadIdx.x + 256 * k];
   double t = 0.0;
-  for (int i = threadIdx.x; i < parts; i += 64) t += part[i];
+#pragma unroll
+  for (int k = 0; k < kStdParts / 256; ++k) t += v[k];
   t = wave_reduce(t, AddD());
+  if (threadIdx.x % kWave == 0) s_w[threadIdx.x / kWave] = t;
+  __syncthreads();
   if (threadIdx.x == 0) {
+    for (int w = 1; w < 256 / kWave; ++w) t += s_w[w];
     const double dn = (double)n - 1.0;
     const double var = t / (dn > 0.0 ? dn : 0.0);   // n <= 1: 0 / 0 = NaN, as torch
     stats[VSIQ_ST_STD] = (double)(float)__builtin_sqrt(var);
@@ -369,7 +379,7 @@ int vsiq_torch_mean_f32(const float *x, int64_t n, int act, int vec, int threads
   if (stats) {
     double *part = reinterpret_cast<double *>(a.csum + (m.nchunks > 0 ? m.nchunks : 1));
     VSIQ_ACT(act, launch_std, x, n, stats, a.L, part, st);
-    hipLaunchKernelGGL(k_std_final, dim3(1), dim3(64), 0, st, part, kStdParts, n, stats);
+    hipLaunchKernelGGL(k_std_final, dim3(1), dim3(256), 0, st, part, n, stats);
   }
   return launch_rc();
 }
