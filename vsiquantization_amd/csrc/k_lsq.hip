@@ -21,7 +21,8 @@ __global__ __launch_bounds__(kBlock) void k_lsq_bwd(const float *__restrict__ g,
   f4 o[G];
   // G <= 2 (C4's small one-round layers): the kernel-uniform qparams as scalar loads after
   // the first x / g loads are issued (round 6).  Deeper grids keep them first: the late
-  // loads cost 2 VGPRs there, one wave per SIMD at G = 4 / 8 (C3's K4: 98 VGPRs, 4 waves).
+  // loads cost 2 VGPRs there, one wave per SIMD at G = 4 / 8 (C3's K4: 98 VGPRs, 4 waves),
+  // and measured equal at C3 (profiles/r06/r06x_k4_late_qparams.txt).
   QP p;
   if constexpr (G <= 2) {
     p = lsq_bwd_block<VEC, NT, ZPL, ACT, G>(g, x, n, [&] { return load_qp<true>(src); }, blockIdx.x, c, o, L);
